@@ -1,0 +1,583 @@
+/*
+ * hhmm_api.cpp -- the C ABI of libhhmm.so (include/hhmm.h).
+ *
+ * Host side of the drop-in boundary: validates a request the way Stan's data
+ * block and parameter constraints would (declared bounds such as
+ * `int<lower=1, upper=L> x[T]`, hmm/stan/hmm-multinom.stan:12), sizes the
+ * workspace, moves host arrays to and from the device for the R path
+ * (hhmm_run), and launches the gfx950 kernels (hhmm_kernels.hip).  There is
+ * no CPU compute path: without a gfx950 device every entry point fails with
+ * HHMM_ERR_NO_DEVICE.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hhmm_internal.h"
+
+namespace hhmm {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+/* ---------------- device pool (per device, size-bucketed) ---------------- */
+struct Pool {
+    std::mutex mu;
+    std::map<int, std::multimap<size_t, void *>> free_blocks;
+    std::map<void *, std::pair<int, size_t>> live;
+};
+static Pool &pool()
+{
+    static Pool p;
+    return p;
+}
+
+static void *pool_get(int dev, size_t bytes)
+{
+    if (bytes == 0)
+        bytes = 256;
+    bytes = (bytes + 4095) & ~(size_t)4095;
+    Pool &p = pool();
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        auto &fb = p.free_blocks[dev];
+        auto it = fb.lower_bound(bytes);
+        if (it != fb.end() && it->first <= bytes + bytes / 4) {
+            void *ptr = it->second;
+            p.live[ptr] = {dev, it->first};
+            fb.erase(it);
+            return ptr;
+        }
+    }
+    void *ptr = nullptr;
+    if (hipMalloc(&ptr, bytes) != hipSuccess) {
+        /* release cached blocks of this device and retry once */
+        std::vector<void *> drop;
+        {
+            std::lock_guard<std::mutex> g(p.mu);
+            for (auto &kv : p.free_blocks[dev])
+                drop.push_back(kv.second);
+            p.free_blocks[dev].clear();
+        }
+        for (void *q : drop)
+            hipFree(q);
+        (void)hipGetLastError();
+        if (hipMalloc(&ptr, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+    }
+    std::lock_guard<std::mutex> g(p.mu);
+    p.live[ptr] = {dev, bytes};
+    return ptr;
+}
+
+static void pool_put(void *ptr)
+{
+    if (!ptr)
+        return;
+    Pool &p = pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    auto it = p.live.find(ptr);
+    if (it == p.live.end())
+        return;
+    p.free_blocks[it->second.first].emplace(it->second.second, ptr);
+    p.live.erase(it);
+}
+
+static void pool_release_all()
+{
+    Pool &p = pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    for (auto &dv : p.free_blocks) {
+        hipSetDevice(dv.first);
+        for (auto &kv : dv.second)
+            hipFree(kv.second);
+    }
+    p.free_blocks.clear();
+}
+
+/* ---------------- request description ---------------- */
+
+static bool is_iohmm(int m)
+{
+    return m == HHMM_MODEL_IOHMM_REG || m == HHMM_MODEL_IOHMM_MIX || m == HHMM_MODEL_IOHMM_HMIX ||
+           m == HHMM_MODEL_IOHMM_HMIX_LITE;
+}
+static bool is_discrete(int m)
+{
+    return m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP || m == HHMM_MODEL_TAYAL ||
+           m == HHMM_MODEL_TAYAL_LITE;
+}
+
+/* Outputs each Stan program declares (TP / GQ names), SURVEY.md §2.3. */
+static uint32_t available_outputs(int m)
+{
+    const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
+                        HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA | HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+    switch (m) {
+    case HHMM_MODEL_HMM_GAUSS:
+    case HHMM_MODEL_HMM_MULTINOM:
+    case HHMM_MODEL_HMM_MULTINOM_SEMISUP:
+    case HHMM_MODEL_TAYAL:
+        return fb;
+    case HHMM_MODEL_IOHMM_REG:
+    case HHMM_MODEL_IOHMM_MIX:
+        return fb | HHMM_OUT_OBLIK_TK | HHMM_OUT_LOGA;
+    case HHMM_MODEL_IOHMM_HMIX:
+        return HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_GAMMA |
+               HHMM_OUT_OBLIK_TK | HHMM_OUT_OBLIK_T | HHMM_OUT_LOGA | HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+    case HHMM_MODEL_IOHMM_HMIX_LITE:
+        return HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_OBLIK_TK | HHMM_OUT_OBLIK_T | HHMM_OUT_LOGA;
+    case HHMM_MODEL_TAYAL_LITE:
+        return HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA_OOS | HHMM_OUT_ALPHA_OOS |
+               HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+    default:
+        return 0;
+    }
+}
+
+/* Models with a gfx950 path in this build. */
+static bool device_supported(int m)
+{
+    return m == HHMM_MODEL_HMM_GAUSS || m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ||
+           m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE;
+}
+
+static int64_t npairs(const hhmm_request *r)
+{
+    if (!r)
+        return -1;
+    if (r->data.n_series < 1 || r->draws.n_draws < 1)
+        return -1;
+    if (r->pairing == HHMM_PAIR_ZIP)
+        return r->data.n_series == r->draws.n_draws ? r->data.n_series : -1;
+    if (r->pairing == HHMM_PAIR_GRID)
+        return r->data.n_series * r->draws.n_draws;
+    return -1;
+}
+
+/* One array of the request: where it lives and how many elements. */
+struct ArrayDesc {
+    const void *host;
+    void **dev_slot; /* field in the device copy of the request/result */
+    size_t elems;
+    size_t esize;
+    bool output;
+};
+
+#define REQUIRE(cond, ...)                                                                          \
+    do {                                                                                            \
+        if (!(cond)) {                                                                              \
+            set_error(__VA_ARGS__);                                                                 \
+            return HHMM_ERR_INVALID_ARGUMENT;                                                       \
+        }                                                                                           \
+    } while (0)
+
+static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool host)
+{
+    REQUIRE(r && o, "request and result must be non-NULL");
+    REQUIRE(r->abi_version == HHMM_ABI_VERSION, "abi_version %u != %u", r->abi_version, HHMM_ABI_VERSION);
+    REQUIRE(r->model >= 1 && r->model <= 9, "unknown model id %d", r->model);
+    REQUIRE(r->pairing == HHMM_PAIR_GRID || r->pairing == HHMM_PAIR_ZIP, "unknown pairing %d", r->pairing);
+    const hhmm_data &d = r->data;
+    const hhmm_draws &w = r->draws;
+    REQUIRE(d.n_series >= 1, "n_series must be >= 1");
+    REQUIRE(w.n_draws >= 1, "n_draws must be >= 1");
+    REQUIRE(npairs(r) >= 1, "ZIP pairing needs n_series == n_draws (%lld vs %lld)", (long long)d.n_series,
+            (long long)w.n_draws);
+    REQUIRE(d.T_max >= 1, "T_max must be >= 1 (int<lower=1> T)");
+    REQUIRE(d.K >= 1, "K must be >= 1 (int<lower=1> K)");
+    const int m = r->model;
+    if (is_discrete(m))
+        REQUIRE(d.L >= 1 && d.x_int, "model %d needs L >= 1 and x_int", m);
+    if (m == HHMM_MODEL_HMM_GAUSS || is_iohmm(m))
+        REQUIRE(d.x_real, "model %d needs x_real", m);
+    if (is_iohmm(m))
+        REQUIRE(d.M >= 1 && d.u, "IOHMM needs M >= 1 and u_tm");
+    if (m == HHMM_MODEL_HMM_MULTINOM_SEMISUP)
+        REQUIRE(d.G >= 1 && d.g, "semisup needs G >= 1 and g");
+    if (m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE) {
+        REQUIRE(d.K == 4, "the Tayal model is the K = 4 flattened HHMM (got K = %d)", d.K);
+        REQUIRE(d.sign && w.p_11 && w.A_row && w.phi_k, "tayal needs sign, p_11, A_row, phi_k");
+    }
+    if (m == HHMM_MODEL_TAYAL_LITE)
+        REQUIRE(d.T_oos_max >= 1 && d.x_oos && d.sign_oos, "tayal-lite needs T_oos_max, x_oos, sign_oos");
+    if (m == HHMM_MODEL_HMM_GAUSS)
+        REQUIRE(w.p_1k && w.A_ij && w.mu_k && w.sigma_k, "hmm-gauss needs p_1k, A_ij, mu_k, sigma_k");
+    if (m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP)
+        REQUIRE(w.p_1k && w.A_ij && w.phi_k, "multinomial HMM needs p_1k, A_ij, phi_k");
+    if (m == HHMM_MODEL_IOHMM_REG)
+        REQUIRE(w.p_1k && w.w_km && w.b_km && w.s_k, "iohmm-reg needs p_1k, w_km, b_km, s_k");
+    if (m == HHMM_MODEL_IOHMM_MIX || m == HHMM_MODEL_IOHMM_HMIX || m == HHMM_MODEL_IOHMM_HMIX_LITE)
+        REQUIRE(d.L >= 1 && w.p_1k && w.w_km && w.lambda_kl && w.mu_kl && w.s_kl,
+                "iohmm-mix needs L, p_1k, w_km, lambda_kl, mu_kl, s_kl");
+
+    const uint32_t avail = available_outputs(m);
+    REQUIRE((r->outputs & ~avail) == 0, "outputs 0x%x not declared by model %d (available 0x%x)",
+            r->outputs & ~avail, m, avail);
+    REQUIRE(r->outputs != 0, "no outputs requested");
+    struct {
+        uint32_t bit;
+        const void *ptr;
+        const char *name;
+    } outs[] = {{HHMM_OUT_LOGLIK, o->loglik, "loglik"},
+                {HHMM_OUT_UNALPHA, o->unalpha_tk, "unalpha_tk"},
+                {HHMM_OUT_ALPHA, o->alpha_tk, "alpha_tk"},
+                {HHMM_OUT_UNBETA, o->unbeta_tk, "unbeta_tk"},
+                {HHMM_OUT_BETA, o->beta_tk, "beta_tk"},
+                {HHMM_OUT_UNGAMMA, o->ungamma_tk, "ungamma_tk"},
+                {HHMM_OUT_GAMMA, o->gamma_tk, "gamma_tk"},
+                {HHMM_OUT_ZSTAR, o->zstar_t, "zstar_t"},
+                {HHMM_OUT_LOGP_ZSTAR, o->logp_zstar, "logp_zstar"},
+                {HHMM_OUT_OBLIK_TK, o->oblik_tk, "oblik_tk"},
+                {HHMM_OUT_OBLIK_T, o->oblik_t, "oblik_t"},
+                {HHMM_OUT_FFBS, o->z_ffbs, "z_ffbs"},
+                {HHMM_OUT_ALPHA_OOS, o->alpha_tk_oos, "alpha_tk_oos"},
+                {HHMM_OUT_UNALPHA_OOS, o->unalpha_tk_oos, "unalpha_tk_oos"},
+                {HHMM_OUT_LOGA, o->logA_ij, "logA_ij"}};
+    for (auto &e : outs)
+        REQUIRE(!(r->outputs & e.bit) || e.ptr, "output %s requested but its pointer is NULL", e.name);
+    if (r->outputs & HHMM_OUT_FFBS)
+        REQUIRE(r->ffbs_u, "FFBS needs ffbs_u");
+
+    if (host) {
+        const int64_t N = d.n_series;
+        const int Tm = d.T_max;
+        if (d.T)
+            for (int64_t n = 0; n < N; ++n)
+                REQUIRE(d.T[n] >= 1 && d.T[n] <= Tm, "T[%lld] = %d outside 1..T_max=%d", (long long)n, d.T[n], Tm);
+        auto len = [&](int64_t n) { return d.T ? d.T[n] : Tm; };
+        if (is_discrete(m))
+            for (int64_t n = 0; n < N; ++n)
+                for (int t = 0; t < len(n); ++t) {
+                    const int32_t v = d.x_int[n + N * (int64_t)t];
+                    REQUIRE(v >= 1 && v <= d.L, "x[%lld, %d] = %d outside 1..L=%d", (long long)n, t + 1, v, d.L);
+                }
+        if (m == HHMM_MODEL_HMM_MULTINOM_SEMISUP)
+            for (int64_t n = 0; n < N; ++n)
+                for (int t = 0; t < len(n); ++t) {
+                    const int32_t v = d.g[n + N * (int64_t)t];
+                    REQUIRE(v >= 1 && v <= d.G, "g[%lld, %d] = %d outside 1..G=%d", (long long)n, t + 1, v, d.G);
+                }
+        if (m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE)
+            for (int64_t n = 0; n < N; ++n)
+                for (int t = 0; t < len(n); ++t) {
+                    const int32_t v = d.sign[n + N * (int64_t)t];
+                    REQUIRE(v == 1 || v == 2, "sign[%lld, %d] = %d outside 1..2", (long long)n, t + 1, v);
+                }
+        if (m == HHMM_MODEL_TAYAL_LITE) {
+            for (int64_t n = 0; n < N; ++n) {
+                const int To = d.T_oos ? d.T_oos[n] : d.T_oos_max;
+                REQUIRE(To >= 1 && To <= d.T_oos_max, "T_oos[%lld] = %d outside 1..T_oos_max", (long long)n, To);
+                for (int t = 0; t < To; ++t) {
+                    const int32_t v = d.x_oos[n + N * (int64_t)t];
+                    const int32_t sg = d.sign_oos[n + N * (int64_t)t];
+                    REQUIRE(v >= 1 && v <= d.L, "x_oos[%lld, %d] = %d outside 1..L", (long long)n, t + 1, v);
+                    REQUIRE(sg == 1 || sg == 2, "sign_oos[%lld, %d] = %d outside 1..2", (long long)n, t + 1, sg);
+                }
+            }
+        }
+        if (m == HHMM_MODEL_HMM_GAUSS)
+            for (int64_t i = 0; i < w.n_draws * d.K; ++i)
+                REQUIRE(w.sigma_k[i] > 0.0, "sigma_k must be > 0 (real<lower=0.0001>)");
+    }
+    return HHMM_OK;
+}
+
+/* Element counts of every input / output array the request uses. */
+static void describe(const hhmm_request *r, const hhmm_result *o, hhmm_request *dr, hhmm_result *dq,
+                     std::vector<ArrayDesc> &v)
+{
+    const hhmm_data &d = r->data;
+    const hhmm_draws &w = r->draws;
+    const size_t N = (size_t)d.n_series, S = (size_t)w.n_draws, Tm = (size_t)d.T_max;
+    const size_t To = (size_t)(d.T_oos_max > 0 ? d.T_oos_max : 0);
+    const size_t K = (size_t)d.K, L = (size_t)(d.L > 0 ? d.L : 0), M = (size_t)(d.M > 0 ? d.M : 0);
+    const size_t P = (size_t)npairs(r);
+    const uint32_t out = r->outputs;
+    auto in = [&](const void *h, const void **slot, size_t n, size_t es) {
+        if (h)
+            v.push_back({h, (void **)slot, n, es, false});
+    };
+    auto ou = [&](uint32_t bit, void *h, void **slot, size_t n, size_t es) {
+        if ((out & bit) && h)
+            v.push_back({h, slot, n, es, true});
+        else
+            *slot = nullptr;
+    };
+    in(d.T, (const void **)&dr->data.T, N, 4);
+    in(d.x_int, (const void **)&dr->data.x_int, N * Tm, 4);
+    in(d.x_real, (const void **)&dr->data.x_real, N * Tm, 8);
+    in(d.g, (const void **)&dr->data.g, N * Tm, 4);
+    in(d.sign, (const void **)&dr->data.sign, N * Tm, 4);
+    in(d.u, (const void **)&dr->data.u, N * Tm * M, 8);
+    in(d.T_oos, (const void **)&dr->data.T_oos, N, 4);
+    in(d.x_oos, (const void **)&dr->data.x_oos, N * To, 4);
+    in(d.sign_oos, (const void **)&dr->data.sign_oos, N * To, 4);
+    dr->data.hyperparams = nullptr;
+    in(w.p_1k, (const void **)&dr->draws.p_1k, S * K, 8);
+    in(w.A_ij, (const void **)&dr->draws.A_ij, S * K * K, 8);
+    in(w.phi_k, (const void **)&dr->draws.phi_k, S * K * L, 8);
+    in(w.mu_k, (const void **)&dr->draws.mu_k, S * K, 8);
+    in(w.sigma_k, (const void **)&dr->draws.sigma_k, S * K, 8);
+    in(w.w_km, (const void **)&dr->draws.w_km, S * K * M, 8);
+    in(w.b_km, (const void **)&dr->draws.b_km, S * K * M, 8);
+    in(w.s_k, (const void **)&dr->draws.s_k, S * K, 8);
+    in(w.lambda_kl, (const void **)&dr->draws.lambda_kl, S * K * L, 8);
+    in(w.mu_kl, (const void **)&dr->draws.mu_kl, S * K * L, 8);
+    in(w.s_kl, (const void **)&dr->draws.s_kl, S * K * L, 8);
+    in(w.p_11, (const void **)&dr->draws.p_11, S, 8);
+    in(w.A_row, (const void **)&dr->draws.A_row, S * 4, 8);
+    in(r->ffbs_u, (const void **)&dr->ffbs_u, P * Tm, 8);
+    const size_t Tz = (r->model == HHMM_MODEL_TAYAL_LITE) ? To : Tm;
+    ou(HHMM_OUT_LOGLIK, o->loglik, (void **)&dq->loglik, P, 8);
+    ou(HHMM_OUT_UNALPHA, o->unalpha_tk, (void **)&dq->unalpha_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_ALPHA, o->alpha_tk, (void **)&dq->alpha_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_UNBETA, o->unbeta_tk, (void **)&dq->unbeta_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_BETA, o->beta_tk, (void **)&dq->beta_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_UNGAMMA, o->ungamma_tk, (void **)&dq->ungamma_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_GAMMA, o->gamma_tk, (void **)&dq->gamma_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_ZSTAR, o->zstar_t, (void **)&dq->zstar_t, P * Tz, 4);
+    ou(HHMM_OUT_LOGP_ZSTAR, o->logp_zstar, (void **)&dq->logp_zstar, P, 8);
+    ou(HHMM_OUT_OBLIK_TK, o->oblik_tk, (void **)&dq->oblik_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_OBLIK_T, o->oblik_t, (void **)&dq->oblik_t, P * Tm, 8);
+    ou(HHMM_OUT_FFBS, o->z_ffbs, (void **)&dq->z_ffbs, P * Tm, 4);
+    ou(HHMM_OUT_ALPHA_OOS, o->alpha_tk_oos, (void **)&dq->alpha_tk_oos, P * To * K, 8);
+    ou(HHMM_OUT_UNALPHA_OOS, o->unalpha_tk_oos, (void **)&dq->unalpha_tk_oos, P * To * K, 8);
+    ou(HHMM_OUT_LOGA, o->logA_ij, (void **)&dq->logA_ij, P * Tm * K, 8);
+}
+
+static hhmm_status hip_fail(hipError_t e, const char *what)
+{
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? HHMM_ERR_OUT_OF_MEMORY : HHMM_ERR_HIP;
+}
+
+static hhmm_status check_device()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible: libhhmm has no CPU path (gfx950 required)");
+        return HHMM_ERR_NO_DEVICE;
+    }
+    return HHMM_OK;
+}
+
+} // namespace hhmm
+
+using namespace hhmm;
+
+extern "C" {
+
+const char *hhmm_version(void) { return "hhmm-mi355x 0.1.0 gfx950 abi 1"; }
+
+const char *hhmm_last_error(void) { return g_last_error.c_str(); }
+
+int64_t hhmm_num_pairs(const hhmm_request *req) { return npairs(req); }
+
+hhmm_status hhmm_validate(const hhmm_request *req, const hhmm_result *res, int host_pointers)
+{
+    return validate(req, res, host_pointers != 0);
+}
+
+hhmm_status hhmm_init(int ndev)
+{
+    hhmm_status s = check_device();
+    if (s != HHMM_OK)
+        return s;
+    int n = 0;
+    hipGetDeviceCount(&n);
+    if (ndev > n) {
+        set_error("%d devices requested, %d visible", ndev, n);
+        return HHMM_ERR_NO_DEVICE;
+    }
+    for (int i = 0; i < (ndev > 0 ? ndev : 1); ++i) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, i) != hipSuccess)
+            return hip_fail(hipGetLastError(), "hipGetDeviceProperties");
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            set_error("device %d is %s, this build targets gfx950", i, prop.gcnArchName);
+            return HHMM_ERR_NO_DEVICE;
+        }
+    }
+    return HHMM_OK;
+}
+
+hhmm_status hhmm_shutdown(void)
+{
+    pool_release_all();
+    return HHMM_OK;
+}
+
+hhmm_status hhmm_workspace_size(const hhmm_request *req, size_t *bytes)
+{
+    if (!req || !bytes) {
+        set_error("NULL argument");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    const int64_t P = npairs(req);
+    if (P < 1) {
+        set_error("request describes no pairs");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    *bytes = workspace_bytes(req->model, req->data.K, req->data.T_max, req->data.T_oos_max, P, req->outputs);
+    return HHMM_OK;
+}
+
+hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res, void *workspace, size_t workspace_bytes_,
+                            void *stream)
+{
+    hhmm_status s = validate(req, res, false);
+    if (s != HHMM_OK)
+        return s;
+    if (!device_supported(req->model)) {
+        set_error("model %d has no gfx950 path in this build", req->model);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    if ((s = check_device()) != HHMM_OK)
+        return s;
+    size_t need = 0;
+    hhmm_workspace_size(req, &need);
+    if (workspace_bytes_ < need || (!workspace && need > 256)) {
+        set_error("workspace of %zu bytes < %zu required", workspace_bytes_, need);
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    return launch_all(req, res, npairs(req), workspace, (hipStream_t)stream);
+}
+
+hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
+{
+    hhmm_status s = validate(req, res, true);
+    if (s != HHMM_OK)
+        return s;
+    if (!device_supported(req->model)) {
+        set_error("model %d has no gfx950 path in this build", req->model);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    if ((s = check_device()) != HHMM_OK)
+        return s;
+    int dev = req->device;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess)
+            return hip_fail(hipGetLastError(), "hipGetDevice");
+    }
+    hipError_t e = hipSetDevice(dev);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipSetDevice");
+
+    const int64_t P = npairs(req);
+    hhmm_request dreq = *req;
+    hhmm_result dres = *res;
+    /* pair_status is always produced on the device to decide the return code */
+    std::vector<int32_t> status_host;
+    int32_t *status_user = res->pair_status;
+    dres.pair_status = nullptr;
+
+    std::vector<ArrayDesc> arrays;
+    describe(req, res, &dreq, &dres, arrays);
+    const bool ragged = req->data.T != nullptr || req->data.T_oos != nullptr;
+
+    std::vector<void *> owned;
+    auto cleanup = [&]() {
+        for (void *p : owned)
+            pool_put(p);
+    };
+    for (auto &a : arrays) {
+        void *dp = pool_get(dev, a.elems * a.esize);
+        if (!dp) {
+            cleanup();
+            set_error("device allocation of %zu bytes failed", a.elems * a.esize);
+            return HHMM_ERR_OUT_OF_MEMORY;
+        }
+        owned.push_back(dp);
+        *a.dev_slot = dp;
+        /* inputs always; outputs too when padded steps must round-trip untouched */
+        if (!a.output || ragged) {
+            e = hipMemcpy(dp, a.host, a.elems * a.esize, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                cleanup();
+                return hip_fail(e, "hipMemcpy H2D");
+            }
+        }
+    }
+    void *dstatus = pool_get(dev, (size_t)P * sizeof(int32_t));
+    if (!dstatus) {
+        cleanup();
+        set_error("device allocation failed (pair_status)");
+        return HHMM_ERR_OUT_OF_MEMORY;
+    }
+    owned.push_back(dstatus);
+    hipMemset(dstatus, 0, (size_t)P * sizeof(int32_t));
+    dres.pair_status = (int32_t *)dstatus;
+
+    size_t wsb = workspace_bytes(req->model, req->data.K, req->data.T_max, req->data.T_oos_max, P, req->outputs);
+    void *ws = pool_get(dev, wsb);
+    if (!ws) {
+        cleanup();
+        set_error("workspace allocation of %zu bytes failed", wsb);
+        return HHMM_ERR_OUT_OF_MEMORY;
+    }
+    owned.push_back(ws);
+
+    s = launch_all(&dreq, &dres, P, ws, nullptr);
+    if (s != HHMM_OK) {
+        cleanup();
+        return s;
+    }
+    e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        cleanup();
+        return hip_fail(e, "kernel execution");
+    }
+    for (auto &a : arrays) {
+        if (!a.output)
+            continue;
+        e = hipMemcpy((void *)a.host, *a.dev_slot, a.elems * a.esize, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            cleanup();
+            return hip_fail(e, "hipMemcpy D2H");
+        }
+    }
+    status_host.resize((size_t)P);
+    e = hipMemcpy(status_host.data(), dstatus, (size_t)P * sizeof(int32_t), hipMemcpyDeviceToHost);
+    cleanup();
+    if (e != hipSuccess)
+        return hip_fail(e, "hipMemcpy D2H (status)");
+    int64_t failures = 0;
+    for (int64_t p = 0; p < P; ++p)
+        failures += status_host[(size_t)p] != 0;
+    if (status_user)
+        memcpy(status_user, status_host.data(), (size_t)P * sizeof(int32_t));
+    if (failures) {
+        set_error("%lld pair(s) hit an unset Viterbi back-pointer (Stan would throw)", (long long)failures);
+        return HHMM_WARN_PAIR_FAILURES;
+    }
+    return HHMM_OK;
+}
+
+hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n)
+{
+    hhmm_status s = check_device();
+    if (s != HHMM_OK)
+        return s;
+    return selftest_cr_log(in, out, n);
+}
+
+} /* extern "C" */

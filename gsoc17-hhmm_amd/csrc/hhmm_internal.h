@@ -1,0 +1,75 @@
+/*
+ * hhmm_internal.h -- declarations shared by the host API (hhmm_api.cpp) and
+ * the gfx950 kernels (hhmm_kernels.hip).  Not part of the public ABI.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hhmm.h"
+
+namespace hhmm {
+
+/* Everything one launch needs, by value in the kernel argument segment.
+ * All pointers are device pointers; layouts as in include/hhmm.h. */
+struct DevArgs {
+    int64_t P;          /* pairs */
+    int64_t N;          /* series */
+    int64_t S;          /* draws */
+    int32_t pairing;    /* HHMM_PAIR_GRID / ZIP */
+    int32_t model;
+    int32_t K, L, M;
+    int32_t Tmax;       /* padded extent of the time axis of the data arrays in use */
+    int32_t Tout;       /* padded extent of the time axis of the [P,T,K] outputs in use */
+    uint32_t outputs;
+    /* series data (already switched to the OOS arrays for a tayal-lite OOS pass) */
+    const int32_t *T;
+    const int32_t *x;
+    const double *xr;
+    const int32_t *g;
+    const int32_t *sign;
+    const double *u;
+    /* draws */
+    const double *p_1k, *A_ij, *phi_k, *mu_k, *sigma_k;
+    const double *w_km, *b_km, *s_k, *lambda_kl, *mu_kl, *s_kl;
+    const double *p_11, *A_row;
+    /* outputs */
+    double *loglik;
+    double *unalpha, *alpha, *unbeta, *beta, *ungamma, *gamma;
+    int32_t *zstar;
+    double *logp_zstar;
+    int32_t *pair_status;
+    /* workspace */
+    double *ckpt;       /* [nchunk][K][P] forward checkpoints */
+    double *ckpt_ls;    /* [nchunk][P]    log scale at each checkpoint */
+    uint32_t *bp;       /* [nword][P]     packed Viterbi back-pointers */
+};
+
+/* Time steps between forward checkpoints kept for the backward sweep. */
+constexpr int fb_chunk(int K) { return K <= 4 ? 8 : 4; }
+
+/* Viterbi back-pointer packing: bits per state, bits per step, steps per word. */
+constexpr int bp_bits(int K) { return K <= 2 ? 1 : (K <= 4 ? 2 : (K <= 8 ? 3 : 4)); }
+constexpr int bp_steps_per_word(int K) { return 32 / (K * bp_bits(K)); }
+
+constexpr int kMaxK = 8;
+constexpr int kBlock = 256;
+constexpr size_t kLdsLimit = 160 * 1024;
+
+/* Bytes of workspace the kernels need for this launch shape. */
+size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs);
+
+/* Carves the workspace into DevArgs pointers. */
+void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos);
+
+/* Launches every kernel the request needs on `stream` (device pointers). */
+hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws,
+                       hipStream_t stream);
+
+/* Device self-test of the correctly rounded log (host arrays). */
+hhmm_status selftest_cr_log(const double *in, double *out, int64_t n);
+
+void set_error(const char *fmt, ...);
+
+} // namespace hhmm

@@ -1,0 +1,1099 @@
+/*
+ * hhmm_kernels.hip -- gfx950 kernels for the HMM-family path.
+ *
+ * Layout in HBM (include/hhmm.h): every array is pair-/series-/draw-fastest,
+ * so one wave of 64 lanes = 64 consecutive pairs reads and writes 64
+ * consecutive elements per (t, k): every global access below is a fully
+ * coalesced 256 B (int32) or 512 B (fp64) wave transaction.
+ *
+ * One LANE owns one (series, draw) PAIR for the whole sequence; the K-state
+ * vectors live in registers.  Per-pair emission tables (phi_k and log phi_k,
+ * K*L doubles) live in LDS, one slab per wave, laid out
+ *     slab[(l * KP + kp) * 64 + lane]  (double2: states 2kp, 2kp+1)
+ * so a 16-lane ds_read_b128 group touches 16 consecutive 16-B slots = all 64
+ * banks once: conflict-free for any per-lane symbol.
+ *
+ * Kernels:
+ *   fb_kernel      A2/A1 emissions, A6 forward + loglik, A7 alpha, A8 backward,
+ *                  A9 gamma, A12/A13 masks.  LINEAR-space scaled recursion
+ *                  (K^2 FMAs + a power-of-two rescale per step; no exp/log in
+ *                  the loop); forward checkpoints every C steps, recomputed
+ *                  chunk by chunk in the backward sweep.  Tolerance 1e-9 rel.
+ *   viterbi_kernel A11 max-plus recursion in LOG space with exactly the
+ *                  reference's operation order and tie rules, log tables from
+ *                  the correctly rounded hhmm_cr_log (bit-identical to the
+ *                  oracle); back-pointers packed 2 bits/state to HBM, backtrack
+ *                  in the same kernel.  Bit-exact.
+ * Build with -ffp-contract=off: the Viterbi sums must round exactly as written.
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "hhmm_internal.h"
+
+#define HHMM_MATH_FN static __device__ __forceinline__
+#define HHMM_MATH_TABLE static __constant__
+#include "hhmm_crmath.h"
+
+namespace hhmm {
+
+constexpr double kLn2 = 0x1.62e42fefa39efp-1;
+
+/* ------------------------------------------------------------------ */
+/* Small device helpers                                                  */
+/* ------------------------------------------------------------------ */
+
+__device__ __forceinline__ double dev_nan() { return __builtin_nan(""); }
+__device__ __forceinline__ double dev_ninf() { return -__builtin_inf(); }
+
+/* max(std::vector<double>) of Stan Math on x86-64 (Eigen SSE2 maxCoeff):
+ * identical to stan_max_vec in oracle/hhmm_oracle.c.  NaN-aware order. */
+__device__ __forceinline__ double sse_max(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double std_max(double a, double b) { return a < b ? b : a; }
+template <int K>
+__device__ __forceinline__ double stan_max_vec(const double (&d)[K])
+{
+    if constexpr (K < 2) {
+        return d[0];
+    } else {
+        constexpr int aligned = K & ~1, aligned2 = K & ~3;
+        double r0a = d[0], r0b = d[1];
+        if constexpr (aligned > 2) {
+            double r1a = d[2], r1b = d[3];
+#pragma unroll
+            for (int i = 4; i < aligned2; i += 4) {
+                r0a = sse_max(r0a, d[i]);
+                r0b = sse_max(r0b, d[i + 1]);
+                r1a = sse_max(r1a, d[i + 2]);
+                r1b = sse_max(r1b, d[i + 3]);
+            }
+            r0a = sse_max(r0a, r1a);
+            r0b = sse_max(r0b, r1b);
+            if constexpr (aligned > aligned2) {
+                r0a = sse_max(r0a, d[aligned2]);
+                r0b = sse_max(r0b, d[aligned2 + 1]);
+            }
+        }
+        double res = sse_max(r0a, r0b);
+#pragma unroll
+        for (int i = aligned; i < K; ++i)
+            res = std_max(res, d[i]);
+        return res;
+    }
+}
+
+/* Keep a K-vector's largest entry in [0.5, 1): scale by 2^-e, count e. */
+template <int K>
+__device__ __forceinline__ void rescale(double (&v)[K], int &ex)
+{
+    double mx = v[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k)
+        mx = fmax(mx, v[k]);
+    const int e = (mx > 0.0) ? __builtin_amdgcn_frexp_exp(mx) : 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        v[k] = ldexp(v[k], -e);
+    ex += e;
+}
+
+/* hmm-multinom-semisup.stan:42 -- j0 is 0-based */
+__device__ __forceinline__ bool semisup_mask(int g, int j0)
+{
+    const int j = j0 + 1;
+    return (g == 1 && (j == 1 || j == 4)) || (g == 2 && (j == 2 || j == 3));
+}
+/* hhmm-tayal2009.stan:62 / :109 / :144 */
+__device__ __forceinline__ bool tayal_pred(int s, int j0)
+{
+    const int j = j0 + 1;
+    return (s == 1 && (j == 2 || j == 3)) || (s == 2 && (j == 1 || j == 4));
+}
+/* hhmm-tayal2009.stan:51 */
+__device__ __forceinline__ bool tayal_init_pred(int s, int j0)
+{
+    const int j = j0 + 1;
+    return (s == 1 && j == 3) || (s == 2 && j == 1);
+}
+
+template <int MODEL>
+struct ModelTraits {
+    static constexpr bool kGauss = (MODEL == HHMM_MODEL_HMM_GAUSS);
+    static constexpr bool kSemisup = (MODEL == HHMM_MODEL_HMM_MULTINOM_SEMISUP);
+    static constexpr bool kTayal = (MODEL == HHMM_MODEL_TAYAL || MODEL == HHMM_MODEL_TAYAL_LITE);
+    static constexpr bool kDiscrete = !kGauss;
+    static constexpr bool kAux = kSemisup || kTayal; /* needs g[] or sign[] per step */
+};
+
+/* One observation step of a series. */
+struct Obs {
+    int x;     /* symbol 1..L (discrete models) */
+    int aux;   /* g (semisup) or sign (tayal) */
+    double xr; /* real observation (gauss) */
+};
+
+template <int MODEL, bool AUX>
+__device__ __forceinline__ Obs load_obs(const DevArgs &a, const int32_t *xb, const int32_t *ab,
+                                        const double *rb, int64_t off)
+{
+    Obs o;
+    o.x = 1;
+    o.aux = 0;
+    o.xr = 0.0;
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        o.x = xb[off];
+    if constexpr (AUX)
+        o.aux = ab[off];
+    if constexpr (ModelTraits<MODEL>::kGauss)
+        o.xr = rb[off];
+    return o;
+}
+
+/* Loads the C observations of chunk [t0, t0+C) (clamped to the lane's length). */
+template <int MODEL, int C, bool AUX = ModelTraits<MODEL>::kAux>
+__device__ __forceinline__ void load_chunk(Obs (&dst)[C], const DevArgs &a, const int32_t *xb,
+                                           const int32_t *ab, const double *rb, int t0, int Tp)
+{
+#pragma unroll
+    for (int u = 0; u < C; ++u) {
+        const int t = t0 + u;
+        if (t < Tp && t >= 0)
+            dst[u] = load_obs<MODEL, AUX>(a, xb, ab, rb, (int64_t)t * a.N);
+        else {
+            dst[u].x = 1;
+            dst[u].aux = 0;
+            dst[u].xr = 0.0;
+        }
+    }
+}
+
+/* Per-pair parameters held in registers. */
+template <int MODEL, int K>
+struct PairParams {
+    double A[K][K];  /* probability (FB) or log (Viterbi) */
+    double p[K];
+    double mu[K], isig[K], lsig[K], c0[K]; /* gauss: 1/sigma, log sigma, NEG_LOG_SQRT_TWO_PI - log sigma */
+};
+
+template <int K>
+__device__ __forceinline__ double draw1(const double *arr, const DevArgs &a, int64_t d, int k)
+{
+    return arr[d + a.S * (int64_t)k];
+}
+template <int K>
+__device__ __forceinline__ double draw2(const double *arr, const DevArgs &a, int64_t d, int i, int j, int I)
+{
+    return arr[d + a.S * ((int64_t)i + (int64_t)I * j)];
+}
+
+/* Loads p_1k, A_ij (Tayal: expands p_11 / A_row, hhmm-tayal2009.stan:30-44)
+ * and the Gaussian constants.  LOG = true puts log A in params.A. */
+template <int MODEL, int K, bool LOG>
+__device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevArgs &a, int64_t d)
+{
+    if constexpr (ModelTraits<MODEL>::kTayal) {
+        static_assert(K == 4, "tayal is a K = 4 model");
+        const double p11 = a.p_11[d];
+        const double r00 = a.A_row[d + a.S * 0], r10 = a.A_row[d + a.S * 1];
+        const double r01 = a.A_row[d + a.S * 2], r11 = a.A_row[d + a.S * 3];
+        double A[4][4] = {{0, r00, r01, 0}, {1, 0, 0, 0}, {r10, 0, 0, r11}, {0, 0, 1, 0}};
+        pp.p[0] = p11;
+        pp.p[1] = 0;
+        pp.p[2] = 1 - p11;
+        pp.p[3] = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                pp.A[i][j] = LOG ? hhmm_cr_log(A[i][j]) : A[i][j];
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            pp.p[k] = draw1<K>(a.p_1k, a, d, k);
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const double v = draw2<K>(a.A_ij, a, d, i, j, K);
+                pp.A[i][j] = LOG ? hhmm_cr_log(v) : v;
+            }
+    }
+    if constexpr (ModelTraits<MODEL>::kGauss) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double sg = draw1<K>(a.sigma_k, a, d, k);
+            pp.mu[k] = draw1<K>(a.mu_k, a, d, k);
+            pp.isig[k] = 1.0 / sg;
+            pp.lsig[k] = hhmm_cr_log(sg);
+            pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - pp.lsig[k];
+        }
+    }
+}
+
+/* Fills this lane's LDS slab with phi_k (LOG: log phi_k). */
+template <int K, bool LOG>
+__device__ __forceinline__ void fill_table(double2 *slab, const DevArgs &a, int64_t d)
+{
+    constexpr int KP = (K + 1) / 2;
+    for (int l = 0; l < a.L; ++l) {
+#pragma unroll
+        for (int kp = 0; kp < KP; ++kp) {
+            double v0 = draw2<K>(a.phi_k, a, d, 2 * kp, l, K);
+            double v1 = (2 * kp + 1 < K) ? draw2<K>(a.phi_k, a, d, 2 * kp + 1, l, K) : 0.0;
+            if (LOG) {
+                v0 = hhmm_cr_log(v0);
+                v1 = hhmm_cr_log(v1);
+            }
+            slab[(l * KP + kp) * 64] = make_double2(v0, v1);
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void read_table(const double2 *slab, int x, int L, double (&e)[K])
+{
+    constexpr int KP = (K + 1) / 2;
+    const int row = min(max(x, 1), L) - 1;
+    const double2 *r = slab + row * KP * 64;
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+        const double2 v = r[kp * 64];
+        e[2 * kp] = v.x;
+        if (2 * kp + 1 < K)
+            e[2 * kp + 1] = v.y;
+    }
+}
+
+/* Stan's scalar normal_lpdf(y | mu_j, sigma_j) with cached c0 = C - log(sigma),
+ * isig = 1/sigma: ((C - log sigma) + (-0.5 * z*z)), z = (y - mu) * isig. */
+template <int MODEL, int K>
+__device__ __forceinline__ double gauss_lpdf(const PairParams<MODEL, K> &pp, double y, int j)
+{
+    const double z = (y - pp.mu[j]) * pp.isig[j];
+    const double z2 = z * z;
+    return pp.c0[j] + (-0.5 * z2);
+}
+
+/* Emission probabilities of one step for the linear-space filter.  Gaussian
+ * densities are divided by their max over states (added to the log scale). */
+template <int MODEL, int K>
+__device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const double2 *slab, int L,
+                                          const Obs &o, double (&e)[K], double &lsc)
+{
+    if constexpr (ModelTraits<MODEL>::kGauss) {
+        double lp[K];
+        double m = dev_ninf();
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            lp[j] = gauss_lpdf<MODEL, K>(pp, o.xr, j);
+            m = fmax(m, lp[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            e[j] = exp(lp[j] - m);
+        lsc += m;
+    } else {
+        read_table<K>(slab, o.x, L, e);
+    }
+}
+
+/* alpha_t = e_t .* (alpha_{t-1} M_t), with the model's transition masks. */
+template <int MODEL, int K>
+__device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL, K> &pp,
+                                         const double (&e)[K], const Obs &o, int &ex)
+{
+    double s[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double acc = al[0] * pp.A[0][j];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            acc = fma(al[i], pp.A[i][j], acc);
+        s[j] = acc;
+    }
+    if constexpr (ModelTraits<MODEL>::kAux) {
+        double tot = al[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            tot += al[i];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            bool on;
+            if constexpr (ModelTraits<MODEL>::kSemisup)
+                on = semisup_mask(o.aux, j);
+            else
+                on = tayal_pred(o.aux, j);
+            s[j] = on ? s[j] : tot;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        al[j] = s[j] * e[j];
+    rescale<K>(al, ex);
+}
+
+/* beta_{t-1} from beta_t and step t's emission / masks. */
+template <int MODEL, int K>
+__device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL, K> &pp,
+                                         const double (&e)[K], const Obs &o, int &ex)
+{
+    double b[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        b[i] = e[i] * be[i];
+    double s[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double acc = pp.A[j][0] * b[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            acc = fma(pp.A[j][i], b[i], acc);
+        s[j] = acc;
+    }
+    if constexpr (ModelTraits<MODEL>::kTayal) { /* predicate on the PREVIOUS state j (Q6) */
+        double tot = b[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            tot += b[i];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            s[j] = tayal_pred(o.aux, j) ? s[j] : tot;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        be[j] = s[j];
+    rescale<K>(be, ex);
+}
+
+/* alpha_1 (t = 0). */
+template <int MODEL, int K>
+__device__ __forceinline__ void fwd_init(double (&al)[K], const PairParams<MODEL, K> &pp,
+                                         const double2 *slab, int L, const Obs &o, double &lsc, int &ex)
+{
+    if constexpr (ModelTraits<MODEL>::kGauss) {
+        /* hmm.stan:30 -- log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k) (Q2) */
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double z = (o.xr - pp.mu[k]) * pp.isig[k];
+            const double z2 = z * z;
+            s += HHMM_NEG_LOG_SQRT_TWO_PI;
+            s -= pp.lsig[k];
+            s += -0.5 * z2;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            al[k] = pp.p[k];
+        lsc += s;
+    } else {
+        double e[K];
+        read_table<K>(slab, o.x, L, e);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if constexpr (ModelTraits<MODEL>::kTayal)
+                al[k] = tayal_init_pred(o.aux, k) ? e[k] * pp.p[k] : e[k];
+            else
+                al[k] = pp.p[k] * e[k];
+        }
+    }
+    rescale<K>(al, ex);
+}
+
+__device__ __forceinline__ void pair_coords(const DevArgs &a, int64_t p, int64_t &n, int64_t &d)
+{
+    if (a.pairing == HHMM_PAIR_ZIP) {
+        n = p;
+        d = p;
+    } else {
+        n = p / a.S;
+        d = p - n * a.S;
+    }
+}
+
+__device__ __forceinline__ int pair_len(const DevArgs &a, int64_t n)
+{
+    int Tp = a.T ? a.T[n] : a.Tmax;
+    return min(max(Tp, 1), a.Tmax);
+}
+
+/* ------------------------------------------------------------------ */
+/* Forward / backward / posteriors                                       */
+/* ------------------------------------------------------------------ */
+
+template <int K>
+__device__ __forceinline__ void store_tk(double *out, const DevArgs &a, int64_t p, int t, const double (&v)[K])
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        out[p + a.P * ((int64_t)t + (int64_t)a.Tout * k)] = v[k];
+}
+
+/* Writes the forward-side outputs of step t (alpha, unalpha). */
+template <int K>
+__device__ __forceinline__ void emit_alpha(const DevArgs &a, int64_t p, int t, const double (&al)[K], double lsc)
+{
+    if ((a.outputs & HHMM_OUT_ALPHA) && a.alpha) {
+        double s = al[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k)
+            s += al[k];
+        const double r = 1.0 / s;
+        double v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            v[k] = al[k] * r;
+        store_tk<K>(a.alpha, a, p, t, v);
+    }
+    if ((a.outputs & HHMM_OUT_UNALPHA) && a.unalpha) {
+        double v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            v[k] = log(al[k]) + lsc;
+        store_tk<K>(a.unalpha, a, p, t, v);
+    }
+}
+
+/* FWD_ONLY: forward pass writing alpha / unalpha / loglik (tayal-lite, or
+ * when no backward-side output is requested).  FULL: track the per-step log
+ * scale (needed for unalpha / unbeta). */
+template <int MODEL, int K, bool FWD_ONLY, bool FULL>
+__global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
+{
+    constexpr int C = fb_chunk(K);
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.P)
+        return;
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    constexpr int KP = (K + 1) / 2;
+    double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+
+    PairParams<MODEL, K> pp;
+    load_params<MODEL, K, false>(pp, a, d);
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        fill_table<K, false>(slab, a, d);
+
+    const int32_t *xb = a.x ? a.x + n : nullptr;
+    const int32_t *ab = nullptr;
+    if constexpr (ModelTraits<MODEL>::kSemisup)
+        ab = a.g + n;
+    if constexpr (ModelTraits<MODEL>::kTayal)
+        ab = a.sign + n;
+    const double *rb = a.xr ? a.xr + n : nullptr;
+
+    /* ---- forward sweep ---- */
+    double al[K];
+    double lsc = 0.0; /* log scale excluding the binary exponent */
+    int ex = 0;       /* sum of binary exponents removed */
+    Obs cur[C];
+    load_chunk<MODEL, C>(cur, a, xb, ab, rb, 0, Tp);
+    const int nchunk = (Tp + C - 1) / C;
+    for (int c = 0; c < nchunk; ++c) {
+        const int t0 = c * C;
+        Obs nxt[C];
+        load_chunk<MODEL, C>(nxt, a, xb, ab, rb, t0 + C, Tp);
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+            const int t = t0 + u;
+            if (t < Tp) {
+                if (u == 0 && c == 0) {
+                    fwd_init<MODEL, K>(al, pp, slab, a.L, cur[0], lsc, ex);
+                } else {
+                    double e[K];
+                    emit_prob<MODEL, K>(pp, slab, a.L, cur[u], e, lsc);
+                    fwd_step<MODEL, K>(al, pp, e, cur[u], ex);
+                }
+                if constexpr (FWD_ONLY) {
+                    emit_alpha<K>(a, p, t, al, lsc + kLn2 * ex);
+                } else if (u == 0) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        a.ckpt[p + a.P * ((int64_t)c * K + k)] = al[k];
+                    a.ckpt_ls[p + a.P * (int64_t)c] = lsc + kLn2 * ex;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < C; ++u)
+            cur[u] = nxt[u];
+    }
+    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik) {
+        double s = al[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k)
+            s += al[k];
+        a.loglik[p] = log(s) + (lsc + kLn2 * ex);
+    }
+    if constexpr (FWD_ONLY)
+        return;
+
+    /* ---- backward sweep: recompute each chunk's alphas from its checkpoint ---- */
+    const bool want_alpha = (a.outputs & (HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) != 0;
+    const bool want_beta = (a.outputs & (HHMM_OUT_BETA | HHMM_OUT_UNBETA)) != 0;
+    const bool want_gamma = (a.outputs & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) != 0;
+    double be[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        be[k] = 1.0;
+    double blsc = 0.0;
+    int bex = 0;
+    load_chunk<MODEL, C>(cur, a, xb, ab, rb, (nchunk - 1) * C, Tp);
+    for (int c = nchunk - 1; c >= 0; --c) {
+        const int t0 = c * C;
+        Obs nxt[C];
+        load_chunk<MODEL, C>(nxt, a, xb, ab, rb, t0 - C, Tp);
+        double abuf[C][K];
+        double lsbuf[FULL ? C : 1];
+        int exbuf = 0;
+        double ls0 = a.ckpt_ls[p + a.P * (int64_t)c];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            abuf[0][k] = a.ckpt[p + a.P * ((int64_t)c * K + k)];
+        if constexpr (FULL)
+            lsbuf[0] = ls0;
+        double lsacc = 0.0;
+#pragma unroll
+        for (int u = 1; u < C; ++u) {
+            if (t0 + u < Tp) {
+                double e[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    abuf[u][k] = abuf[u - 1][k];
+                emit_prob<MODEL, K>(pp, slab, a.L, cur[u], e, lsacc);
+                fwd_step<MODEL, K>(abuf[u], pp, e, cur[u], exbuf);
+                if constexpr (FULL)
+                    lsbuf[u] = ls0 + (lsacc + kLn2 * exbuf);
+            }
+        }
+#pragma unroll
+        for (int u = C - 1; u >= 0; --u) {
+            const int t = t0 + u;
+            if (t < Tp) {
+                double lsa = 0.0;
+                if constexpr (FULL)
+                    lsa = lsbuf[u];
+                if (want_alpha)
+                    emit_alpha<K>(a, p, t, abuf[u], lsa);
+                double sb = be[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k)
+                    sb += be[k];
+                if (want_beta) {
+                    if ((a.outputs & HHMM_OUT_BETA) && a.beta) {
+                        const double r = 1.0 / sb;
+                        double v[K];
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            v[k] = be[k] * r;
+                        store_tk<K>(a.beta, a, p, t, v);
+                    }
+                    if ((a.outputs & HHMM_OUT_UNBETA) && a.unbeta) {
+                        /* unbeta_tk[T] = 1 (Q1): every unbeta carries +1 */
+                        double v[K];
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            v[k] = (log(be[k]) + (blsc + kLn2 * bex)) + 1.0;
+                        store_tk<K>(a.unbeta, a, p, t, v);
+                    }
+                }
+                if (want_gamma) {
+                    double sa = abuf[u][0];
+#pragma unroll
+                    for (int k = 1; k < K; ++k)
+                        sa += abuf[u][k];
+                    const double ra = 1.0 / sa, rb2 = 1.0 / sb;
+                    double ug[K];
+                    double sg = 0.0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        ug[k] = (abuf[u][k] * ra) * (be[k] * rb2);
+                        sg += ug[k];
+                    }
+                    if ((a.outputs & HHMM_OUT_UNGAMMA) && a.ungamma)
+                        store_tk<K>(a.ungamma, a, p, t, ug);
+                    if ((a.outputs & HHMM_OUT_GAMMA) && a.gamma) {
+                        const double rg = 1.0 / sg;
+                        double v[K];
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            v[k] = ug[k] * rg;
+                        store_tk<K>(a.gamma, a, p, t, v);
+                    }
+                }
+                if (t > 0) {
+                    double e[K];
+                    emit_prob<MODEL, K>(pp, slab, a.L, cur[u], e, blsc);
+                    bwd_step<MODEL, K>(be, pp, e, cur[u], bex);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < C; ++u)
+            cur[u] = nxt[u];
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Viterbi                                                                */
+/* ------------------------------------------------------------------ */
+
+/* Log emission of state j at one step, bit-identical to the reference. */
+template <int MODEL, int K>
+__device__ __forceinline__ void emit_log(const PairParams<MODEL, K> &pp, const double2 *slab, int L,
+                                         const Obs &o, double (&le)[K])
+{
+    if constexpr (ModelTraits<MODEL>::kGauss) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            le[j] = gauss_lpdf<MODEL, K>(pp, o.xr, j);
+    } else {
+        read_table<K>(slab, o.x, L, le);
+    }
+}
+
+template <int MODEL, int K>
+__global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
+{
+    constexpr int BITS = bp_bits(K);
+    constexpr int SPW = bp_steps_per_word(K);
+    constexpr int STEPB = K * BITS;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    constexpr int C = 8;
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.P)
+        return;
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    constexpr int KP = (K + 1) / 2;
+    double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+
+    PairParams<MODEL, K> pp;
+    load_params<MODEL, K, true>(pp, a, d);
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        fill_table<K, true>(slab, a, d);
+
+    const int32_t *xb = a.x ? a.x + n : nullptr;
+    const int32_t *ab = nullptr;
+    if constexpr (ModelTraits<MODEL>::kSemisup)
+        ab = a.g + n;
+    if constexpr (ModelTraits<MODEL>::kTayal)
+        ab = a.sign + n;
+    const double *rb = a.xr ? a.xr + n : nullptr;
+
+    constexpr bool VAUX = ModelTraits<MODEL>::kTayal; /* semisup Viterbi is unmasked (Q7) */
+    /* delta_tk[1, K] = emission of j for j = 1..K: only column K is written,
+     * the others keep stanc's NaN (Q3, e.g. hmm-multinom.stan:236-237). */
+    double dl[K];
+    Obs cur[C];
+    load_chunk<MODEL, C, VAUX>(cur, a, xb, ab, rb, 0, Tp);
+    {
+        double le[K];
+        emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
+#pragma unroll
+        for (int k = 0; k < K - 1; ++k)
+            dl[k] = dev_nan();
+        dl[K - 1] = le[K - 1];
+    }
+    uint32_t word = 0;
+    uint32_t *bpp = a.bp + p;
+    const int nchunk = (Tp + C - 1) / C;
+    for (int c = 0; c < nchunk; ++c) {
+        const int t0 = c * C;
+        Obs nxt[C];
+        load_chunk<MODEL, C, VAUX>(nxt, a, xb, ab, rb, t0 + C, Tp);
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+            const int t = t0 + u;
+            if (t >= 1 && t < Tp) {
+                double le[K];
+                emit_log<MODEL, K>(pp, slab, a.L, cur[u], le);
+                double nd[K];
+                const int slot = t % SPW;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    double best = dev_ninf();
+                    uint32_t arg = 0;
+                    bool on = true;
+                    if constexpr (ModelTraits<MODEL>::kTayal)
+                        on = tayal_pred(cur[u].aux, j);
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        double cand;
+                        if constexpr (ModelTraits<MODEL>::kTayal) {
+                            /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
+                            cand = dl[i] + le[j];
+                            cand = on ? cand + pp.A[i][j] : cand;
+                        } else {
+                            /* (delta + log A) + emission (hmm.stan:111) */
+                            cand = (dl[i] + pp.A[i][j]) + le[j];
+                        }
+                        if (cand > best) {
+                            best = cand;
+                            arg = (uint32_t)i;
+                        }
+                    }
+                    nd[j] = best;
+                    word |= arg << (slot * STEPB + j * BITS);
+                }
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    dl[j] = nd[j];
+                if (slot == SPW - 1 || t == Tp - 1) {
+                    bpp[a.P * (int64_t)(t / SPW)] = word;
+                    word = 0;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < C; ++u)
+            cur[u] = nxt[u];
+    }
+
+    /* logp_zstar = max(delta_tk[T]); zstar[T] = LAST j attaining it (hmm.stan:120-124). */
+    const double lp = stan_max_vec<K>(dl);
+    int z = -1;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (dl[j] == lp)
+            z = j;
+    /* Backtracking reads an unset back-pointer exactly when zstar[T] is unset
+     * (NaN row at T = 1) or every delta_T is -inf. */
+    const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
+    if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
+        a.logp_zstar[p] = lp;
+    if (a.pair_status)
+        a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+    if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
+        return;
+    int32_t *zp = a.zstar + p;
+    if (invalid) {
+        for (int t = 0; t < Tp; ++t)
+            zp[a.P * (int64_t)t] = 0;
+        return;
+    }
+    zp[a.P * (int64_t)(Tp - 1)] = z + 1;
+    int wi = (Tp - 1) / SPW;
+    uint32_t w = bpp[a.P * (int64_t)wi];
+    uint32_t wprev = (wi > 0) ? bpp[a.P * (int64_t)(wi - 1)] : 0u;
+    for (int t = Tp - 1; t >= 1; --t) {
+        const int wt = t / SPW;
+        if (wt != wi) {
+            w = wprev;
+            wi = wt;
+            wprev = (wi > 0) ? bpp[a.P * (int64_t)(wi - 1)] : 0u;
+        }
+        const int slot = t % SPW;
+        z = (int)((w >> (slot * STEPB + z * BITS)) & MASK);
+        zp[a.P * (int64_t)(t - 1)] = z + 1;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Self-test kernel                                                       */
+/* ------------------------------------------------------------------ */
+__global__ void cr_log_kernel(const double *in, double *out, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        out[i] = hhmm_cr_log(in[i]);
+}
+
+/* ------------------------------------------------------------------ */
+/* Host-side launch plumbing                                             */
+/* ------------------------------------------------------------------ */
+
+static bool model_has_backward(int model)
+{
+    return model == HHMM_MODEL_HMM_GAUSS || model == HHMM_MODEL_HMM_MULTINOM ||
+           model == HHMM_MODEL_HMM_MULTINOM_SEMISUP || model == HHMM_MODEL_TAYAL;
+}
+
+static bool needs_backward(int model, uint32_t out)
+{
+    return model_has_backward(model) &&
+           (out & (HHMM_OUT_UNBETA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
+}
+
+static int nchunk_of(int K, int T) { return (T + fb_chunk(K) - 1) / fb_chunk(K); }
+static int nword_of(int K, int T) { return T / bp_steps_per_word(K) + 1; }
+
+static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs)
+{
+    size_t bytes = 0;
+    if (needs_backward(model, outputs)) {
+        bytes += align256((size_t)nchunk_of(K, Tmax) * K * P * sizeof(double));
+        bytes += align256((size_t)nchunk_of(K, Tmax) * P * sizeof(double));
+    }
+    if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
+        const int Tv = (model == HHMM_MODEL_TAYAL_LITE) ? Toos : Tmax;
+        bytes += align256((size_t)nword_of(K, Tv) * P * sizeof(uint32_t));
+    }
+    return bytes + 256;
+}
+
+void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos)
+{
+    char *b = (char *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+    a.ckpt = nullptr;
+    a.ckpt_ls = nullptr;
+    a.bp = nullptr;
+    if (needs_backward(a.model, a.outputs)) {
+        a.ckpt = (double *)b;
+        b += align256((size_t)nchunk_of(a.K, Tmax) * a.K * a.P * sizeof(double));
+        a.ckpt_ls = (double *)b;
+        b += align256((size_t)nchunk_of(a.K, Tmax) * a.P * sizeof(double));
+    }
+    if (a.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
+        a.bp = (uint32_t *)b;
+    }
+    (void)Toos;
+}
+
+struct LaunchShape {
+    dim3 grid, block;
+    size_t lds;
+};
+
+static bool shape_for(const DevArgs &a, bool discrete, LaunchShape &s)
+{
+    const int KP = (a.K + 1) / 2;
+    size_t per_wave = discrete ? (size_t)a.L * KP * 64 * sizeof(double2) : 0;
+    int waves = 4;
+    if (per_wave > 0) {
+        while (waves > 0 && per_wave * waves > kLdsLimit)
+            --waves;
+        if (waves == 0)
+            return false;
+    }
+    const int threads = 64 * waves;
+    s.block = dim3(threads);
+    s.grid = dim3((unsigned)((a.P + threads - 1) / threads));
+    s.lds = per_wave * waves;
+    return true;
+}
+
+template <int MODEL, int K>
+static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
+{
+    LaunchShape s;
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
+        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const bool full = (a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) != 0;
+    if (fwd_only)
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, true, false>), s.grid, s.block, s.lds, st, a);
+    else if (full)
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, false, true>), s.grid, s.block, s.lds, st, a);
+    else
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, false, false>), s.grid, s.block, s.lds, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("fb_kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+template <int MODEL, int K>
+static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
+{
+    LaunchShape s;
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
+        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL((viterbi_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("viterbi_kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+template <int MODEL, int K>
+static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const hhmm_result *res,
+                               hipStream_t st)
+{
+    hhmm_status s = HHMM_OK;
+    const uint32_t out = a.outputs;
+    if (MODEL == HHMM_MODEL_TAYAL_LITE) {
+        /* in-sample forward: alpha_tk / unalpha_tk / loglik (hhmm-tayal2009-lite.stan:216-258) */
+        if (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) {
+            s = launch_fb<MODEL, K>(a, true, st);
+            if (s != HHMM_OK)
+                return s;
+        }
+        /* out-of-sample forward and Viterbi on (x_oos, sign_oos) (:260-324) */
+        DevArgs o = a;
+        o.Tmax = req->data.T_oos_max;
+        o.Tout = req->data.T_oos_max;
+        o.T = req->data.T_oos;
+        o.x = req->data.x_oos;
+        o.sign = req->data.sign_oos;
+        o.loglik = nullptr;
+        o.alpha = res->alpha_tk_oos;
+        o.unalpha = res->unalpha_tk_oos;
+        o.outputs = out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR);
+        if (out & HHMM_OUT_ALPHA_OOS)
+            o.outputs |= HHMM_OUT_ALPHA;
+        if (out & HHMM_OUT_UNALPHA_OOS)
+            o.outputs |= HHMM_OUT_UNALPHA;
+        if (o.outputs & (HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) {
+            s = launch_fb<MODEL, K>(o, true, st);
+            if (s != HHMM_OK)
+                return s;
+        }
+        if (o.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
+            s = launch_viterbi<MODEL, K>(o, st);
+        return s;
+    }
+    const bool any_fwd = (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA |
+                                 HHMM_OUT_UNBETA | HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) != 0;
+    if (any_fwd) {
+        s = launch_fb<MODEL, K>(a, !needs_backward(MODEL, out), st);
+        if (s != HHMM_OK)
+            return s;
+    }
+    if (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
+        s = launch_viterbi<MODEL, K>(a, st);
+    return s;
+}
+
+template <int MODEL>
+static hhmm_status run_model(const DevArgs &a, const hhmm_request *req, const hhmm_result *res,
+                             hipStream_t st)
+{
+    if constexpr (ModelTraits<MODEL>::kTayal) {
+        if (a.K != 4) {
+            set_error("the Tayal model is defined for K = 4 (got %d)", a.K);
+            return HHMM_ERR_INVALID_ARGUMENT;
+        }
+        return run_model_k<MODEL, 4>(a, req, res, st);
+    } else {
+        switch (a.K) {
+        case 1: return run_model_k<MODEL, 1>(a, req, res, st);
+        case 2: return run_model_k<MODEL, 2>(a, req, res, st);
+        case 3: return run_model_k<MODEL, 3>(a, req, res, st);
+        case 4: return run_model_k<MODEL, 4>(a, req, res, st);
+        case 5: return run_model_k<MODEL, 5>(a, req, res, st);
+        case 6: return run_model_k<MODEL, 6>(a, req, res, st);
+        case 7: return run_model_k<MODEL, 7>(a, req, res, st);
+        case 8: return run_model_k<MODEL, 8>(a, req, res, st);
+        default:
+            set_error("K = %d not supported (1..%d)", a.K, kMaxK);
+            return HHMM_ERR_UNSUPPORTED;
+        }
+    }
+}
+
+DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
+{
+    DevArgs a;
+    memset(&a, 0, sizeof(a));
+    const hhmm_data &d = req->data;
+    const hhmm_draws &w = req->draws;
+    a.P = P;
+    a.N = d.n_series;
+    a.S = w.n_draws;
+    a.pairing = req->pairing;
+    a.model = req->model;
+    a.K = d.K;
+    a.L = d.L > 0 ? d.L : 1;
+    a.M = d.M;
+    a.Tmax = d.T_max;
+    a.Tout = d.T_max;
+    a.outputs = req->outputs;
+    a.T = d.T;
+    a.x = d.x_int;
+    a.xr = d.x_real;
+    a.g = d.g;
+    a.sign = d.sign;
+    a.u = d.u;
+    a.p_1k = w.p_1k;
+    a.A_ij = w.A_ij;
+    a.phi_k = w.phi_k;
+    a.mu_k = w.mu_k;
+    a.sigma_k = w.sigma_k;
+    a.w_km = w.w_km;
+    a.b_km = w.b_km;
+    a.s_k = w.s_k;
+    a.lambda_kl = w.lambda_kl;
+    a.mu_kl = w.mu_kl;
+    a.s_kl = w.s_kl;
+    a.p_11 = w.p_11;
+    a.A_row = w.A_row;
+    a.loglik = res->loglik;
+    a.unalpha = res->unalpha_tk;
+    a.alpha = res->alpha_tk;
+    a.unbeta = res->unbeta_tk;
+    a.beta = res->beta_tk;
+    a.ungamma = res->ungamma_tk;
+    a.gamma = res->gamma_tk;
+    a.zstar = res->zstar_t;
+    a.logp_zstar = res->logp_zstar;
+    a.pair_status = res->pair_status;
+    return a;
+}
+
+hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws,
+                       hipStream_t st)
+{
+    DevArgs a = make_args(req, res, P);
+    bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max);
+    if (req->model == HHMM_MODEL_TAYAL_LITE && (req->outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))) {
+        /* the OOS Viterbi is the only workspace user of tayal-lite */
+        a.bp = (uint32_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+    }
+    switch (req->model) {
+    case HHMM_MODEL_HMM_GAUSS: return run_model<HHMM_MODEL_HMM_GAUSS>(a, req, res, st);
+    case HHMM_MODEL_HMM_MULTINOM: return run_model<HHMM_MODEL_HMM_MULTINOM>(a, req, res, st);
+    case HHMM_MODEL_HMM_MULTINOM_SEMISUP: return run_model<HHMM_MODEL_HMM_MULTINOM_SEMISUP>(a, req, res, st);
+    case HHMM_MODEL_TAYAL: return run_model<HHMM_MODEL_TAYAL>(a, req, res, st);
+    case HHMM_MODEL_TAYAL_LITE: return run_model<HHMM_MODEL_TAYAL_LITE>(a, req, res, st);
+    default:
+        set_error("model %d has no device path in this build", req->model);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+}
+
+hhmm_status selftest_cr_log(const double *in, double *out, int64_t n)
+{
+    double *din = nullptr, *dout = nullptr;
+    const size_t bytes = (size_t)(n > 0 ? n : 1) * sizeof(double);
+    if (hipMalloc(&din, bytes) != hipSuccess || hipMalloc(&dout, bytes) != hipSuccess) {
+        hipFree(din);
+        set_error("hipMalloc failed in selftest");
+        return HHMM_ERR_OUT_OF_MEMORY;
+    }
+    hipError_t e = hipMemcpy(din, in, (size_t)n * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess && n > 0) {
+        hipLaunchKernelGGL(cr_log_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, din, dout, n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipMemcpy(out, dout, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
+    hipFree(din);
+    hipFree(dout);
+    if (e != hipSuccess) {
+        set_error("selftest: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+} // namespace hhmm

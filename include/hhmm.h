@@ -1,0 +1,222 @@
+/*
+ * hhmm.h -- C ABI of the MI355X batched HMM-family engine (libhhmm.so).
+ *
+ * Drop-in boundary.  The reference evaluates its hot path inside one Stan
+ * program per fit: R hands the model's `data` block to
+ *     rstan::stan(file, data = list(...))          (hmm/main.R:49-54,
+ *                                                   tayal2009/main.R:103-108)
+ * and reads the transformed parameters / generated quantities back with
+ *     rstan::extract(fit, pars = '<name>')          (hmm/main.R:67-68,98;
+ *                                                   hassan2005/main.R:90-95).
+ * Per saved draw, stanc's `write_array(params -> TP + GQ)` recomputes the
+ * forward filter, backward pass, smoothed posteriors and Viterbi decoding
+ * (e.g. hmm/stan/hmm.stan:24-130).  This library replaces that per-draw
+ * evaluation for a whole batch of (series x posterior draw) PAIRS at once:
+ *
+ *   inputs  = the `data` block of the Stan program, batched over series
+ *             (hhmm_data), and the `parameters` block as rstan::extract()
+ *             returns it for S draws (hhmm_draws);
+ *   outputs = the TP / GQ arrays with the names and shapes extract() gives
+ *             (hhmm_result), plus the model-block log-likelihood and FFBS.
+ *
+ * Layout convention: every array is R column-major with its FIRST index
+ * fastest, exactly the memory of the R array (zero-copy from .Call):
+ *   series arrays  [N, T_max]      x[n + N*t]
+ *                  [N, T_max, M]   u[n + N*(t + T_max*m)]
+ *   draw arrays    [S, K]          p_1k[s + S*k]
+ *                  [S, K, K]       A_ij[s + S*(i + K*j)]   (row i = from, col j = to)
+ *                  [S, K, L]       phi_k[s + S*(k + K*l)]
+ *   pair outputs   [P]             loglik[p]
+ *                  [P, T_max]      zstar_t[p + P*t]
+ *                  [P, T_max, K]   gamma_tk[p + P*(t + T_max*k)]
+ * Indices in and out are 1-based as in Stan/R (x in 1..L, sign in 1..2,
+ * g in 1..G, zstar in 1..K).  Time steps t >= T[n] of a padded series are
+ * neither read nor written.
+ *
+ * Pairing: HHMM_PAIR_GRID evaluates every series under every draw,
+ * P = N*S, pair p = s + S*n (draw fastest: a batch of draws of one series is
+ * rstan's [S, ...] slab).  HHMM_PAIR_ZIP pairs series n with draw n (N == S).
+ *
+ * Errors: every entry point returns hhmm_status; the message of the last
+ * failure on the calling thread is hhmm_last_error().  No C++ exception or
+ * longjmp crosses this ABI.  Where Stan would throw inside write_array
+ * (a Viterbi backtrack through an unset back-pointer: the Q3 initialisation
+ * quirk of SURVEY.md App. A, or all delta_T = -inf), the pair's zstar_t is
+ * filled with 0, pair_status[p] = HHMM_PAIR_INVALID_BACKPOINTER and the call
+ * returns HHMM_WARN_PAIR_FAILURES after completing every other pair.
+ *
+ * Ownership: the caller owns every input and output buffer; the library never
+ * retains a caller pointer after return.  The library owns its device pool,
+ * released by hhmm_shutdown().
+ */
+#ifndef HHMM_H
+#define HHMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HHMM_ABI_VERSION 1u
+
+typedef enum hhmm_status {
+    HHMM_OK = 0,
+    HHMM_WARN_PAIR_FAILURES = 1,       /* completed; some pair_status != 0 */
+    HHMM_ERR_INVALID_ARGUMENT = -1,
+    HHMM_ERR_OUT_OF_MEMORY = -2,
+    HHMM_ERR_HIP = -3,
+    HHMM_ERR_UNSUPPORTED = -4,
+    HHMM_ERR_NO_DEVICE = -5
+} hhmm_status;
+
+/* Per-pair status codes (hhmm_result.pair_status). */
+#define HHMM_PAIR_OK 0
+#define HHMM_PAIR_INVALID_BACKPOINTER 1
+
+/* One id per Stan program on the path. */
+typedef enum hhmm_model {
+    HHMM_MODEL_HMM_GAUSS = 1,            /* hmm/stan/hmm.stan */
+    HHMM_MODEL_HMM_MULTINOM = 2,         /* hmm/stan/hmm-multinom.stan */
+    HHMM_MODEL_HMM_MULTINOM_SEMISUP = 3, /* hmm/stan/hmm-multinom-semisup.stan */
+    HHMM_MODEL_IOHMM_REG = 4,            /* iohmm-reg/stan/iohmm-reg.stan */
+    HHMM_MODEL_IOHMM_MIX = 5,            /* iohmm-mix/stan/iohmm-mix.stan */
+    HHMM_MODEL_IOHMM_HMIX = 6,           /* iohmm-mix/stan/iohmm-hmix.stan */
+    HHMM_MODEL_IOHMM_HMIX_LITE = 7,      /* iohmm-mix/stan/iohmm-hmix-lite.stan */
+    HHMM_MODEL_TAYAL = 8,                /* tayal2009/stan/hhmm-tayal2009.stan */
+    HHMM_MODEL_TAYAL_LITE = 9            /* tayal2009/stan/hhmm-tayal2009-lite.stan */
+} hhmm_model;
+
+typedef enum hhmm_pairing {
+    HHMM_PAIR_GRID = 0,
+    HHMM_PAIR_ZIP = 1
+} hhmm_pairing;
+
+/* Output selection bitmask (hhmm_request.outputs).  Names are the Stan names. */
+#define HHMM_OUT_LOGLIK        (1u << 0)  /* target += log_sum_exp(unalpha_tk[T])   [P] */
+#define HHMM_OUT_UNALPHA       (1u << 1)  /* unalpha_tk                             [P,T,K] */
+#define HHMM_OUT_ALPHA         (1u << 2)  /* alpha_tk                               [P,T,K] */
+#define HHMM_OUT_UNBETA        (1u << 3)  /* unbeta_tk                              [P,T,K] */
+#define HHMM_OUT_BETA          (1u << 4)  /* beta_tk                                [P,T,K] */
+#define HHMM_OUT_UNGAMMA       (1u << 5)  /* ungamma_tk                             [P,T,K] */
+#define HHMM_OUT_GAMMA         (1u << 6)  /* gamma_tk                               [P,T,K] */
+#define HHMM_OUT_ZSTAR         (1u << 7)  /* zstar_t (Viterbi path, 1-based)        [P,T] */
+#define HHMM_OUT_LOGP_ZSTAR    (1u << 8)  /* logp_zstar_t / logp_zstar              [P] */
+#define HHMM_OUT_OBLIK_TK      (1u << 9)  /* oblik_tk (IOHMM emission log-density)  [P,T,K] */
+#define HHMM_OUT_OBLIK_T       (1u << 10) /* oblik_t  (iohmm-hmix[-lite])           [P,T] */
+#define HHMM_OUT_FFBS          (1u << 11) /* FFBS state draw (needs ffbs_u)          [P,T] */
+#define HHMM_OUT_ALPHA_OOS     (1u << 12) /* tayal-lite alpha_tk_oos                [P,T_oos,K] */
+#define HHMM_OUT_UNALPHA_OOS   (1u << 13) /* tayal-lite unalpha_tk_oos              [P,T_oos,K] */
+#define HHMM_OUT_LOGA          (1u << 14) /* IOHMM A_ij / logA_ij per t             [P,T,K] */
+
+/* The Stan `data` block, batched over N series (series fastest). */
+typedef struct hhmm_data {
+    int64_t n_series;          /* N */
+    int32_t T_max;             /* padded time extent of every [N, T_max] array */
+    int32_t K;                 /* hidden states */
+    int32_t L;                 /* outputs per state (multinom/tayal) or mixture components (iohmm-mix) */
+    int32_t M;                 /* input dimension (iohmm) */
+    int32_t G;                 /* feature sets (semisup) */
+    int32_t T_oos_max;         /* tayal-lite: padded out-of-sample extent */
+    const int32_t *T;          /* [N] lengths 1..T_max; NULL: every series has T_max */
+    const int32_t *x_int;      /* [N, T_max] int<lower=1,upper=L> x[T] */
+    const double  *x_real;     /* [N, T_max] real x[T] / x_t[T] */
+    const int32_t *g;          /* [N, T_max] semisup group 1..G */
+    const int32_t *sign;       /* [N, T_max] tayal sign 1 = up, 2 = down */
+    const double  *u;          /* [N, T_max, M] iohmm inputs u_tm */
+    const int32_t *T_oos;      /* [N] tayal-lite out-of-sample lengths; NULL: T_oos_max */
+    const int32_t *x_oos;      /* [N, T_oos_max] */
+    const int32_t *sign_oos;   /* [N, T_oos_max] */
+    const double  *hyperparams;/* [9] iohmm-hmix priors: read by no path output (model block only) */
+} hhmm_data;
+
+/* The `parameters` block for S draws, as rstan::extract() returns it (S fastest). */
+typedef struct hhmm_draws {
+    int64_t n_draws;           /* S */
+    const double *p_1k;        /* [S, K] simplex */
+    const double *A_ij;        /* [S, K, K] A_ij[i][j] = p(z_t = j | z_{t-1} = i) */
+    const double *phi_k;       /* [S, K, L] simplex rows */
+    const double *mu_k;        /* [S, K] hmm.stan */
+    const double *sigma_k;     /* [S, K] hmm.stan */
+    const double *w_km;        /* [S, K, M] iohmm state regressors */
+    const double *b_km;        /* [S, K, M] iohmm-reg mean regressors */
+    const double *s_k;         /* [S, K] iohmm-reg residual sd */
+    const double *lambda_kl;   /* [S, K, L] iohmm-mix component weights */
+    const double *mu_kl;       /* [S, K, L] iohmm-mix component means */
+    const double *s_kl;        /* [S, K, L] iohmm-mix component sds */
+    const double *p_11;        /* [S] tayal */
+    const double *A_row;       /* [S, 2, 2] tayal A_row[r][c] at s + S*(r + 2*c) */
+} hhmm_draws;
+
+typedef struct hhmm_request {
+    uint32_t abi_version;      /* HHMM_ABI_VERSION */
+    int32_t model;             /* hhmm_model */
+    int32_t pairing;           /* hhmm_pairing */
+    uint32_t outputs;          /* HHMM_OUT_* */
+    hhmm_data data;
+    hhmm_draws draws;
+    const double *ffbs_u;      /* [P, T_max] uniforms in (0,1) for HHMM_OUT_FFBS */
+    int32_t device;            /* HIP device ordinal for hhmm_run; -1 = current */
+    int32_t reserved;
+} hhmm_request;
+
+/* Caller-allocated outputs; a pointer may be NULL when its bit is not requested. */
+typedef struct hhmm_result {
+    double  *loglik;           /* [P] */
+    double  *unalpha_tk;       /* [P, T_max, K] */
+    double  *alpha_tk;         /* [P, T_max, K] */
+    double  *unbeta_tk;        /* [P, T_max, K] */
+    double  *beta_tk;          /* [P, T_max, K] */
+    double  *ungamma_tk;       /* [P, T_max, K] */
+    double  *gamma_tk;         /* [P, T_max, K] */
+    int32_t *zstar_t;          /* [P, T_max]; tayal-lite: [P, T_oos_max] */
+    double  *logp_zstar;       /* [P] */
+    double  *oblik_tk;         /* [P, T_max, K] */
+    double  *oblik_t;          /* [P, T_max] */
+    int32_t *z_ffbs;           /* [P, T_max] */
+    double  *alpha_tk_oos;     /* [P, T_oos_max, K] */
+    double  *unalpha_tk_oos;   /* [P, T_oos_max, K] */
+    double  *logA_ij;          /* [P, T_max, K] */
+    int32_t *pair_status;      /* [P] optional */
+} hhmm_result;
+
+/* Library identity, e.g. "hhmm-mi355x 0.1.0 gfx950 abi 1". */
+const char *hhmm_version(void);
+
+/* Message of the last non-OK status returned on this thread ("" if none). */
+const char *hhmm_last_error(void);
+
+/* Number of pairs the request describes (N*S for GRID, N for ZIP), or -1. */
+int64_t hhmm_num_pairs(const hhmm_request *req);
+
+/* Checks a request (dims, pointers for the requested outputs, index ranges on
+ * host data).  hhmm_run calls it; exposed for the R shim and tests. */
+hhmm_status hhmm_validate(const hhmm_request *req, const hhmm_result *res, int host_pointers);
+
+/* Optional explicit init: verifies that ndev gfx950 devices are visible. */
+hhmm_status hhmm_init(int ndev);
+
+/* Releases the device pool (R finaliser / process exit). */
+hhmm_status hhmm_shutdown(void);
+
+/* Host-pointer entry (the R .Call path): uploads, runs on request->device,
+ * downloads, synchronises.  Replaces rstan write_array over all pairs. */
+hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res);
+
+/* Device-resident entry: every pointer in req/res is a device pointer on the
+ * current HIP device; enqueues on `stream` (hipStream_t, NULL = default) and
+ * returns without synchronising.  `workspace` must hold
+ * hhmm_workspace_size() bytes.  Per-pair failures land in res->pair_status. */
+hhmm_status hhmm_workspace_size(const hhmm_request *req, size_t *bytes);
+hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res,
+                            void *workspace, size_t workspace_bytes, void *stream);
+
+/* Self-test hook: the device's correctly rounded log over n host doubles. */
+hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HHMM_H */

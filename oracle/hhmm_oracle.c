@@ -1,0 +1,1058 @@
+/*
+ * hhmm_oracle.c -- CPU ORACLE for the batched HMM-family path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the
+ * checker / the timed CPU baseline.  The product (libhhmm.so) never links,
+ * loads or falls back to it.
+ *
+ * What it is: a scalar, one-pair-at-a-time restatement of the Stan programs'
+ * transformed-parameters / model / generated-quantities blocks, in stanc's
+ * evaluation order, with the reference's quirks and
+ * the Stan Math 2.14 semantics it relies on (Appendix B).  Every function
+ * cites the reference lines it follows.  It consumes the same hhmm_request /
+ * hhmm_result structs as the engine (include/hhmm.h), with host pointers.
+ *
+ * Parity status: UNPINNED against the reference's own outputs -- the
+ * reference has no tests, golden vectors or saved fits, and R/Stan are not
+ * available here or on the GPU box.  The restatement is
+ * cross-checked instead by an independent NumPy transcription
+ * (tests/oracle_numpy.py), analytic known-answer tests, and committed
+ * fixtures (tests/golden/).
+ *
+ * Transcendentals: `log` is hhmm_cr_log (correctly rounded; identical code
+ * on the GPU) unless built with -DHHMM_ORACLE_LIBM_LOG, which uses the host
+ * libm `log` exactly as Stan would; `exp` is the host libm in both builds.
+ */
+#include <limits.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hhmm.h"
+
+#define HHMM_MATH_FN static inline
+#define HHMM_MATH_TABLE static
+#include "hhmm_crmath.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#ifdef HHMM_ORACLE_LIBM_LOG
+#define OR_LOG(x) log(x)
+#else
+#define OR_LOG(x) hhmm_cr_log(x)
+#endif
+#define OR_EXP(x) exp(x)
+
+#define NEG_INF (-INFINITY)
+#define STAN_INT_UNSET INT_MIN /* stanc 2.x fills local ints with INT_MIN */
+
+/* ------------------------------------------------------------------ */
+/* Stan Math 2.14 primitives                    */
+/* ------------------------------------------------------------------ */
+
+/* log_sum_exp(std::vector<double>) and the Eigen-vector overload:
+ * max by strict `>` (NaN ignored), sum of exp(x - max) over x != -inf,
+ * sequential; max + log(sum).  Used by every `real accumulator[K]`
+ * (e.g. hmm/stan/hmm.stan:39,81) and by `target +=` (hmm.stan:46). */
+static double stan_log_sum_exp(const double *x, int n)
+{
+    double mx = NEG_INF;
+    for (int i = 0; i < n; ++i)
+        if (x[i] > mx)
+            mx = x[i];
+    double sum = 0.0;
+    for (int i = 0; i < n; ++i)
+        if (x[i] != NEG_INF)
+            sum += OR_EXP(x[i] - mx);
+    return mx + OR_LOG(sum);
+}
+
+/* softmax(v): theta = exp(v - max(v)); theta / sum(theta) (sequential). */
+static void stan_softmax(const double *v, int n, double *out)
+{
+    double mx = v[0];
+    for (int i = 1; i < n; ++i)
+        if (v[i] > mx)
+            mx = v[i];
+    double sum = 0.0;
+    for (int i = 0; i < n; ++i) {
+        out[i] = OR_EXP(v[i] - mx);
+        sum += out[i];
+    }
+    for (int i = 0; i < n; ++i)
+        out[i] = out[i] / sum;
+}
+
+/* sum(vector) = Eigen redux on x86-64 SSE2: two 2-wide partial sums over
+ * blocks of 4, one more packet, horizontal add, scalar tail. */
+static double stan_sum_vec(const double *a, int n)
+{
+    if (n < 2)
+        return n == 1 ? a[0] : 0.0;
+    const int aligned = n & ~1, aligned2 = n & ~3;
+    double r0a = a[0], r0b = a[1];
+    if (aligned > 2) {
+        double r1a = a[2], r1b = a[3];
+        for (int i = 4; i < aligned2; i += 4) {
+            r0a = r0a + a[i];
+            r0b = r0b + a[i + 1];
+            r1a = r1a + a[i + 2];
+            r1b = r1b + a[i + 3];
+        }
+        r0a = r0a + r1a;
+        r0b = r0b + r1b;
+        if (aligned > aligned2) {
+            r0a = r0a + a[aligned2];
+            r0b = r0b + a[aligned2 + 1];
+        }
+    }
+    double res = r0a + r0b;
+    for (int i = aligned; i < n; ++i)
+        res = res + a[i];
+    return res;
+}
+
+/* normalize(x) = x / sum(x)  (every functions{} block, e.g. hmm.stan:2-4). */
+static void stan_normalize(const double *x, int n, double *out)
+{
+    const double sum = stan_sum_vec(x, n);
+    for (int i = 0; i < n; ++i)
+        out[i] = x[i] / sum;
+}
+
+/* max(std::vector<double>) = Eigen::Map<VectorXd>(...).maxCoeff() on x86-64
+ * (SSE2 packet reduction, 16-byte aligned heap rows): maxpd / maxsd return
+ * their SECOND operand when either is NaN, the scalar tail is std::max.
+ * Values only differ from a plain max when NaN is present, i.e. the Viterbi
+ * delta_tk[1] row left NaN by the Q3 initialisation (T == 1). */
+static inline double sse_max(double a, double b) { return a > b ? a : b; }
+static inline double std_max(double a, double b) { return a < b ? b : a; }
+static double stan_max_vec(const double *d, int n)
+{
+    if (n == 0)
+        return NEG_INF;
+    if (n < 2) {
+        return d[0];
+    }
+    const int aligned = n & ~1, aligned2 = n & ~3;
+    double r0a = d[0], r0b = d[1];
+    if (aligned > 2) {
+        double r1a = d[2], r1b = d[3];
+        for (int i = 4; i < aligned2; i += 4) {
+            r0a = sse_max(r0a, d[i]);
+            r0b = sse_max(r0b, d[i + 1]);
+            r1a = sse_max(r1a, d[i + 2]);
+            r1b = sse_max(r1b, d[i + 3]);
+        }
+        r0a = sse_max(r0a, r1a);
+        r0b = sse_max(r0b, r1b);
+        if (aligned > aligned2) {
+            r0a = sse_max(r0a, d[aligned2]);
+            r0b = sse_max(r0b, d[aligned2 + 1]);
+        }
+    }
+    double res = sse_max(r0a, r0b);
+    for (int i = aligned; i < n; ++i)
+        res = std_max(res, d[i]);
+    return res;
+}
+
+/* row_vector * vector = Eigen dot on x86-64 SSE2: two 2-wide partial sums
+ * over blocks of 4, one more packet, horizontal add, scalar tail.
+ * (iohmm-reg/stan/iohmm-reg.stan:183,192). */
+static double stan_dot(const double *a, const double *b, int n)
+{
+    if (n < 2) {
+        return n == 1 ? a[0] * b[0] : 0.0;
+    }
+    const int aligned = n & ~1, aligned2 = n & ~3;
+    double r0a = a[0] * b[0], r0b = a[1] * b[1];
+    if (aligned > 2) {
+        double r1a = a[2] * b[2], r1b = a[3] * b[3];
+        for (int i = 4; i < aligned2; i += 4) {
+            r0a = r0a + a[i] * b[i];
+            r0b = r0b + a[i + 1] * b[i + 1];
+            r1a = r1a + a[i + 2] * b[i + 2];
+            r1b = r1b + a[i + 3] * b[i + 3];
+        }
+        r0a = r0a + r1a;
+        r0b = r0b + r1b;
+        if (aligned > aligned2) {
+            r0a = r0a + a[aligned2] * b[aligned2];
+            r0b = r0b + a[aligned2 + 1] * b[aligned2 + 1];
+        }
+    }
+    double res = r0a + r0b;
+    for (int i = aligned; i < n; ++i)
+        res = res + a[i] * b[i];
+    return res;
+}
+
+/* normal_lpdf(y | mu, sigma), not propto: logp = 0; logp += NEG_LOG_SQRT_TWO_PI;
+ * logp -= log(sigma); logp += -0.5 * ((y - mu) * (1/sigma))^2. */
+static double stan_normal_lpdf(double y, double mu, double sigma)
+{
+    const double inv_sigma = 1.0 / sigma;
+    const double log_sigma = OR_LOG(sigma);
+    const double z = (y - mu) * inv_sigma;
+    const double z2 = z * z;
+    double logp = 0.0;
+    logp += HHMM_NEG_LOG_SQRT_TWO_PI;
+    logp -= log_sigma;
+    logp += -0.5 * z2;
+    return logp;
+}
+
+/* Vectorised normal_lpdf(y | mu_k, sigma_k): the SUM over k of the terms,
+ * accumulated in the same order (hmm/stan/hmm.stan:30). */
+static double stan_normal_lpdf_vec(double y, const double *mu, const double *sigma, int K)
+{
+    double logp = 0.0;
+    for (int k = 0; k < K; ++k) {
+        const double inv_sigma = 1.0 / sigma[k];
+        const double log_sigma = OR_LOG(sigma[k]);
+        const double z = (y - mu[k]) * inv_sigma;
+        const double z2 = z * z;
+        logp += HHMM_NEG_LOG_SQRT_TWO_PI;
+        logp -= log_sigma;
+        logp += -0.5 * z2;
+    }
+    return logp;
+}
+
+/* ------------------------------------------------------------------ */
+/* Per-pair working set                                                 */
+/* ------------------------------------------------------------------ */
+
+typedef struct pair_ctx {
+    int K, L, M, T, T_oos;
+    /* series data, gathered contiguous (0-based t) */
+    int32_t *x, *g, *sgn, *x_oos, *sgn_oos;
+    double *xr, *u; /* u[t*M + m] */
+    /* draw parameters, natural Stan index order */
+    double *p;      /* [K] */
+    double *A;      /* [K*K] A[i*K + j] */
+    double *phi;    /* [K*L] phi[k*L + l] */
+    double *mu, *sigma;          /* [K] */
+    double *w, *b;               /* [K*M] */
+    double *sk;                  /* [K] */
+    double *lambda, *mukl, *skl; /* [K*L] */
+    /* work arrays [T*K] */
+    double *unalpha, *alpha, *unbeta, *beta, *ungamma, *gamma;
+    double *oblik, *Arow, *logA, *delta, *acc, *tmp;
+    int32_t *bp, *zstar;
+    double *oblik_t;
+    double *unalpha_oos, *alpha_oos;
+    double loglik, logp_zstar;
+    int status;
+} pair_ctx;
+
+static void *xmalloc(size_t n)
+{
+    void *p = malloc(n ? n : 1);
+    if (!p) {
+        fprintf(stderr, "hhmm_oracle: out of memory\n");
+        abort();
+    }
+    return p;
+}
+
+static void ctx_alloc(pair_ctx *c, int K, int L, int M, int Tm, int Toos)
+{
+    memset(c, 0, sizeof(*c));
+    int TT = Tm > Toos ? Tm : Toos;
+    if (TT < 1)
+        TT = 1;
+    size_t tk = (size_t)TT * K;
+    int KL = K * (L > 0 ? L : 1);
+    int KM = K * (M > 0 ? M : 1);
+    c->x = xmalloc(sizeof(int32_t) * TT);
+    c->g = xmalloc(sizeof(int32_t) * TT);
+    c->sgn = xmalloc(sizeof(int32_t) * TT);
+    c->x_oos = xmalloc(sizeof(int32_t) * TT);
+    c->sgn_oos = xmalloc(sizeof(int32_t) * TT);
+    c->xr = xmalloc(sizeof(double) * TT);
+    c->u = xmalloc(sizeof(double) * (size_t)TT * (M > 0 ? M : 1));
+    c->p = xmalloc(sizeof(double) * K);
+    c->A = xmalloc(sizeof(double) * K * K);
+    c->phi = xmalloc(sizeof(double) * KL);
+    c->mu = xmalloc(sizeof(double) * K);
+    c->sigma = xmalloc(sizeof(double) * K);
+    c->w = xmalloc(sizeof(double) * KM);
+    c->b = xmalloc(sizeof(double) * KM);
+    c->sk = xmalloc(sizeof(double) * K);
+    c->lambda = xmalloc(sizeof(double) * KL);
+    c->mukl = xmalloc(sizeof(double) * KL);
+    c->skl = xmalloc(sizeof(double) * KL);
+    c->unalpha = xmalloc(sizeof(double) * tk);
+    c->alpha = xmalloc(sizeof(double) * tk);
+    c->unbeta = xmalloc(sizeof(double) * tk);
+    c->beta = xmalloc(sizeof(double) * tk);
+    c->ungamma = xmalloc(sizeof(double) * tk);
+    c->gamma = xmalloc(sizeof(double) * tk);
+    c->oblik = xmalloc(sizeof(double) * tk);
+    c->Arow = xmalloc(sizeof(double) * tk);
+    c->logA = xmalloc(sizeof(double) * tk);
+    c->delta = xmalloc(sizeof(double) * tk);
+    c->acc = xmalloc(sizeof(double) * (K > KL ? K : KL));
+    c->tmp = xmalloc(sizeof(double) * (K > KL ? K : KL));
+    c->bp = xmalloc(sizeof(int32_t) * tk);
+    c->zstar = xmalloc(sizeof(int32_t) * TT);
+    c->oblik_t = xmalloc(sizeof(double) * TT);
+    c->unalpha_oos = xmalloc(sizeof(double) * tk);
+    c->alpha_oos = xmalloc(sizeof(double) * tk);
+}
+
+static void ctx_free(pair_ctx *c)
+{
+    void *ptrs[] = {c->x, c->g, c->sgn, c->x_oos, c->sgn_oos, c->xr, c->u, c->p, c->A, c->phi,
+                    c->mu, c->sigma, c->w, c->b, c->sk, c->lambda, c->mukl, c->skl,
+                    c->unalpha, c->alpha, c->unbeta, c->beta, c->ungamma, c->gamma, c->oblik,
+                    c->Arow, c->logA, c->delta, c->acc, c->tmp, c->bp, c->zstar, c->oblik_t,
+                    c->unalpha_oos, c->alpha_oos};
+    for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i)
+        free(ptrs[i]);
+}
+
+#define TK(a, t, k) ((a)[(size_t)(t) * K + (k)])
+
+/* ------------------------------------------------------------------ */
+/* Shared GQ blocks                                                     */
+/* ------------------------------------------------------------------ */
+
+/* alpha_tk[t] = softmax(unalpha_tk[t])  (hmm.stan:60-63 and every model). */
+static void gq_softmax_rows(const double *un, double *out, int T, int K)
+{
+    for (int t = 0; t < T; ++t)
+        stan_softmax(&un[(size_t)t * K], K, &out[(size_t)t * K]);
+}
+
+/* ungamma = alpha .* beta; gamma = normalize(ungamma)  (hmm.stan:89-96). */
+static void gq_gamma(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    for (int t = 0; t < T; ++t) {
+        for (int k = 0; k < K; ++k)
+            TK(c->ungamma, t, k) = TK(c->alpha, t, k) * TK(c->beta, t, k);
+        stan_normalize(&TK(c->ungamma, t, 0), K, &TK(c->gamma, t, 0));
+    }
+}
+
+/* Viterbi epilogue (hmm.stan:120-128): logp = max(delta[T]); zstar[T] = LAST j
+ * with delta[T, j] == logp; backtrack through a_tk.  An unset back-pointer
+ * (INT_MIN) is where Stan throws: the pair is flagged and zstar zeroed. */
+static void viterbi_finish(pair_ctx *c, int T)
+{
+    const int K = c->K;
+    c->logp_zstar = stan_max_vec(&TK(c->delta, T - 1, 0), K);
+    int z = STAN_INT_UNSET;
+    for (int j = 0; j < K; ++j)
+        if (TK(c->delta, T - 1, j) == c->logp_zstar)
+            z = j + 1;
+    c->zstar[T - 1] = z;
+    int bad = (z == STAN_INT_UNSET);
+    for (int t = 1; t < T && !bad; ++t) {
+        const int zn = c->zstar[T - t];
+        const int zp = TK(c->bp, T - t, zn - 1);
+        if (zp == STAN_INT_UNSET) {
+            bad = 1;
+            break;
+        }
+        c->zstar[T - 1 - t] = zp;
+    }
+    if (bad) {
+        c->status = HHMM_PAIR_INVALID_BACKPOINTER;
+        for (int t = 0; t < T; ++t)
+            c->zstar[t] = 0;
+    }
+}
+
+static void viterbi_reset(pair_ctx *c, int T)
+{
+    const int K = c->K;
+    for (int t = 0; t < T; ++t)
+        for (int k = 0; k < K; ++k) {
+            TK(c->delta, t, k) = NAN;        /* stanc fills local reals with NaN */
+            TK(c->bp, t, k) = STAN_INT_UNSET;
+        }
+}
+
+/* ------------------------------------------------------------------ */
+/* hmm/stan/hmm.stan -- Gaussian emissions                              */
+/* ------------------------------------------------------------------ */
+static void model_hmm_gauss(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    double *acc = c->acc;
+    /* TP forward, hmm.stan:27-42.  t = 1 adds the SUM over k of the
+     * per-state densities (vectorised normal_lpdf, Q2). */
+    {
+        const double s = stan_normal_lpdf_vec(c->xr[0], c->mu, c->sigma, K);
+        for (int j = 0; j < K; ++j)
+            TK(c->unalpha, 0, j) = OR_LOG(c->p[j]) + s;
+    }
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i)
+                acc[i] = TK(c->unalpha, t - 1, i) + OR_LOG(c->A[i * K + j]) +
+                         stan_normal_lpdf(c->xr[t], c->mu[j], c->sigma[j]);
+            TK(c->unalpha, t, j) = stan_log_sum_exp(acc, K);
+        }
+    /* model block, hmm.stan:46 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K);
+    /* GQ forward, hmm.stan:60-63 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);
+    /* GQ backward, hmm.stan:65-87 (unbeta[T] = 1, Q1) */
+    for (int j = 0; j < K; ++j)
+        TK(c->unbeta, T - 1, j) = 1;
+    for (int tf = 0; tf <= T - 2; ++tf) {
+        const int t = T - 1 - tf; /* 0-based; Stan's t = T - tforward */
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i)
+                acc[i] = TK(c->unbeta, t, i) + OR_LOG(c->A[j * K + i]) +
+                         stan_normal_lpdf(c->xr[t], c->mu[i], c->sigma[i]);
+            TK(c->unbeta, t - 1, j) = stan_log_sum_exp(acc, K);
+        }
+    }
+    gq_softmax_rows(c->unbeta, c->beta, T, K);
+    gq_gamma(c); /* hmm.stan:89-96 */
+    /* Viterbi, hmm.stan:98-130 (Q3: only delta[1, K] is written) */
+    viterbi_reset(c, T);
+    for (int j = 0; j < K; ++j)
+        TK(c->delta, 0, K - 1) = stan_normal_lpdf(c->xr[0], c->mu[j], c->sigma[j]);
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            TK(c->delta, t, j) = NEG_INF;
+            for (int i = 0; i < K; ++i) {
+                const double logp = TK(c->delta, t - 1, i) + OR_LOG(c->A[i * K + j]) +
+                                    stan_normal_lpdf(c->xr[t], c->mu[j], c->sigma[j]);
+                if (logp > TK(c->delta, t, j)) {
+                    TK(c->bp, t, j) = i + 1;
+                    TK(c->delta, t, j) = logp;
+                }
+            }
+        }
+    viterbi_finish(c, T);
+}
+
+/* ------------------------------------------------------------------ */
+/* hmm/stan/hmm-multinom.stan -- multinomial emissions                  */
+/* ------------------------------------------------------------------ */
+#define PHI(k, l) (c->phi[(size_t)(k) * c->L + (l)])
+
+static void model_hmm_multinom(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    double *acc = c->acc;
+    /* TP forward, hmm-multinom.stan:27-44 */
+    for (int j = 0; j < K; ++j)
+        TK(c->unalpha, 0, j) = OR_LOG(c->p[j]) + OR_LOG(PHI(j, c->x[0] - 1));
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i)
+                acc[i] = TK(c->unalpha, t - 1, i) + OR_LOG(c->A[i * K + j]) +
+                         OR_LOG(PHI(j, c->x[t] - 1));
+            TK(c->unalpha, t, j) = stan_log_sum_exp(acc, K);
+        }
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :48 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :62-65 */
+    /* backward, hmm-multinom.stan:67-89 */
+    for (int j = 0; j < K; ++j)
+        TK(c->unbeta, T - 1, j) = 1;
+    for (int tf = 0; tf <= T - 2; ++tf) {
+        const int t = T - 1 - tf;
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i)
+                acc[i] = TK(c->unbeta, t, i) + OR_LOG(c->A[j * K + i]) + OR_LOG(PHI(i, c->x[t] - 1));
+            TK(c->unbeta, t - 1, j) = stan_log_sum_exp(acc, K);
+        }
+    }
+    gq_softmax_rows(c->unbeta, c->beta, T, K);
+    gq_gamma(c); /* :91-98 */
+    /* Viterbi, hmm-multinom.stan:100-132 */
+    viterbi_reset(c, T);
+    for (int j = 0; j < K; ++j)
+        TK(c->delta, 0, K - 1) = OR_LOG(PHI(j, c->x[0] - 1));
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            TK(c->delta, t, j) = NEG_INF;
+            for (int i = 0; i < K; ++i) {
+                const double logp = TK(c->delta, t - 1, i) + OR_LOG(c->A[i * K + j]) +
+                                    OR_LOG(PHI(j, c->x[t] - 1));
+                if (logp > TK(c->delta, t, j)) {
+                    TK(c->bp, t, j) = i + 1;
+                    TK(c->delta, t, j) = logp;
+                }
+            }
+        }
+    viterbi_finish(c, T);
+}
+
+/* ------------------------------------------------------------------ */
+/* hmm/stan/hmm-multinom-semisup.stan -- group-masked forward            */
+/* ------------------------------------------------------------------ */
+static int semisup_mask(int g, int j1)
+{
+    /* hmm-multinom-semisup.stan:42 (j1 is 1-based) */
+    return (g == 1 && (j1 == 1 || j1 == 4)) || (g == 2 && (j1 == 2 || j1 == 3));
+}
+
+static void model_hmm_multinom_semisup(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    double *acc = c->acc;
+    /* TP forward, semisup.stan:29-49 (transition only under the mask, Q7) */
+    for (int j = 0; j < K; ++j)
+        TK(c->unalpha, 0, j) = OR_LOG(c->p[j]) + OR_LOG(PHI(j, c->x[0] - 1));
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i) {
+                acc[i] = TK(c->unalpha, t - 1, i) + OR_LOG(PHI(j, c->x[t] - 1));
+                if (semisup_mask(c->g[t], j + 1))
+                    acc[i] = acc[i] + OR_LOG(c->A[i * K + j]);
+            }
+            TK(c->unalpha, t, j) = stan_log_sum_exp(acc, K);
+        }
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :53 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :67-70 */
+    /* backward, semisup.stan:72-94 (unmasked) */
+    for (int j = 0; j < K; ++j)
+        TK(c->unbeta, T - 1, j) = 1;
+    for (int tf = 0; tf <= T - 2; ++tf) {
+        const int t = T - 1 - tf;
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i)
+                acc[i] = TK(c->unbeta, t, i) + OR_LOG(c->A[j * K + i]) + OR_LOG(PHI(i, c->x[t] - 1));
+            TK(c->unbeta, t - 1, j) = stan_log_sum_exp(acc, K);
+        }
+    }
+    gq_softmax_rows(c->unbeta, c->beta, T, K);
+    gq_gamma(c); /* :96-103 */
+    /* Viterbi, semisup.stan:105-137 (unmasked) */
+    viterbi_reset(c, T);
+    for (int j = 0; j < K; ++j)
+        TK(c->delta, 0, K - 1) = OR_LOG(PHI(j, c->x[0] - 1));
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            TK(c->delta, t, j) = NEG_INF;
+            for (int i = 0; i < K; ++i) {
+                const double logp = TK(c->delta, t - 1, i) + OR_LOG(c->A[i * K + j]) +
+                                    OR_LOG(PHI(j, c->x[t] - 1));
+                if (logp > TK(c->delta, t, j)) {
+                    TK(c->bp, t, j) = i + 1;
+                    TK(c->delta, t, j) = logp;
+                }
+            }
+        }
+    viterbi_finish(c, T);
+}
+
+/* ------------------------------------------------------------------ */
+/* IOHMM shared blocks                                                  */
+/* ------------------------------------------------------------------ */
+
+/* Transition TP: unA[1] = A[1] = p_1k (filler); A[t] = softmax(u_t' w_j)
+ * (iohmm-reg.stan:178-187; iohmm-mix.stan:42-51).  Arow[t*K + i]. */
+static void iohmm_transitions(pair_ctx *c)
+{
+    const int K = c->K, T = c->T, M = c->M;
+    for (int k = 0; k < K; ++k)
+        TK(c->Arow, 0, k) = c->p[k];
+    for (int t = 1; t < T; ++t) {
+        for (int j = 0; j < K; ++j)
+            c->tmp[j] = stan_dot(&c->u[(size_t)t * M], &c->w[(size_t)j * M], M);
+        stan_softmax(c->tmp, K, &TK(c->Arow, t, 0));
+    }
+}
+
+/* hmix: logA[1] = log(p_1k); logA[t] = log(softmax(u_t' w_j))
+ * (iohmm-hmix.stan:232-244; lite :422-434). */
+static void iohmm_log_transitions(pair_ctx *c)
+{
+    const int K = c->K, T = c->T, M = c->M;
+    for (int k = 0; k < K; ++k)
+        TK(c->logA, 0, k) = OR_LOG(c->p[k]);
+    for (int t = 1; t < T; ++t) {
+        for (int j = 0; j < K; ++j)
+            c->tmp[j] = stan_dot(&c->u[(size_t)t * M], &c->w[(size_t)j * M], M);
+        stan_softmax(c->tmp, K, c->acc);
+        for (int j = 0; j < K; ++j)
+            TK(c->logA, t, j) = OR_LOG(c->acc[j]);
+    }
+}
+
+/* Gaussian-mixture emission: loglambda = log(lambda_kl);
+ * oblik[t][j] = LSE_l(loglambda[j][l] + normal_lpdf(x_t | mu_kl, s_kl))
+ * (iohmm-mix.stan:53-65; iohmm-hmix.stan:246-258). */
+static void iohmm_mixture_oblik(pair_ctx *c)
+{
+    const int K = c->K, T = c->T, L = c->L;
+    double *ll = c->tmp; /* [K*L] */
+    for (int k = 0; k < K * L; ++k)
+        ll[k] = OR_LOG(c->lambda[k]);
+    for (int t = 0; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            for (int l = 0; l < L; ++l)
+                c->acc[l] = ll[j * L + l] +
+                            stan_normal_lpdf(c->xr[t], c->mukl[j * L + l], c->skl[j * L + l]);
+            TK(c->oblik, t, j) = stan_log_sum_exp(c->acc, L);
+        }
+}
+
+/* Forward with the prev-state-indexed K-vector transition (Q5):
+ * acc[i] = unalpha[t-1, i] + logA_t(i) + oblik[t][j]. */
+static void iohmm_forward(pair_ctx *c, int use_logA_table)
+{
+    const int K = c->K, T = c->T;
+    double *acc = c->acc;
+    for (int j = 0; j < K; ++j)
+        TK(c->unalpha, 0, j) = OR_LOG(c->p[j]) + TK(c->oblik, 0, j);
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i) {
+                const double la = use_logA_table ? TK(c->logA, t, i) : OR_LOG(TK(c->Arow, t, i));
+                acc[i] = TK(c->unalpha, t - 1, i) + la + TK(c->oblik, t, j);
+            }
+            TK(c->unalpha, t, j) = stan_log_sum_exp(acc, K);
+        }
+}
+
+/* Backward: acc[i] = unbeta[t, i] + logA_t(i) + oblik[t][i], the same for
+ * every j (iohmm-reg.stan:218-240; iohmm-hmix.stan:281-304). */
+static void iohmm_backward(pair_ctx *c, int use_logA_table)
+{
+    const int K = c->K, T = c->T;
+    double *acc = c->acc;
+    for (int j = 0; j < K; ++j)
+        TK(c->unbeta, T - 1, j) = 1;
+    for (int tf = 0; tf <= T - 2; ++tf) {
+        const int t = T - 1 - tf;
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i) {
+                const double la = use_logA_table ? TK(c->logA, t, i) : OR_LOG(TK(c->Arow, t, i));
+                acc[i] = TK(c->unbeta, t, i) + la + TK(c->oblik, t, i);
+            }
+            TK(c->unbeta, t - 1, j) = stan_log_sum_exp(acc, K);
+        }
+    }
+}
+
+/* Viterbi: (delta + logA_t(i)) + oblik[t][j]; buggy init unless fixed_init
+ * (iohmm-reg.stan:288-319; iohmm-hmix.stan:356-389 has the fixed init). */
+static void iohmm_viterbi(pair_ctx *c, int use_logA_table, int fixed_init)
+{
+    const int K = c->K, T = c->T;
+    viterbi_reset(c, T);
+    if (fixed_init) {
+        for (int j = 0; j < K; ++j)
+            TK(c->delta, 0, j) = TK(c->oblik, 0, j);
+    } else {
+        for (int j = 0; j < K; ++j)
+            TK(c->delta, 0, K - 1) = TK(c->oblik, 0, j);
+    }
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            TK(c->delta, t, j) = NEG_INF;
+            for (int i = 0; i < K; ++i) {
+                const double la = use_logA_table ? TK(c->logA, t, i) : OR_LOG(TK(c->Arow, t, i));
+                const double logp = TK(c->delta, t - 1, i) + la + TK(c->oblik, t, j);
+                if (logp > TK(c->delta, t, j)) {
+                    TK(c->bp, t, j) = i + 1;
+                    TK(c->delta, t, j) = logp;
+                }
+            }
+        }
+    viterbi_finish(c, T);
+}
+
+/* iohmm-reg/stan/iohmm-reg.stan */
+static void model_iohmm_reg(pair_ctx *c)
+{
+    const int K = c->K, T = c->T, M = c->M;
+    iohmm_transitions(c); /* :178-187 */
+    for (int t = 0; t < T; ++t) /* emission, :189-195 */
+        for (int j = 0; j < K; ++j)
+            TK(c->oblik, t, j) = stan_normal_lpdf(
+                c->xr[t], stan_dot(&c->u[(size_t)t * M], &c->b[(size_t)j * M], M), c->sk[j]);
+    iohmm_forward(c, 0);                                        /* :197-212 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :214-215 */
+    iohmm_backward(c, 0);                                       /* :218-236 */
+    gq_softmax_rows(c->unbeta, c->beta, T, K);                  /* :238-239 */
+    gq_gamma(c);                                                /* :242-248 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :258 (priors excluded) */
+    iohmm_viterbi(c, 0, 0);                                     /* :288-319 */
+}
+
+/* iohmm-mix/stan/iohmm-mix.stan */
+static void model_iohmm_mix(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    iohmm_transitions(c);  /* :42-51 */
+    iohmm_mixture_oblik(c); /* :53-65 */
+    /* forward uses `logA_ij = log(A_ij)` (:69, :79) */
+    for (int t = 0; t < T; ++t)
+        for (int k = 0; k < K; ++k)
+            TK(c->logA, t, k) = OR_LOG(TK(c->Arow, t, k));
+    iohmm_forward(c, 1);                                        /* :67-83 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :85-86 */
+    iohmm_backward(c, 0);                                       /* :89-107, log(A_ij) */
+    gq_softmax_rows(c->unbeta, c->beta, T, K);                  /* :109-110 */
+    gq_gamma(c);                                                /* :113-119 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :129 */
+    iohmm_viterbi(c, 0, 0);                                     /* :164-195, log(A_ij) */
+}
+
+/* oblik_t[t] = log_sum_exp(log(alpha_tk[t]) + oblik_tk[t]) (iohmm-hmix.stan:314-317);
+ * lite recomputes log(softmax(unalpha)) (iohmm-hmix-lite.stan:468-471, Q10). */
+static void iohmm_oblik_t(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    for (int t = 0; t < T; ++t) {
+        for (int k = 0; k < K; ++k)
+            c->acc[k] = OR_LOG(TK(c->alpha, t, k)) + TK(c->oblik, t, k);
+        c->oblik_t[t] = stan_log_sum_exp(c->acc, K);
+    }
+}
+
+/* iohmm-mix/stan/iohmm-hmix.stan */
+static void model_iohmm_hmix(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    iohmm_log_transitions(c);                                   /* :232-244 */
+    iohmm_mixture_oblik(c);                                     /* :246-258 */
+    iohmm_forward(c, 1);                                        /* :260-275 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :277-278 */
+    iohmm_backward(c, 1);                                       /* :281-300 */
+    gq_softmax_rows(c->unbeta, c->beta, T, K);                  /* :302-303 */
+    for (int t = 0; t < T; ++t) {                               /* :306-312 */
+        for (int k = 0; k < K; ++k)
+            TK(c->ungamma, t, k) = TK(c->alpha, t, k) * TK(c->beta, t, k);
+        const double s = stan_sum_vec(&TK(c->ungamma, t, 0), K);
+        for (int k = 0; k < K; ++k)
+            TK(c->gamma, t, k) = TK(c->ungamma, t, k) / s;
+    }
+    iohmm_oblik_t(c);                                           /* :314-317 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :330 */
+    iohmm_viterbi(c, 1, 1);                                     /* :356-389 */
+}
+
+/* iohmm-mix/stan/iohmm-hmix-lite.stan */
+static void model_iohmm_hmix_lite(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    iohmm_log_transitions(c);                                   /* :422-434 */
+    iohmm_mixture_oblik(c);                                     /* :436-448 */
+    iohmm_forward(c, 1);                                        /* :450-466 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* softmax in :470 */
+    iohmm_oblik_t(c);                                           /* :468-471 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :484 */
+}
+
+/* ------------------------------------------------------------------ */
+/* tayal2009/stan -- flattened HHMM with sign-masked transitions         */
+/* ------------------------------------------------------------------ */
+
+/* Expansion p_1k / A_ij from p_11, A_row (hhmm-tayal2009.stan:30-44). */
+static void tayal_expand(pair_ctx *c, double p11, const double Arow[2][2])
+{
+    const int K = 4;
+    for (int k = 0; k < K; ++k)
+        c->p[k] = 0;
+    c->p[0] = p11;
+    c->p[2] = 1 - p11;
+    for (int k = 0; k < K * K; ++k)
+        c->A[k] = 0;
+    c->A[0 * K + 1] = Arow[0][0];
+    c->A[0 * K + 2] = Arow[0][1];
+    c->A[1 * K + 0] = 1;
+    c->A[2 * K + 0] = Arow[1][0];
+    c->A[2 * K + 3] = Arow[1][1];
+    c->A[3 * K + 2] = 1;
+}
+
+static int tayal_pred(int sign, int j1)
+{
+    /* hhmm-tayal2009.stan:62 / :109 / :144 (j1 is 1-based) */
+    return (sign == 1 && (j1 == 2 || j1 == 3)) || (sign == 2 && (j1 == 1 || j1 == 4));
+}
+
+static int tayal_init_pred(int sign, int j1)
+{
+    return (sign == 1 && j1 == 3) || (sign == 2 && j1 == 1); /* :51 */
+}
+
+/* Tayal forward over (x, sign) of length T into un (hhmm-tayal2009.stan:46-70). */
+static void tayal_forward(pair_ctx *c, const int32_t *x, const int32_t *sg, int T, double *un)
+{
+    const int K = c->K;
+    double *acc = c->acc;
+    for (int j = 0; j < K; ++j) {
+        TK(un, 0, j) = OR_LOG(PHI(j, x[0] - 1));
+        if (tayal_init_pred(sg[0], j + 1))
+            TK(un, 0, j) = TK(un, 0, j) + OR_LOG(c->p[j]);
+    }
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i) {
+                acc[i] = TK(un, t - 1, i) + OR_LOG(PHI(j, x[t] - 1));
+                if (tayal_pred(sg[t], j + 1))
+                    acc[i] = acc[i] + OR_LOG(c->A[i * K + j]);
+            }
+            TK(un, t, j) = stan_log_sum_exp(acc, K);
+        }
+}
+
+/* Tayal Viterbi over (x, sign) (hhmm-tayal2009.stan:130-165; lite :289-324). */
+static void tayal_viterbi(pair_ctx *c, const int32_t *x, const int32_t *sg, int T)
+{
+    const int K = c->K;
+    viterbi_reset(c, T);
+    for (int j = 0; j < K; ++j)
+        TK(c->delta, 0, K - 1) = OR_LOG(PHI(j, x[0] - 1));
+    for (int t = 1; t < T; ++t)
+        for (int j = 0; j < K; ++j) {
+            TK(c->delta, t, j) = NEG_INF;
+            for (int i = 0; i < K; ++i) {
+                double logp = TK(c->delta, t - 1, i) + OR_LOG(PHI(j, x[t] - 1));
+                if (tayal_pred(sg[t], j + 1))
+                    logp = logp + OR_LOG(c->A[i * K + j]);
+                if (logp > TK(c->delta, t, j)) {
+                    TK(c->bp, t, j) = i + 1;
+                    TK(c->delta, t, j) = logp;
+                }
+            }
+        }
+    viterbi_finish(c, T);
+}
+
+static void model_tayal(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    double *acc = c->acc;
+    tayal_forward(c, c->x, c->sgn, T, c->unalpha);              /* :46-70 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :74 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :88-91 */
+    /* backward, :93-119 (predicate on j = previous state, Q6) */
+    for (int j = 0; j < K; ++j)
+        TK(c->unbeta, T - 1, j) = 1;
+    for (int tf = 0; tf <= T - 2; ++tf) {
+        const int t = T - 1 - tf;
+        for (int j = 0; j < K; ++j) {
+            for (int i = 0; i < K; ++i) {
+                acc[i] = TK(c->unbeta, t, i) + OR_LOG(PHI(i, c->x[t] - 1));
+                if (tayal_pred(c->sgn[t], j + 1))
+                    acc[i] = acc[i] + OR_LOG(c->A[j * K + i]);
+            }
+            TK(c->unbeta, t - 1, j) = stan_log_sum_exp(acc, K);
+        }
+    }
+    gq_softmax_rows(c->unbeta, c->beta, T, K);
+    gq_gamma(c);                          /* :121-128 */
+    tayal_viterbi(c, c->x, c->sgn, T);    /* :130-165 */
+}
+
+static void model_tayal_lite(pair_ctx *c)
+{
+    const int K = c->K, T = c->T;
+    tayal_forward(c, c->x, c->sgn, T, c->unalpha);              /* lite :216-240 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :244 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :255-258 */
+    tayal_forward(c, c->x_oos, c->sgn_oos, c->T_oos, c->unalpha_oos); /* :260-283 */
+    gq_softmax_rows(c->unalpha_oos, c->alpha_oos, c->T_oos, K);       /* :285-286 */
+    tayal_viterbi(c, c->x_oos, c->sgn_oos, c->T_oos);                 /* :289-324 */
+}
+
+/* ------------------------------------------------------------------ */
+/* Batch driver                                                         */
+/* ------------------------------------------------------------------ */
+
+static int64_t num_pairs(const hhmm_request *r)
+{
+    if (r->pairing == HHMM_PAIR_ZIP)
+        return r->data.n_series == r->draws.n_draws ? r->data.n_series : -1;
+    return r->data.n_series * r->draws.n_draws;
+}
+
+static void gather(pair_ctx *c, const hhmm_request *r, int64_t n, int64_t s)
+{
+    const hhmm_data *d = &r->data;
+    const hhmm_draws *w = &r->draws;
+    const int64_t N = d->n_series, S = w->n_draws;
+    const int K = c->K, L = c->L, M = c->M;
+    const int Tm = d->T_max;
+    for (int t = 0; t < c->T; ++t) {
+        const size_t ix = (size_t)n + (size_t)N * t;
+        if (d->x_int) c->x[t] = d->x_int[ix];
+        if (d->x_real) c->xr[t] = d->x_real[ix];
+        if (d->g) c->g[t] = d->g[ix];
+        if (d->sign) c->sgn[t] = d->sign[ix];
+        if (d->u)
+            for (int m = 0; m < M; ++m)
+                c->u[(size_t)t * M + m] = d->u[(size_t)n + (size_t)N * ((size_t)t + (size_t)Tm * m)];
+    }
+    for (int t = 0; t < c->T_oos; ++t) {
+        const size_t ix = (size_t)n + (size_t)N * t;
+        c->x_oos[t] = d->x_oos[ix];
+        c->sgn_oos[t] = d->sign_oos[ix];
+    }
+#define DRAW1(arr, k) ((arr)[(size_t)s + (size_t)S * (size_t)(k)])
+#define DRAW2(arr, a, b, A_) ((arr)[(size_t)s + (size_t)S * ((size_t)(a) + (size_t)(A_) * (size_t)(b))])
+    if (w->p_1k) for (int k = 0; k < K; ++k) c->p[k] = DRAW1(w->p_1k, k);
+    if (w->A_ij) for (int i = 0; i < K; ++i) for (int j = 0; j < K; ++j) c->A[i * K + j] = DRAW2(w->A_ij, i, j, K);
+    if (w->phi_k) for (int k = 0; k < K; ++k) for (int l = 0; l < L; ++l) c->phi[k * L + l] = DRAW2(w->phi_k, k, l, K);
+    if (w->mu_k) for (int k = 0; k < K; ++k) c->mu[k] = DRAW1(w->mu_k, k);
+    if (w->sigma_k) for (int k = 0; k < K; ++k) c->sigma[k] = DRAW1(w->sigma_k, k);
+    if (w->w_km) for (int k = 0; k < K; ++k) for (int m = 0; m < M; ++m) c->w[k * M + m] = DRAW2(w->w_km, k, m, K);
+    if (w->b_km) for (int k = 0; k < K; ++k) for (int m = 0; m < M; ++m) c->b[k * M + m] = DRAW2(w->b_km, k, m, K);
+    if (w->s_k) for (int k = 0; k < K; ++k) c->sk[k] = DRAW1(w->s_k, k);
+    if (w->lambda_kl) for (int k = 0; k < K; ++k) for (int l = 0; l < L; ++l) c->lambda[k * L + l] = DRAW2(w->lambda_kl, k, l, K);
+    if (w->mu_kl) for (int k = 0; k < K; ++k) for (int l = 0; l < L; ++l) c->mukl[k * L + l] = DRAW2(w->mu_kl, k, l, K);
+    if (w->s_kl) for (int k = 0; k < K; ++k) for (int l = 0; l < L; ++l) c->skl[k * L + l] = DRAW2(w->s_kl, k, l, K);
+    if (r->model == HHMM_MODEL_TAYAL || r->model == HHMM_MODEL_TAYAL_LITE) {
+        double ar[2][2];
+        for (int a = 0; a < 2; ++a)
+            for (int b2 = 0; b2 < 2; ++b2)
+                ar[a][b2] = DRAW2(w->A_row, a, b2, 2);
+        tayal_expand(c, DRAW1(w->p_11, 0), ar);
+    }
+#undef DRAW1
+#undef DRAW2
+}
+
+static void scatter(const pair_ctx *c, const hhmm_request *r, hhmm_result *o, int64_t p, int64_t P)
+{
+    const uint32_t out = r->outputs;
+    const int K = c->K, T = c->T, Tm = r->data.T_max, To = r->data.T_oos_max;
+#define PTK(arr, t, k, TT) (arr)[(size_t)p + (size_t)P * ((size_t)(t) + (size_t)(TT) * (size_t)(k))]
+#define PUT_TK(bit, dst, src)                                     \
+    if ((out & (bit)) && (dst))                                   \
+        for (int t = 0; t < T; ++t)                               \
+            for (int k = 0; k < K; ++k)                           \
+                PTK(dst, t, k, Tm) = src[(size_t)t * K + k];
+    if ((out & HHMM_OUT_LOGLIK) && o->loglik)
+        o->loglik[p] = c->loglik;
+    PUT_TK(HHMM_OUT_UNALPHA, o->unalpha_tk, c->unalpha)
+    PUT_TK(HHMM_OUT_ALPHA, o->alpha_tk, c->alpha)
+    PUT_TK(HHMM_OUT_UNBETA, o->unbeta_tk, c->unbeta)
+    PUT_TK(HHMM_OUT_BETA, o->beta_tk, c->beta)
+    PUT_TK(HHMM_OUT_UNGAMMA, o->ungamma_tk, c->ungamma)
+    PUT_TK(HHMM_OUT_GAMMA, o->gamma_tk, c->gamma)
+    PUT_TK(HHMM_OUT_OBLIK_TK, o->oblik_tk, c->oblik)
+    if ((out & HHMM_OUT_LOGA) && o->logA_ij) {
+        const double *src = (r->model == HHMM_MODEL_IOHMM_HMIX || r->model == HHMM_MODEL_IOHMM_HMIX_LITE)
+                                ? c->logA : c->Arow;
+        PUT_TK(HHMM_OUT_LOGA, o->logA_ij, src)
+    }
+    if ((out & HHMM_OUT_OBLIK_T) && o->oblik_t)
+        for (int t = 0; t < T; ++t)
+            o->oblik_t[(size_t)p + (size_t)P * t] = c->oblik_t[t];
+    const int Tz = (r->model == HHMM_MODEL_TAYAL_LITE) ? c->T_oos : T;
+    if ((out & HHMM_OUT_ZSTAR) && o->zstar_t)
+        for (int t = 0; t < Tz; ++t)
+            o->zstar_t[(size_t)p + (size_t)P * t] = c->zstar[t];
+    if ((out & HHMM_OUT_LOGP_ZSTAR) && o->logp_zstar)
+        o->logp_zstar[p] = c->logp_zstar;
+    if (r->model == HHMM_MODEL_TAYAL_LITE) {
+        if ((out & HHMM_OUT_ALPHA_OOS) && o->alpha_tk_oos)
+            for (int t = 0; t < c->T_oos; ++t)
+                for (int k = 0; k < K; ++k)
+                    PTK(o->alpha_tk_oos, t, k, To) = c->alpha_oos[(size_t)t * K + k];
+        if ((out & HHMM_OUT_UNALPHA_OOS) && o->unalpha_tk_oos)
+            for (int t = 0; t < c->T_oos; ++t)
+                for (int k = 0; k < K; ++k)
+                    PTK(o->unalpha_tk_oos, t, k, To) = c->unalpha_oos[(size_t)t * K + k];
+    }
+    if (o->pair_status)
+        o->pair_status[p] = c->status;
+#undef PUT_TK
+#undef PTK
+}
+
+static void run_pair(pair_ctx *c, const hhmm_request *r)
+{
+    switch (r->model) {
+    case HHMM_MODEL_HMM_GAUSS: model_hmm_gauss(c); break;
+    case HHMM_MODEL_HMM_MULTINOM: model_hmm_multinom(c); break;
+    case HHMM_MODEL_HMM_MULTINOM_SEMISUP: model_hmm_multinom_semisup(c); break;
+    case HHMM_MODEL_IOHMM_REG: model_iohmm_reg(c); break;
+    case HHMM_MODEL_IOHMM_MIX: model_iohmm_mix(c); break;
+    case HHMM_MODEL_IOHMM_HMIX: model_iohmm_hmix(c); break;
+    case HHMM_MODEL_IOHMM_HMIX_LITE: model_iohmm_hmix_lite(c); break;
+    case HHMM_MODEL_TAYAL: model_tayal(c); break;
+    case HHMM_MODEL_TAYAL_LITE: model_tayal_lite(c); break;
+    default: break;
+    }
+}
+
+/* Runs pairs [p0, p1) of the request; nthreads <= 0 uses the OpenMP default.
+ * Returns 0, or 1 if some pair failed its Viterbi backtrack, or -1 on a bad request. */
+int hhmm_oracle_run_range(const hhmm_request *r, hhmm_result *o, int64_t p0, int64_t p1, int nthreads)
+{
+    const int64_t P = num_pairs(r);
+    if (P < 0 || r->model < 1 || r->model > 9)
+        return -1;
+    if (p1 > P)
+        p1 = P;
+    const int K = r->data.K;
+    const int L = r->data.L, M = r->data.M;
+    int failures = 0;
+#ifdef _OPENMP
+    if (nthreads > 0)
+        omp_set_num_threads(nthreads);
+#pragma omp parallel reduction(+ : failures)
+#endif
+    {
+        pair_ctx c;
+        ctx_alloc(&c, K, L, M, r->data.T_max, r->data.T_oos_max);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 16)
+#endif
+        for (int64_t p = p0; p < p1; ++p) {
+            const int64_t S = r->draws.n_draws;
+            const int64_t n = (r->pairing == HHMM_PAIR_ZIP) ? p : p / S;
+            const int64_t s = (r->pairing == HHMM_PAIR_ZIP) ? p : p % S;
+            c.K = K;
+            c.L = L;
+            c.M = M;
+            c.T = r->data.T ? r->data.T[n] : r->data.T_max;
+            c.T_oos = (r->model == HHMM_MODEL_TAYAL_LITE)
+                          ? (r->data.T_oos ? r->data.T_oos[n] : r->data.T_oos_max) : 0;
+            c.status = 0;
+            c.loglik = NAN;
+            c.logp_zstar = NAN;
+            gather(&c, r, n, s);
+            run_pair(&c, r);
+            if (c.status)
+                failures += 1;
+            scatter(&c, r, o, p, P);
+        }
+        ctx_free(&c);
+    }
+    return failures ? 1 : 0;
+}
+
+int hhmm_oracle_run(const hhmm_request *r, hhmm_result *o, int nthreads)
+{
+    return hhmm_oracle_run_range(r, o, 0, INT64_MAX, nthreads);
+}
+
+/* The oracle's log (correctly rounded unless built with HHMM_ORACLE_LIBM_LOG). */
+void hhmm_oracle_log_array(const double *in, double *out, int64_t n)
+{
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = OR_LOG(in[i]);
+}
+
+const char *hhmm_oracle_variant(void)
+{
+#ifdef HHMM_ORACLE_LIBM_LOG
+    return "libm-log";
+#else
+    return "cr-log";
+#endif
+}

@@ -1,0 +1,74 @@
+"""ctypes loader for the CPU oracle (oracle/hhmm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker or the timed CPU baseline.  It
+uses the product's request builder (hhmm_amd.api.PreparedRequest) so both
+sides see byte-identical inputs, and returns results in the same layout.
+"""
+import ctypes as C
+import pathlib
+import subprocess
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent
+REPO = ROOT.parent
+sys.path.insert(0, str(REPO / "gsoc17-hhmm_amd"))
+
+from hhmm_amd import _abi  # noqa: E402
+from hhmm_amd.api import PreparedRequest  # noqa: E402
+
+_LIBS = {}
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(ROOT)], check=True)
+
+
+def load(variant="cr"):
+    """variant 'cr': correctly rounded log (the checker); 'libm': host libm log."""
+    if variant in _LIBS:
+        return _LIBS[variant]
+    name = {"cr": "liboracle.so", "libm": "liboracle_libm.so"}[variant]
+    path = ROOT / "build" / name
+    if not path.exists():
+        build()
+    lib = C.CDLL(str(path))
+    RP = C.POINTER(_abi.Request)
+    SP = C.POINTER(_abi.Result)
+    lib.hhmm_oracle_run.argtypes = [RP, SP, C.c_int]
+    lib.hhmm_oracle_run.restype = C.c_int
+    lib.hhmm_oracle_run_range.argtypes = [RP, SP, C.c_int64, C.c_int64, C.c_int]
+    lib.hhmm_oracle_run_range.restype = C.c_int
+    lib.hhmm_oracle_log_array.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int64]
+    lib.hhmm_oracle_variant.restype = C.c_char_p
+    _LIBS[variant] = lib
+    return lib
+
+
+def gqs(model, data, draws, pars=None, pairing="grid", nthreads=1, variant="cr", return_status=False,
+        pair_range=None):
+    """Same contract as hhmm_amd.gqs, computed by the scalar CPU oracle."""
+    lib = load(variant)
+    pr = PreparedRequest(model, data, draws, pars, pairing)
+    if pair_range is None:
+        st = lib.hhmm_oracle_run(C.byref(pr.req), C.byref(pr.res), nthreads)
+    else:
+        st = lib.hhmm_oracle_run_range(C.byref(pr.req), C.byref(pr.res), pair_range[0], pair_range[1],
+                                       nthreads)
+    if st < 0:
+        raise RuntimeError(f"oracle rejected the request ({st})")
+    out = dict(pr.out)
+    if return_status:
+        out["pair_status"] = pr.status
+        out["status"] = st
+    return out
+
+
+def log_array(x, variant="cr"):
+    import numpy as np
+    lib = load(variant)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib.hhmm_oracle_log_array(x.ctypes.data_as(C.POINTER(C.c_double)),
+                              y.ctypes.data_as(C.POINTER(C.c_double)), x.size)
+    return y

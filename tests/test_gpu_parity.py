@@ -1,0 +1,115 @@
+"""GPU parity: libhhmm.so (gfx950) against the CPU oracle on identical inputs.
+
+Posteriors / log-likelihoods within the tolerances of tests/tolerances.py;
+Viterbi paths, logp_zstar and pair_status bit-exact (the oracle and the
+device share the correctly rounded log and the reference's operation order).
+"""
+import numpy as np
+import pytest
+
+from hhmm_amd import synth
+from tolerances import compare, compare_all
+
+pytestmark = pytest.mark.gpu
+
+DEVICE_MODELS = ["hmm", "hmm-multinom", "hmm-multinom-semisup", "hhmm-tayal2009", "hhmm-tayal2009-lite"]
+
+
+def run_both(engine, oracle, model, data, draws, pars, pairing="grid"):
+    import hhmm_amd
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, pairing=pairing, lib=engine, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, pairing=pairing, return_status=True)
+    return got, ref
+
+
+def test_cr_log_device_matches_oracle(engine, oracle):
+    import ctypes as C
+    g = np.random.Generator(np.random.Philox(7))
+    bits = g.integers(1, 0x7FF0000000000000, size=200_000, dtype=np.int64).view(np.float64)
+    near1 = 1.0 + (g.random(100_000) - 0.5) * 2.0 ** -6
+    small = g.random(100_000)
+    special = np.array([1.0, 2.0, 0.5, 0.0, -1.0, np.inf, np.nan, 5e-324, 2.2250738585072014e-308,
+                        1.7976931348623157e308, 1 - 2 ** -53, 1 + 2 ** -52])
+    x = np.concatenate([bits, near1, small, special])
+    y = np.empty_like(x)
+    st = engine.hhmm_selftest_cr_log(x.ctypes.data_as(C.POINTER(C.c_double)),
+                                     y.ctypes.data_as(C.POINTER(C.c_double)), x.size)
+    assert st == 0, engine.hhmm_last_error()
+    ref = oracle.log_array(x, "cr")
+    same = (y.view(np.int64) == ref.view(np.int64)) | (np.isnan(y) & np.isnan(ref))
+    assert same.all(), f"{(~same).sum()} device logs differ from the oracle's"
+
+
+CASES = [
+    ("hmm", dict(K=1)), ("hmm", dict(K=2)), ("hmm", dict(K=3)), ("hmm", dict(K=4)), ("hmm", dict(K=6)),
+    ("hmm-multinom", dict(K=1, L=3)), ("hmm-multinom", dict(K=2, L=5)), ("hmm-multinom", dict(K=3, L=5)),
+    ("hmm-multinom", dict(K=4, L=9)), ("hmm-multinom", dict(K=5, L=7)), ("hmm-multinom", dict(K=8, L=9)),
+    ("hmm-multinom-semisup", dict(K=4, L=9)), ("hhmm-tayal2009", dict()), ("hhmm-tayal2009-lite", dict()),
+]
+
+
+@pytest.mark.parametrize("model,kw", CASES, ids=[f"{m}-{'-'.join(f'{k}{v}' for k, v in kw.items())}"
+                                                 for m, kw in CASES])
+@pytest.mark.parametrize("T", [1, 2, 37, 130])
+def test_parity_grid(engine, oracle, model, kw, T):
+    data, draws = synth.GENERATORS[model](N=3, S=70, T=T, **kw)
+    got, ref = run_both(engine, oracle, model, data, draws, synth.PARS[model])
+    compare_all(got, ref, synth.PARS[model] + ["pair_status"])
+    assert got["status"] == ref["status"]
+
+
+@pytest.mark.parametrize("model", DEVICE_MODELS)
+def test_parity_zip_many_pairs(engine, oracle, model):
+    N = 1000
+    data, draws = synth.GENERATORS[model](N=N, S=N, T=64)
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"] if model != "hhmm-tayal2009-lite" else \
+        ["loglik", "alpha_tk", "alpha_tk_oos", "zstar_t", "logp_zstar"]
+    got, ref = run_both(engine, oracle, model, data, draws, pars, pairing="zip")
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+@pytest.mark.parametrize("model", DEVICE_MODELS)
+def test_parity_ragged(engine, oracle, model):
+    N, S, T = 5, 64, 90
+    data, draws = synth.GENERATORS[model](N=N, S=S, T=T)
+    data["T"] = np.array([90, 1, 17, 64, 33], dtype=np.int32)
+    if "x_oos" in data:
+        data["T_oos"] = np.array([3, 48, 1, 20, 47], dtype=np.int32)
+    pars = synth.PARS[model]
+    import hhmm_amd
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, return_status=True)
+    # entries past a series' length are not written by either side (NaN-prefilled)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+def test_invalid_backpointer_flagged(engine, oracle):
+    """All delta_T = -inf (an impossible observation under every state):
+    Stan would throw while backtracking; the pair is flagged, zstar zeroed."""
+    data, draws = synth.hmm_multinom(N=1, S=4, T=12, K=3, L=4)
+    draws["phi_k"][:, :, 3] = 0.0
+    draws["phi_k"] /= draws["phi_k"].sum(axis=2, keepdims=True)
+    data["x"][0, 7] = 4
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    got, ref = run_both(engine, oracle, "hmm-multinom", data, draws, pars)
+    assert (ref["pair_status"] == 1).all() and ref["status"] == 1
+    compare_all(got, ref, pars + ["pair_status"])
+    assert got["status"] == 1
+
+
+def test_deterministic_emissions_recover_path(engine):
+    """KAT (hmm/main-multinom-semisup.R:31-35: B = identity rows): with
+    noise-free emissions the Viterbi path is the observed symbol sequence,
+    except zstar[1] = K from the Q3 initialisation quirk."""
+    import hhmm_amd
+    K, L, T = 4, 4, 50
+    g = np.random.Generator(np.random.Philox(3))
+    z = g.integers(1, K + 1, size=T)
+    z[0] = K  # otherwise delta_1 = (NaN, .., log 0): every path is -inf and Stan throws
+    data = {"K": K, "L": L, "x": z.reshape(1, T)}
+    draws = {"p_1k": np.full((1, K), 0.25), "A_ij": np.full((1, K, K), 0.25),
+             "phi_k": np.eye(K).reshape(1, K, L)}
+    out = hhmm_amd.gqs("hmm-multinom", data, draws, pars=["zstar_t"], lib=engine)
+    path = out["zstar_t"][0]
+    assert path[0] == K
+    assert np.array_equal(path[1:], z[1:])

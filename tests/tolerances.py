@@ -1,0 +1,50 @@
+"""Parity tolerances (north_star: 1e-9 relative in fp64; paths bit-exact).
+
+* probability-space outputs (alpha, beta, gamma, ungamma): |a - b| <= 1e-9 |b| + 1e-250.
+  The reference normalises in probability space, so components below ~1e-308
+  flush to 0; the floor keeps such underflow from counting.
+* log-space outputs (loglik, unalpha, unbeta, logp_zstar, oblik): |a - b| <= 1e-9 max(|b|, 1).
+  A relative error is meaningless for a log-density near 0; 1e-9 absolute in
+  log space is 1e-9 relative in probability.
+* NaN / +-inf must sit in the same places on both sides.
+* integer outputs (zstar_t, z_ffbs, pair_status): exact.
+"""
+import numpy as np
+
+PROB = {"alpha_tk", "beta_tk", "gamma_tk", "ungamma_tk", "alpha_tk_oos"}
+LOG = {"loglik", "unalpha_tk", "unbeta_tk", "logp_zstar", "oblik_tk", "oblik_t", "unalpha_tk_oos", "logA_ij"}
+INT = {"zstar_t", "z_ffbs", "pair_status"}
+RTOL = 1e-9
+
+
+def compare(name, got, ref):
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    assert got.shape == ref.shape, (name, got.shape, ref.shape)
+    if name in INT:
+        bad = np.flatnonzero((got != ref).ravel(order="F"))
+        assert bad.size == 0, f"{name}: {bad.size} mismatches, first at flat index {bad[:5]}"
+        return
+    gn, rn = np.isnan(got), np.isnan(ref)
+    assert np.array_equal(gn, rn), f"{name}: NaN placement differs ({gn.sum()} vs {rn.sum()})"
+    gi, ri = np.isinf(got), np.isinf(ref)
+    assert np.array_equal(gi, ri) and np.array_equal(got[gi], ref[ri]), f"{name}: inf placement differs"
+    m = ~(gn | gi)
+    g, r = got[m], ref[m]
+    if name in PROB:
+        tol = RTOL * np.abs(r) + 1e-250
+    elif name in LOG:
+        tol = RTOL * np.maximum(np.abs(r), 1.0)
+    else:
+        raise KeyError(name)
+    err = np.abs(g - r)
+    worst = int(np.argmax(err - tol)) if err.size else 0
+    assert np.all(err <= tol), (f"{name}: max err {err.max():.3e} exceeds tolerance "
+                                f"(got {g[worst]!r}, ref {r[worst]!r})")
+
+
+def compare_all(got, ref, names=None):
+    for k in names or ref:
+        if k in ("status",):
+            continue
+        compare(k, got[k], ref[k])
