@@ -1,0 +1,316 @@
+#!/usr/bin/env python3
+"""Benchmark: series-timesteps/s of forward-backward + gamma + Viterbi (K=4).
+
+Workload (BASELINE.json configs[1], the metric's single-GPU config C2):
+hmm/stan/hmm-multinom.stan, K=4, L=9, 1,000,000 (series, draw) pairs
+(one posterior draw per series, HHMM_PAIR_ZIP) x T=1000, fp64.  One step =
+one pass of the hot path over the whole batch with inputs resident in HBM:
+libhhmm's fb_kernel (alpha/beta/gamma + loglik) and viterbi_kernel
+(zstar + logp_zstar), launched through the C ABI (hhmm_run_device) on
+torch's current stream.  Outputs: gamma_tk [P,T,K], zstar_t [P,T],
+loglik [P], logp_zstar [P].
+
+Multi-GPU (torch.distributed.run, one process per GPU): every rank evaluates
+its own 1M pairs (weak scaling, no data-path collective); the per-step
+summed log-likelihood is all-reduced over RCCL (the path's only exchange).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+`roofline` for the dominant kernel (HIP events on the launch stream) and
+`cpu_baseline` (the stanc-faithful CPU oracle, libm log, timed on a bounded
+sample of the same workload on the host cores).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "gsoc17-hhmm_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import hhmm_amd  # noqa: E402
+from hhmm_amd import _abi, synth  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU")
+    ap.add_argument("--T", type=int, default=1000)
+    ap.add_argument("--seed", type=int, default=synth.SEED)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="also check a slice against the oracle")
+    return ap.parse_args()
+
+
+K, L = 4, 9
+
+
+def make_batch(P, T, seed, dev):
+    """Synthetic C2 batch on the device.  x from the true HMM of
+    hmm/main-multinom-semisup.R:12-17 with emission rows normalize(1 + 9 e_k);
+    one posterior draw per series, jittered as in hhmm_amd.synth."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    A = torch.tensor(synth.A_SEMISUP, device=dev)
+    p1 = torch.tensor(synth.P1_SEMISUP, device=dev)
+    B = torch.tensor(synth.smoothed_identity(K, L), device=dev)
+    cA, cB, cp = A.cumsum(1), B.cumsum(1), p1.cumsum(0)
+    # x: [N, T] column-major (series fastest) == torch (T, N) row-major
+    x = torch.empty((T, P), dtype=torch.int32, device=dev)
+    z = torch.searchsorted(cp, torch.rand(P, generator=g, device=dev, dtype=torch.float64) * cp[-1])
+    z = z.clamp_(max=K - 1)
+    for t in range(T):
+        if t > 0:
+            rows = cA[z]
+            u = torch.rand(P, 1, generator=g, device=dev, dtype=torch.float64) * rows[:, -1:]
+            z = (u >= rows).sum(1).clamp_(max=K - 1)
+        rb = cB[z]
+        u = torch.rand(P, 1, generator=g, device=dev, dtype=torch.float64) * rb[:, -1:]
+        x[t] = ((u >= rb).sum(1).clamp_(max=L - 1) + 1).to(torch.int32)
+
+    def dirichlet_rows(rows, S):
+        # rows (R, C) -> F-order [S, R, C] == torch (C, R, S)
+        conc = 200.0 * rows + 1.0
+        out = torch.empty((rows.shape[1], rows.shape[0], S), dtype=torch.float64, device=dev)
+        for r in range(rows.shape[0]):
+            gam = torch._standard_gamma(conc[r].expand(S, -1).contiguous(), generator=g)
+            out[:, r, :] = (gam / gam.sum(1, keepdim=True)).T
+        return out
+
+    draws = {
+        "p_1k": dirichlet_rows(p1[None, :], P),          # (K, 1, S)
+        "A_ij": dirichlet_rows(A, P),                     # (K, K, S)
+        "phi_k": dirichlet_rows(B, P),                    # (L, K, S)
+    }
+    return x, draws
+
+
+class DeviceRun:
+    """Holds device buffers and two prepared requests (FB and Viterbi)."""
+
+    def __init__(self, lib, x, draws, P, T, dev):
+        self.lib = lib
+        self.out = {
+            "loglik": torch.empty(P, dtype=torch.float64, device=dev),
+            "gamma_tk": torch.empty((K, T, P), dtype=torch.float64, device=dev),
+            "zstar_t": torch.empty((T, P), dtype=torch.int32, device=dev),
+            "logp_zstar": torch.empty(P, dtype=torch.float64, device=dev),
+            "pair_status": torch.zeros(P, dtype=torch.int32, device=dev),
+        }
+        self.reqs = {}
+        for name, outs in (("fb", ["loglik", "gamma_tk"]), ("viterbi", ["zstar_t", "logp_zstar"])):
+            r = _abi.Request()
+            r.abi_version = _abi.ABI_VERSION
+            r.model = _abi.MODELS["hmm-multinom"]
+            r.pairing = _abi.PAIR_ZIP
+            r.device = -1
+            r.data.n_series = P
+            r.data.T_max = T
+            r.data.K = K
+            r.data.L = L
+            r.data.x_int = x.data_ptr()
+            r.draws.n_draws = P
+            for k, v in draws.items():
+                setattr(r.draws, k, v.data_ptr())
+            res = _abi.Result()
+            for o in outs:
+                r.outputs |= _abi.OUT[o]
+                setattr(res, o, self.out[o].data_ptr())
+            res.pair_status = self.out["pair_status"].data_ptr()
+            ws = C.c_size_t(0)
+            assert lib.hhmm_workspace_size(C.byref(r), C.byref(ws)) == 0
+            wsbuf = torch.empty(max(int(ws.value), 256), dtype=torch.uint8, device=dev)
+            self.reqs[name] = (r, res, wsbuf)
+
+    def launch(self, name):
+        r, res, ws = self.reqs[name]
+        st = self.lib.hhmm_run_device(C.byref(r), C.byref(res), ws.data_ptr(), ws.numel(),
+                                      torch.cuda.current_stream().cuda_stream)
+        if st != 0:
+            raise RuntimeError(self.lib.hhmm_last_error().decode())
+
+
+def bytes_per_step(T):
+    """Algorithmic (compulsory) bytes per series-timestep, SURVEY.md §8d (C2)."""
+    params = (K + K * K + K * L) * 8  # p_1k, A_ij, phi_k per pair
+    fb = 4 + K * 8 + (params + 8) / T          # x, gamma, params, loglik
+    vit = 4 + 4 + (K * K + K * L) * 8 / T + 8 / T  # x, zstar, A/phi, logp
+    whole = 4 + K * 8 + 4 + (params + 16) / T  # x once, gamma, zstar, params, loglik+logp
+    return fb, vit, whole
+
+
+def cpu_baseline(T, target_s, seed):
+    """Stanc-faithful CPU oracle (libm log, in-loop log/LSE as Stan) on a
+    bounded sample of the same workload (same shapes, host cores)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    n = 8 * threads
+    data, draws = synth.hmm_multinom(N=n, S=n, T=T, K=K, L=L, seed=seed)
+    pyoracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", nthreads=threads, variant="libm")
+    t0 = time.perf_counter()
+    pyoracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", nthreads=threads, variant="libm")
+    dt = time.perf_counter() - t0
+    n2 = int(max(n, min(200_000, n * target_s / max(dt, 1e-3))))
+    n2 = (n2 // threads) * threads or threads
+    data, draws = synth.hmm_multinom(N=n2, S=n2, T=T, K=K, L=L, seed=seed + 1)
+    t0 = time.perf_counter()
+    pyoracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", nthreads=threads, variant="libm")
+    dt = time.perf_counter() - t0
+    return {"value": n2 * T / dt, "unit": "series-timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{n2} pairs x T={T} (hmm-multinom K=4 L=9, zip), FB+gamma+Viterbi, "
+                      f"{dt:.1f} s on {threads} threads, oracle libm-log build"}
+
+
+def load_traffic(tag):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass
+    (profiles/<tag>_pmc.json, written by tools/pmc_summary.py) or None."""
+    p = ROOT / "profiles" / f"{tag}_pmc.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text())
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    lib = hhmm_amd.load_library()
+    assert lib.hhmm_init(1) == 0, lib.hhmm_last_error().decode()
+
+    P, T = a.pairs, a.T
+    x, draws = make_batch(P, T, a.seed + 7919 * rank, dev)
+    run = DeviceRun(lib, x, draws, P, T, dev)
+    torch.cuda.synchronize()
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        run.launch("fb")
+        if ev:
+            ev[1].record()
+        run.launch("viterbi")
+        if ev:
+            ev[2].record()
+        if world > 1:
+            import torch.distributed as dist
+            s = run.out["loglik"].sum().reshape(1)
+            dist.all_reduce(s)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if a.check:
+        check_slice(run, x, draws, P, T)
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    fb_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    vit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    bad = int((run.out["pair_status"] != 0).sum().item())
+
+    if rank == 0:
+        fb_b, vit_b, whole_b = bytes_per_step(T)
+        units = P * T
+        if fb_ms >= vit_ms:
+            dom, dom_ms, dom_b = "fb_kernel", fb_ms, fb_b
+        else:
+            dom, dom_ms, dom_b = "viterbi_kernel", vit_ms, vit_b
+        achieved = dom_b * units / (dom_ms * 1e-3)
+        pmc = load_traffic("r01")
+        traffic = None
+        if pmc and pmc.get("kernel") == dom and pmc.get("pairs") == P and pmc.get("T") == T:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        value = world * units * a.steps / elapsed
+        line = {
+            "metric": "series-timesteps/sec forward-backward+Viterbi (K=4) at 1/2/4/8 GPU; % HBM roofline",
+            "value": value,
+            "unit": "series-timesteps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded HMM of hmm/main-multinom-semisup.R, Dirichlet-jittered draws)",
+            "config": {"workload": "C2 hmm-multinom K=4 L=9, 1M pairs x T=1000 per GPU (zip pairing)",
+                       "pairs_per_gpu": P, "T": T, "outputs": "gamma_tk zstar_t loglik logp_zstar",
+                       "parallelism": f"pairs sharded over {world} GPU(s)"},
+            "whole_step_roofline_frac": whole_b * world * units * a.steps / elapsed / (HBM_PEAK * world),
+            "kernels_ms": {"fb_kernel": fb_ms, "viterbi_kernel": vit_ms},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                         "traffic": traffic, "algorithmic_bytes_per_series_timestep": dom_b},
+            "pair_failures": bad,
+        }
+        if not a.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(T, a.cpu_seconds, a.seed)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def check_slice(run, x, draws, P, T):
+    """Compares the first 64 pairs with the oracle (test infrastructure)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import pyoracle
+    from tolerances import compare
+    n = min(64, P)
+    data = {"K": K, "L": L, "x": x[:, :n].T.cpu().numpy()}
+    dr = {k: v[..., :n].permute(*reversed(range(v.dim()))).cpu().numpy() for k, v in draws.items()}
+    dr["p_1k"] = dr["p_1k"][:, 0, :]
+    ref = pyoracle.gqs("hmm-multinom", data, dr, pars=["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
+                       pairing="zip", nthreads=8)
+    got = {
+        "loglik": run.out["loglik"][:n].cpu().numpy(),
+        "logp_zstar": run.out["logp_zstar"][:n].cpu().numpy(),
+        "zstar_t": run.out["zstar_t"][:, :n].T.cpu().numpy(),
+        "gamma_tk": run.out["gamma_tk"][:, :, :n].permute(2, 1, 0).cpu().numpy(),
+    }
+    for k in got:
+        compare(k, got[k], ref[k])
+    print(f"check: first {n} pairs match the oracle", file=sys.stderr, flush=True)
+
+
+if __name__ == "__main__":
+    main()

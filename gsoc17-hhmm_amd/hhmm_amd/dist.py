@@ -1,0 +1,95 @@
+"""Multi-GPU sharding of a batch of (series x draw) pairs.
+
+One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI).
+Pairs are independent -- the reference itself runs one fit per series and
+parallelises fits over worker processes (tayal2009/R/wf-trade.R:30-34) -- so
+each rank evaluates a contiguous block of SERIES under all S draws, with no
+collective on the data path.  The only exchanges are the ones the north star
+names: an all-reduce of the per-draw summed log-likelihood and a gather of
+the decoded Viterbi paths to rank 0.
+
+`compute` defaults to hhmm_amd.gqs (the gfx950 engine); tests inject the CPU
+oracle to exercise the same orchestration under the gloo backend.
+"""
+import numpy as np
+
+
+def shard_range(n, world, rank):
+    """Contiguous [begin, end) block of n items for `rank` (sizes differ by <= 1)."""
+    q, r = divmod(n, world)
+    begin = rank * q + min(rank, r)
+    return begin, begin + q + (1 if rank < r else 0)
+
+
+_SERIES_KEYS = ("x", "x_t", "g", "sign", "u_tm", "T", "x_oos", "sign_oos", "T_oos")
+
+
+def slice_series(data, b, e):
+    """The data block restricted to series [b, e) (series is the first axis)."""
+    out = {}
+    for k, v in data.items():
+        if k in _SERIES_KEYS:
+            a = np.asarray(v)
+            if k in ("T", "T_oos"):
+                out[k] = a.reshape(-1)[b:e]
+            elif a.ndim >= 2 or k in ("x", "x_t", "g", "sign", "x_oos", "sign_oos"):
+                a = np.atleast_2d(a) if k != "u_tm" else (a if a.ndim == 3 else a[None])
+                out[k] = a[b:e]
+            else:
+                out[k] = a
+        else:
+            out[k] = v
+    return out
+
+
+def slice_draws(draws, b, e):
+    return {k: np.asarray(v)[b:e] for k, v in draws.items()}
+
+
+def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=None, device=None):
+    """Evaluates this rank's shard and performs the two exchanges.
+
+    Returns (local, summed_loglik, paths):
+      local          this rank's outputs (pairs of its series block, ABI order)
+      summed_loglik  [S] per-draw log-likelihood summed over ALL series (all-reduce)
+      paths          on rank 0: zstar_t of every pair in global ABI order, else None
+    """
+    import torch
+    import torch.distributed as dist
+
+    if compute is None:
+        from .api import gqs as compute
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    xkey = "x_t" if model.startswith("iohmm") else "x"
+    N = np.atleast_2d(np.asarray(data[xkey])).shape[0] if np.asarray(data[xkey]).ndim > 1 or \
+        not model.startswith("iohmm") else 1
+    S = next(np.asarray(v).shape[0] for v in draws.values())
+    b, e = shard_range(N, world, rank)
+    ldata = slice_series(data, b, e)
+    ldraws = draws if pairing == "grid" else slice_draws(draws, b, e)
+    local = compute(model, ldata, ldraws, pars=pars, pairing=pairing) if e > b else {}
+
+    dev = device if device is not None else torch.device("cpu")
+    summed = None
+    if "loglik" in pars:
+        s_len = S if pairing == "grid" else N
+        acc = torch.zeros(s_len, dtype=torch.float64, device=dev)
+        if e > b:
+            ll = np.asarray(local["loglik"])
+            if pairing == "grid":  # pair p = s + S*n -> (S, n_local)
+                acc += torch.from_numpy(ll.reshape((S, e - b), order="F").sum(axis=1)).to(dev)
+            else:
+                acc[b:e] += torch.from_numpy(ll).to(dev)
+        dist.all_reduce(acc, group=group)
+        summed = acc.cpu().numpy()
+
+    paths = None
+    if "zstar_t" in pars:
+        mine = np.asarray(local.get("zstar_t", np.zeros((0, 0), dtype=np.int32)))
+        gathered = [None] * world if rank == 0 else None
+        dist.gather_object(mine, gathered, dst=0, group=group)
+        if rank == 0:
+            paths = np.concatenate([g for g in gathered if g.size], axis=0) if any(g.size for g in gathered) \
+                else mine
+    return local, summed, paths

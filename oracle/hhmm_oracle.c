@@ -1010,7 +1010,7 @@ int hhmm_oracle_run_range(const hhmm_request *r, hhmm_result *o, int64_t p0, int
         pair_ctx c;
         ctx_alloc(&c, K, L, M, r->data.T_max, r->data.T_oos_max);
 #ifdef _OPENMP
-#pragma omp for schedule(dynamic, 16)
+#pragma omp for schedule(dynamic, 1)
 #endif
         for (int64_t p = p0; p < p1; ++p) {
             const int64_t S = r->draws.n_draws;

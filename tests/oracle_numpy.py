@@ -1,0 +1,484 @@
+"""Independent pure-Python transcription of the reference Stan programs.
+
+TEST INFRASTRUCTURE ONLY.  Written line by line from the .stan files (1-based
+loops kept as in Stan) to cross-check the C oracle (oracle/hhmm_oracle.c);
+it shares no code with it.  Transcendentals are Python's math.log / math.exp
+(the host libm), so it is compared with the oracle's libm build.
+
+Stan Math 2.14 semantics are restated here as small
+helpers: log_sum_exp (strict-> max, skip -inf), softmax, Eigen packet-order
+sum / dot / maxCoeff, normal_lpdf (not propto), stanc's NaN / INT_MIN fill.
+Only for small cases: T <= a few hundred, a handful of pairs.
+"""
+import math
+
+import numpy as np
+
+NAN = float("nan")
+NINF = float("-inf")
+INT_MIN = -(2 ** 31)
+NEG_LOG_SQRT_TWO_PI = -math.log(math.sqrt(2.0 * math.pi))
+
+
+# ---------------- Stan Math helpers ----------------
+def div(a, b):
+    """IEEE division (Python raises on /0)."""
+    if b == 0.0:
+        if a == 0.0 or math.isnan(a):
+            return NAN
+        return math.copysign(math.inf, a) * math.copysign(1.0, b)
+    return a / b
+
+
+def log_sum_exp(v):
+    mx = NINF
+    for a in v:
+        if a > mx:
+            mx = a
+    s = 0.0
+    for a in v:
+        if a != NINF:
+            s += math.exp(a - mx)
+    return mx + (NINF if s == 0.0 else math.log(s))
+
+
+def softmax(v):
+    mx = v[0]
+    for a in v[1:]:
+        if a > mx:
+            mx = a
+    th = []
+    s = 0.0
+    for a in v:
+        e = math.exp(a - mx)
+        th.append(e)
+        s += e
+    return [div(e, s) for e in th]
+
+
+def _packet_reduce(vals, op, tail_op):
+    n = len(vals)
+    if n < 2:
+        return vals[0]
+    aligned, aligned2 = n & ~1, n & ~3
+    r0a, r0b = vals[0], vals[1]
+    if aligned > 2:
+        r1a, r1b = vals[2], vals[3]
+        for i in range(4, aligned2, 4):
+            r0a, r0b = op(r0a, vals[i]), op(r0b, vals[i + 1])
+            r1a, r1b = op(r1a, vals[i + 2]), op(r1b, vals[i + 3])
+        r0a, r0b = op(r0a, r1a), op(r0b, r1b)
+        if aligned > aligned2:
+            r0a, r0b = op(r0a, vals[aligned2]), op(r0b, vals[aligned2 + 1])
+    res = op(r0a, r0b)
+    for i in range(aligned, n):
+        res = tail_op(res, vals[i])
+    return res
+
+
+def eigen_sum(v):
+    return _packet_reduce(list(v), lambda a, b: a + b, lambda a, b: a + b)
+
+
+def eigen_dot(a, b):
+    return _packet_reduce([x * y for x, y in zip(a, b)], lambda p, q: p + q, lambda p, q: p + q)
+
+
+def stan_max(v):
+    """max(std::vector<double>) = Eigen maxCoeff (SSE2: maxpd returns the 2nd operand on NaN)."""
+    if len(v) == 0:
+        return NINF
+    return _packet_reduce(list(v), lambda a, b: a if a > b else b, lambda a, b: b if a < b else a)
+
+
+def normalize(v):
+    s = eigen_sum(v)
+    return [div(a, s) for a in v]
+
+
+def normal_lpdf(y, mu, sigma):
+    inv = 1.0 / sigma
+    ls = math.log(sigma)
+    z = (y - mu) * inv
+    lp = 0.0
+    lp += NEG_LOG_SQRT_TWO_PI
+    lp -= ls
+    lp += -0.5 * (z * z)
+    return lp
+
+
+def normal_lpdf_vec(y, mus, sigmas):
+    lp = 0.0
+    for mu, sigma in zip(mus, sigmas):
+        inv = 1.0 / sigma
+        ls = math.log(sigma)
+        z = (y - mu) * inv
+        lp += NEG_LOG_SQRT_TWO_PI
+        lp -= ls
+        lp += -0.5 * (z * z)
+    return lp
+
+
+def log(x):
+    if x == 0:
+        return NINF
+    if x < 0:
+        return NAN
+    return math.log(x)
+
+
+# ---------------- shared GQ blocks ----------------
+def gq_posteriors(unalpha, unbeta, T):
+    alpha = [None] + [softmax(unalpha[t]) for t in range(1, T + 1)]
+    beta = [None] + [softmax(unbeta[t]) for t in range(1, T + 1)]
+    ungamma = [None] + [[a * b for a, b in zip(alpha[t], beta[t])] for t in range(1, T + 1)]
+    gamma = [None] + [normalize(ungamma[t]) for t in range(1, T + 1)]
+    return alpha, beta, ungamma, gamma
+
+
+def viterbi(T, K, init, cand):
+    """delta[1, K] = init(j) for j in 1..K (only column K survives: Q3)."""
+    delta = [[NAN] * (K + 1) for _ in range(T + 1)]
+    a = [[INT_MIN] * (K + 1) for _ in range(T + 1)]
+    for j in range(1, K + 1):
+        delta[1][K] = init(j)
+    for t in range(2, T + 1):
+        for j in range(1, K + 1):
+            delta[t][j] = NINF
+            for i in range(1, K + 1):
+                logp = cand(t, i, j, delta[t - 1][i])
+                if logp > delta[t][j]:
+                    a[t][j] = i
+                    delta[t][j] = logp
+    return finish_viterbi(T, K, delta, a)
+
+
+def finish_viterbi(T, K, delta, a):
+    logp = stan_max(delta[T][1:])
+    z = [INT_MIN] * (T + 1)
+    for j in range(1, K + 1):
+        if delta[T][j] == logp:
+            z[T] = j
+    ok = z[T] != INT_MIN
+    for t in range(1, T):
+        if not ok:
+            break
+        nxt = z[T - t + 1]
+        z[T - t] = a[T - t + 1][nxt]
+        if z[T - t] == INT_MIN:
+            ok = False
+    if not ok:
+        z = [0] * (T + 1)
+    return z[1:], logp, (0 if ok else 1)
+
+
+def pack(T, K, unalpha=None, alpha=None, unbeta=None, beta=None, ungamma=None, gamma=None, loglik=None,
+         zstar=None, logp=None, status=0, **extra):
+    out = {"pair_status": status}
+    for name, v in (("unalpha_tk", unalpha), ("alpha_tk", alpha), ("unbeta_tk", unbeta), ("beta_tk", beta),
+                    ("ungamma_tk", ungamma), ("gamma_tk", gamma)):
+        if v is not None:
+            out[name] = np.array([v[t] for t in range(1, T + 1)], dtype=np.float64)
+    if loglik is not None:
+        out["loglik"] = loglik
+    if zstar is not None:
+        out["zstar_t"] = np.array(zstar, dtype=np.int32)
+        out["logp_zstar"] = logp
+    out.update(extra)
+    return out
+
+
+# ---------------- hmm/stan/hmm.stan ----------------
+def hmm_gauss(T, K, x, p_1k, A_ij, mu_k, sigma_k):
+    X = [None] + list(x)
+    unalpha = [None] * (T + 1)
+    s = normal_lpdf_vec(X[1], mu_k, sigma_k)
+    unalpha[1] = [log(p_1k[j]) + s for j in range(K)]                         # :30
+    for t in range(2, T + 1):                                                 # :32-41
+        unalpha[t] = [0.0] * K
+        for j in range(1, K + 1):
+            acc = [unalpha[t - 1][i - 1] + log(A_ij[i - 1][j - 1]) + normal_lpdf(X[t], mu_k[j - 1], sigma_k[j - 1])
+                   for i in range(1, K + 1)]
+            unalpha[t][j - 1] = log_sum_exp(acc)
+    loglik = log_sum_exp(unalpha[T])                                          # :46
+    unbeta = [None] * (T + 1)
+    unbeta[T] = [1.0] * K                                                     # :68-69
+    for tf in range(0, T - 1):                                                # :71-83
+        t = T - tf
+        unbeta[t - 1] = [0.0] * K
+        for j in range(1, K + 1):
+            acc = [unbeta[t][i - 1] + log(A_ij[j - 1][i - 1]) + normal_lpdf(X[t], mu_k[i - 1], sigma_k[i - 1])
+                   for i in range(1, K + 1)]
+            unbeta[t - 1][j - 1] = log_sum_exp(acc)
+    alpha, beta, ungamma, gamma = gq_posteriors(unalpha, unbeta, T)
+    z, lp, st = viterbi(T, K, lambda j: normal_lpdf(X[1], mu_k[j - 1], sigma_k[j - 1]),
+                        lambda t, i, j, d: d + log(A_ij[i - 1][j - 1]) + normal_lpdf(X[t], mu_k[j - 1], sigma_k[j - 1]))
+    return pack(T, K, unalpha, alpha, unbeta, beta, ungamma, gamma, loglik, z, lp, st)
+
+
+# ---------------- hmm/stan/hmm-multinom.stan (+ semisup) ----------------
+def hmm_multinom(T, K, x, p_1k, A_ij, phi_k, g=None):
+    X = [None] + list(x)
+    G = [None] + list(g) if g is not None else None
+    phi = lambda k, l: phi_k[k - 1][l - 1]  # noqa: E731
+    unalpha = [None] * (T + 1)
+    unalpha[1] = [log(p_1k[j - 1]) + log(phi(j, X[1])) for j in range(1, K + 1)]
+    for t in range(2, T + 1):
+        unalpha[t] = [0.0] * K
+        for j in range(1, K + 1):
+            acc = []
+            for i in range(1, K + 1):
+                if G is None:   # hmm-multinom.stan:170
+                    a = unalpha[t - 1][i - 1] + log(A_ij[i - 1][j - 1]) + log(phi(j, X[t]))
+                else:           # hmm-multinom-semisup.stan:39-44
+                    a = unalpha[t - 1][i - 1] + log(phi(j, X[t]))
+                    if (G[t] == 1 and (j == 1 or j == 4)) or (G[t] == 2 and (j == 2 or j == 3)):
+                        a = a + log(A_ij[i - 1][j - 1])
+                acc.append(a)
+            unalpha[t][j - 1] = log_sum_exp(acc)
+    loglik = log_sum_exp(unalpha[T])
+    unbeta = [None] * (T + 1)
+    unbeta[T] = [1.0] * K
+    for tf in range(0, T - 1):
+        t = T - tf
+        unbeta[t - 1] = [0.0] * K
+        for j in range(1, K + 1):
+            acc = [unbeta[t][i - 1] + log(A_ij[j - 1][i - 1]) + log(phi(i, X[t])) for i in range(1, K + 1)]
+            unbeta[t - 1][j - 1] = log_sum_exp(acc)
+    alpha, beta, ungamma, gamma = gq_posteriors(unalpha, unbeta, T)
+    z, lp, st = viterbi(T, K, lambda j: log(phi(j, X[1])),
+                        lambda t, i, j, d: d + log(A_ij[i - 1][j - 1]) + log(phi(j, X[t])))
+    return pack(T, K, unalpha, alpha, unbeta, beta, ungamma, gamma, loglik, z, lp, st)
+
+
+# ---------------- tayal2009 ----------------
+def _tayal_pred(s, j):
+    return (s == 1 and (j == 2 or j == 3)) or (s == 2 and (j == 1 or j == 4))
+
+
+def tayal_expand(p_11, A_row):
+    p_1k = [0.0] * 4
+    p_1k[0] = p_11
+    p_1k[2] = 1 - p_11
+    A = [[0.0] * 4 for _ in range(4)]
+    A[0][1] = A_row[0][0]
+    A[0][2] = A_row[0][1]
+    A[1][0] = 1
+    A[2][0] = A_row[1][0]
+    A[2][3] = A_row[1][1]
+    A[3][2] = 1
+    return p_1k, A
+
+
+def _tayal_forward(T, K, X, S, p_1k, A, phi):
+    un = [None] * (T + 1)
+    un[1] = [0.0] * K
+    for j in range(1, K + 1):
+        un[1][j - 1] = log(phi(j, X[1]))
+        if (S[1] == 1 and j == 3) or (S[1] == 2 and j == 1):
+            un[1][j - 1] = un[1][j - 1] + log(p_1k[j - 1])
+    for t in range(2, T + 1):
+        un[t] = [0.0] * K
+        for j in range(1, K + 1):
+            acc = []
+            for i in range(1, K + 1):
+                a = un[t - 1][i - 1] + log(phi(j, X[t]))
+                if _tayal_pred(S[t], j):
+                    a = a + log(A[i - 1][j - 1])
+                acc.append(a)
+            un[t][j - 1] = log_sum_exp(acc)
+    return un
+
+
+def _tayal_viterbi(T, K, X, S, A, phi):
+    def cand(t, i, j, d):
+        lp = d + log(phi(j, X[t]))
+        if _tayal_pred(S[t], j):
+            lp = lp + log(A[i - 1][j - 1])
+        return lp
+    return viterbi(T, K, lambda j: log(phi(j, X[1])), cand)
+
+
+def tayal(T, x, sign, p_11, A_row, phi_k):
+    K = 4
+    X, S = [None] + list(x), [None] + list(sign)
+    p_1k, A = tayal_expand(p_11, A_row)
+    phi = lambda k, l: phi_k[k - 1][l - 1]  # noqa: E731
+    unalpha = _tayal_forward(T, K, X, S, p_1k, A, phi)
+    loglik = log_sum_exp(unalpha[T])
+    unbeta = [None] * (T + 1)
+    unbeta[T] = [1.0] * K
+    for tf in range(0, T - 1):
+        t = T - tf
+        unbeta[t - 1] = [0.0] * K
+        for j in range(1, K + 1):
+            acc = []
+            for i in range(1, K + 1):
+                a = unbeta[t][i - 1] + log(phi(i, X[t]))
+                if _tayal_pred(S[t], j):
+                    a = a + log(A[j - 1][i - 1])
+                acc.append(a)
+            unbeta[t - 1][j - 1] = log_sum_exp(acc)
+    alpha, beta, ungamma, gamma = gq_posteriors(unalpha, unbeta, T)
+    z, lp, st = _tayal_viterbi(T, K, X, S, A, phi)
+    return pack(T, K, unalpha, alpha, unbeta, beta, ungamma, gamma, loglik, z, lp, st)
+
+
+def tayal_lite(T, x, sign, T_oos, x_oos, sign_oos, p_11, A_row, phi_k):
+    K = 4
+    X, S = [None] + list(x), [None] + list(sign)
+    Xo, So = [None] + list(x_oos), [None] + list(sign_oos)
+    p_1k, A = tayal_expand(p_11, A_row)
+    phi = lambda k, l: phi_k[k - 1][l - 1]  # noqa: E731
+    unalpha = _tayal_forward(T, K, X, S, p_1k, A, phi)
+    loglik = log_sum_exp(unalpha[T])
+    alpha = [None] + [softmax(unalpha[t]) for t in range(1, T + 1)]
+    un_oos = _tayal_forward(T_oos, K, Xo, So, p_1k, A, phi)
+    al_oos = [None] + [softmax(un_oos[t]) for t in range(1, T_oos + 1)]
+    z, lp, st = _tayal_viterbi(T_oos, K, Xo, So, A, phi)
+    return pack(T, K, unalpha, alpha, None, None, None, None, loglik, z, lp, st,
+                unalpha_tk_oos=np.array(un_oos[1:]), alpha_tk_oos=np.array(al_oos[1:]))
+
+
+# ---------------- IOHMM ----------------
+def _iohmm_common(T, K, M, u, w_km, p_1k, logA_mode):
+    """A_ij[t] = softmax(u_t' w_j) with A[1] = p_1k (filler); logA for hmix."""
+    A = [None] * (T + 1)
+    A[1] = list(p_1k)
+    logA = [None] * (T + 1)
+    logA[1] = [log(p) for p in p_1k]
+    for t in range(2, T + 1):
+        un = [eigen_dot(u[t - 1], w_km[j - 1]) for j in range(1, K + 1)]
+        A[t] = softmax(un)
+        logA[t] = [log(a) for a in A[t]]
+    return A, logA
+
+
+def _mix_oblik(T, K, L, X, lambda_kl, mu_kl, s_kl):
+    ll = [[log(lambda_kl[k][l]) for l in range(L)] for k in range(K)]
+    ob = [None] * (T + 1)
+    for t in range(1, T + 1):
+        ob[t] = [log_sum_exp([ll[j][l] + normal_lpdf(X[t], mu_kl[j][l], s_kl[j][l]) for l in range(L)])
+                 for j in range(K)]
+    return ob
+
+
+def _iohmm_fwd(T, K, p_1k, ob, la):
+    un = [None] * (T + 1)
+    un[1] = [log(p_1k[j]) + ob[1][j] for j in range(K)]
+    for t in range(2, T + 1):
+        un[t] = [log_sum_exp([un[t - 1][i] + la(t, i) + ob[t][j] for i in range(K)]) for j in range(K)]
+    return un
+
+
+def _iohmm_bwd(T, K, ob, la):
+    ub = [None] * (T + 1)
+    ub[T] = [1.0] * K
+    for tf in range(0, T - 1):
+        t = T - tf
+        ub[t - 1] = [log_sum_exp([ub[t][i] + la(t, i) + ob[t][i] for i in range(K)]) for _ in range(K)]
+    return ub
+
+
+def _iohmm_viterbi(T, K, ob, la, fixed):
+    if not fixed:
+        return viterbi(T, K, lambda j: ob[1][j - 1], lambda t, i, j, d: d + la(t, i - 1) + ob[t][j - 1])
+    delta = [[NAN] * (K + 1) for _ in range(T + 1)]
+    a = [[INT_MIN] * (K + 1) for _ in range(T + 1)]
+    for j in range(1, K + 1):
+        delta[1][j] = ob[1][j - 1]
+    for t in range(2, T + 1):
+        for j in range(1, K + 1):
+            delta[t][j] = NINF
+            for i in range(1, K + 1):
+                logp = delta[t - 1][i] + la(t, i - 1) + ob[t][j - 1]
+                if logp > delta[t][j]:
+                    a[t][j] = i
+                    delta[t][j] = logp
+    return finish_viterbi(T, K, delta, a)
+
+
+def iohmm_reg(T, K, M, x_t, u_tm, p_1k, w_km, b_km, s_k):
+    X = [None] + list(x_t)
+    u = [list(r) for r in u_tm]
+    A, _ = _iohmm_common(T, K, M, u, w_km, p_1k, False)
+    ob = [None] + [[normal_lpdf(X[t], eigen_dot(u[t - 1], b_km[j]), s_k[j]) for j in range(K)]
+                   for t in range(1, T + 1)]
+    la = lambda t, i: log(A[t][i])  # noqa: E731
+    un = _iohmm_fwd(T, K, p_1k, ob, la)
+    ub = _iohmm_bwd(T, K, ob, la)
+    alpha, beta, ungamma, gamma = gq_posteriors(un, ub, T)
+    loglik = log_sum_exp(un[T])
+    z, lp, st = _iohmm_viterbi(T, K, ob, la, False)
+    return pack(T, K, un, alpha, ub, beta, ungamma, gamma, loglik, z, lp, st,
+                oblik_tk=np.array(ob[1:]), logA_ij=np.array(A[1:]))
+
+
+def iohmm_mix(T, K, M, L, x_t, u_tm, p_1k, w_km, lambda_kl, mu_kl, s_kl, variant):
+    X = [None] + list(x_t)
+    u = [list(r) for r in u_tm]
+    A, logA = _iohmm_common(T, K, M, u, w_km, p_1k, True)
+    ob = _mix_oblik(T, K, L, X, lambda_kl, mu_kl, s_kl)
+    if variant == "mix":
+        la_f = lambda t, i: logA[t][i]  # noqa: E731  (logA_ij = log(A_ij), :69)
+        la_b = lambda t, i: log(A[t][i])  # noqa: E731
+    else:
+        la_f = la_b = lambda t, i: logA[t][i]  # noqa: E731
+    un = _iohmm_fwd(T, K, p_1k, ob, la_f)
+    loglik = log_sum_exp(un[T])
+    alpha = [None] + [softmax(un[t]) for t in range(1, T + 1)]
+    oblik_t = np.array([log_sum_exp([log(alpha[t][k]) + ob[t][k] for k in range(K)]) for t in range(1, T + 1)])
+    if variant == "lite":
+        return pack(T, K, un, None, None, None, None, None, loglik, oblik_tk=np.array(ob[1:]), oblik_t=oblik_t,
+                    logA_ij=np.array(logA[1:]))
+    ub = _iohmm_bwd(T, K, ob, la_b)
+    beta = [None] + [softmax(ub[t]) for t in range(1, T + 1)]
+    ungamma = [None] + [[a * b for a, b in zip(alpha[t], beta[t])] for t in range(1, T + 1)]
+    gamma = [None] + [[div(v, eigen_sum(ungamma[t])) for v in ungamma[t]] for t in range(1, T + 1)]
+    z, lp, st = _iohmm_viterbi(T, K, ob, la_b, variant == "hmix")
+    if variant == "mix":
+        return pack(T, K, un, alpha, ub, beta, ungamma, gamma, loglik, z, lp, st, oblik_tk=np.array(ob[1:]),
+                    logA_ij=np.array(A[1:]))
+    return pack(T, K, un, alpha, None, beta, None, gamma, loglik, z, lp, st, oblik_tk=np.array(ob[1:]),
+                oblik_t=oblik_t, logA_ij=np.array(logA[1:]))
+
+
+# ---------------- batch driver (pair p = s + S*n) ----------------
+def run(model, data, draws, pairing="grid"):
+    """Per-pair dicts keyed like hhmm_amd.gqs outputs, for pairs in ABI order."""
+    xkey = "x_t" if model.startswith("iohmm") else "x"
+    x = np.atleast_2d(np.asarray(data[xkey]))
+    N, Tm = x.shape
+    S = next(np.asarray(v).shape[0] for k, v in draws.items())
+    Ts = np.asarray(data["T"]).reshape(N) if "T" in data else np.full(N, Tm)
+    pairs = [(p // S, p % S) for p in range(N * S)] if pairing == "grid" else [(p, p) for p in range(N)]
+    K = int(data["K"])
+    res = []
+    for n, s in pairs:
+        T = int(Ts[n])
+        d = {k: np.asarray(v)[s] for k, v in draws.items()}
+        if model == "hmm":
+            r = hmm_gauss(T, K, x[n, :T], d["p_1k"], d["A_ij"], d["mu_k"], d["sigma_k"])
+        elif model == "hmm-multinom":
+            r = hmm_multinom(T, K, x[n, :T], d["p_1k"], d["A_ij"], d["phi_k"])
+        elif model == "hmm-multinom-semisup":
+            r = hmm_multinom(T, K, x[n, :T], d["p_1k"], d["A_ij"], d["phi_k"], g=np.asarray(data["g"])[n, :T])
+        elif model == "hhmm-tayal2009":
+            r = tayal(T, x[n, :T], np.asarray(data["sign"])[n, :T], float(d["p_11"]), d["A_row"], d["phi_k"])
+        elif model == "hhmm-tayal2009-lite":
+            xo = np.atleast_2d(np.asarray(data["x_oos"]))
+            To = int(np.asarray(data["T_oos"]).reshape(N)[n]) if "T_oos" in data else xo.shape[1]
+            r = tayal_lite(T, x[n, :T], np.asarray(data["sign"])[n, :T], To, xo[n, :To],
+                           np.atleast_2d(np.asarray(data["sign_oos"]))[n, :To], float(d["p_11"]), d["A_row"],
+                           d["phi_k"])
+        elif model == "iohmm-reg":
+            u = np.asarray(data["u_tm"]).reshape(N, Tm, -1)
+            r = iohmm_reg(T, K, int(data["M"]), x[n, :T], u[n, :T], d["p_1k"], d["w_km"], d["b_km"], d["s_k"])
+        else:
+            u = np.asarray(data["u_tm"]).reshape(N, Tm, -1)
+            variant = {"iohmm-mix": "mix", "iohmm-hmix": "hmix", "iohmm-hmix-lite": "lite"}[model]
+            r = iohmm_mix(T, K, int(data["M"]), int(data["L"]), x[n, :T], u[n, :T], d["p_1k"], d["w_km"],
+                          d["lambda_kl"], d["mu_kl"], d["s_kl"], variant)
+        r["T"] = T
+        res.append(r)
+    return res

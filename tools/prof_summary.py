@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output into profiles/ (committed evidence).
+
+  python tools/prof_summary.py TAG gpurun_out/prof_TAG [--bench gpurun_out/bench_TAG.json]
+
+Writes profiles/TAG_kernel_stats.csv (per-kernel calls / total / avg / min / max
+duration from the --kernel-trace --stats pass; SQLite .db or CSV input),
+profiles/TAG_pmc.csv (per-kernel averages of every PMC counter collected in the
+separate --pmc passes) and, when FETCH_SIZE / WRITE_SIZE are present,
+profiles/TAG_pmc.json with HBM bytes per launch of each libhhmm kernel.
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half
+of the bytes of wide coalesced streaming reads; the corrected figure doubles
+it.  Both raw and corrected values are recorded.
+"""
+import csv
+import glob
+import json
+import os
+import pathlib
+import sqlite3
+import statistics
+import sys
+from collections import defaultdict
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+
+
+def short(name):
+    for key in ("fb_kernel", "viterbi_kernel", "cr_log_kernel", "scan_", "ffbs_", "iohmm_"):
+        if key in name:
+            return name.split("(")[0].replace("void ", "")
+    return None
+
+
+def kernel_rows_from_db(path):
+    db = sqlite3.connect(path)
+    rows = defaultdict(list)
+    for name, dur in db.execute("select name, duration from kernels"):
+        rows[name].append(dur)
+    return rows
+
+
+def kernel_rows_from_csv(path):
+    rows = defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name") or r.get("kernel_name") or r.get("Name")
+            s, e = r.get("Start_Timestamp"), r.get("End_Timestamp")
+            if name and s and e:
+                rows[name].append(int(e) - int(s))
+    return rows
+
+
+def main():
+    tag, d = sys.argv[1], pathlib.Path(sys.argv[2])
+    out = ROOT / "profiles"
+    out.mkdir(exist_ok=True)
+    rows = None
+    dbs = glob.glob(str(d / "**" / "*.db"), recursive=True)
+    csvs = glob.glob(str(d / "**" / "*kernel_trace.csv"), recursive=True)
+    if csvs:
+        rows = kernel_rows_from_csv(csvs[0])
+    elif dbs:
+        rows = kernel_rows_from_db(dbs[0])
+    if rows:
+        with open(out / f"{tag}_kernel_stats.csv", "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "calls", "total_ns", "avg_ns", "min_ns", "max_ns", "share_of_hhmm_time"])
+            tot = sum(sum(v) for k, v in rows.items() if short(k))
+            for k, v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
+                if not short(k):
+                    continue
+                w.writerow([short(k), len(v), sum(v), round(statistics.mean(v)), min(v), max(v),
+                            round(sum(v) / tot, 4)])
+        print("wrote", out / f"{tag}_kernel_stats.csv")
+
+    # PMC passes: counter_collection.csv per pass
+    pmc = defaultdict(lambda: defaultdict(list))
+    for path in glob.glob(str(d / "pmc*" / "**" / "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                name = r.get("Kernel_Name", "")
+                if not short(name):
+                    continue
+                ctr = r.get("Counter_Name")
+                val = float(r.get("Counter_Value", "nan"))
+                pmc[short(name)][(ctr, r.get("Dispatch_Id"))].append(val)
+    if pmc:
+        agg = {}
+        for k, d2 in pmc.items():
+            per = defaultdict(list)
+            for (ctr, disp), vals in d2.items():
+                per[ctr].append(sum(vals))  # sum over dimensions (XCD/SE instances)
+            agg[k] = {c: statistics.mean(v) for c, v in per.items()}
+        with open(out / f"{tag}_pmc.csv", "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "counter", "mean_per_dispatch"])
+            for k, cs in agg.items():
+                for c, v in sorted(cs.items()):
+                    w.writerow([k, c, v])
+        print("wrote", out / f"{tag}_pmc.csv")
+        summ = {}
+        for k, cs in agg.items():
+            if "FETCH_SIZE" in cs or "WRITE_SIZE" in cs:
+                fetch_kb = cs.get("FETCH_SIZE", float("nan"))
+                write_kb = cs.get("WRITE_SIZE", float("nan"))
+                summ[k] = {"fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+                           "hbm_bytes_per_launch_raw": (fetch_kb + write_kb) * 1024,
+                           "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
+                           "correction": "FETCH_SIZE doubled (gfx950, MI355X_MICROARCH.md §HBM)"}
+        if summ:
+            (out / f"{tag}_pmc_traffic.json").write_text(json.dumps(summ, indent=1))
+            print("wrote", out / f"{tag}_pmc_traffic.json")
+
+
+if __name__ == "__main__":
+    main()
