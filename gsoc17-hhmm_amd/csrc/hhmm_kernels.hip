@@ -16,9 +16,15 @@
  * Kernels:
  *   fb_kernel      A2/A1 emissions, A6 forward + loglik, A7 alpha, A8 backward,
  *                  A9 gamma, A12/A13 masks.  LINEAR-space scaled recursion
- *                  (K^2 FMAs + a power-of-two rescale per step; no exp/log in
- *                  the loop); forward checkpoints every C steps, recomputed
- *                  chunk by chunk in the backward sweep.  Tolerance 1e-9 rel.
+ *                  (K^2 FMAs per step, a power-of-two renormalisation only when
+ *                  the exponent drifts; no exp/log in the discrete loop);
+ *                  forward checkpoints every C steps, recomputed chunk by chunk
+ *                  in the backward sweep.  Tolerance 1e-9 rel.
+ * Latency rules used throughout (the kernels are latency-, not issue-bound at
+ * the 2 waves/SIMD the LDS tables allow): observation loads are issued
+ * unconditionally (clamped index) one chunk ahead, checkpoints and
+ * back-pointer words one chunk ahead, and each step's LDS emission row is
+ * fetched one step ahead.
  *   viterbi_kernel A11 max-plus recursion in LOG space with exactly the
  *                  reference's operation order and tie rules, log tables from
  *                  the correctly rounded hhmm_cr_log (bit-identical to the
@@ -85,19 +91,40 @@ __device__ __forceinline__ double stan_max_vec(const double (&d)[K])
     }
 }
 
-/* Keep a K-vector's largest entry in [0.5, 1): scale by 2^-e, count e. */
+/* Lazy power-of-two renormalisation of a K-vector: only when the largest
+ * entry's exponent leaves [-255, 256] (rare; a scalar-skipped branch).  The
+ * removed exponent is accumulated in `ex`; mx == 0 / NaN leave v unchanged. */
 template <int K>
-__device__ __forceinline__ void rescale(double (&v)[K], int &ex)
+__device__ __forceinline__ void renorm(double (&v)[K], int &ex)
 {
     double mx = v[0];
 #pragma unroll
     for (int k = 1; k < K; ++k)
         mx = fmax(mx, v[k]);
-    const int e = (mx > 0.0) ? __builtin_amdgcn_frexp_exp(mx) : 0;
+    const uint32_t hi = (uint32_t)((uint64_t)__double_as_longlong(mx) >> 32);
+    const uint32_t eb = (hi >> 20) & 0x7ffu;
+    if (__builtin_expect(eb - (1023u - 255u) > 511u, 0)) {
+        const int e = __builtin_amdgcn_frexp_exp(mx);
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-        v[k] = ldexp(v[k], -e);
-    ex += e;
+        for (int k = 0; k < K; ++k)
+            v[k] = ldexp(v[k], -e);
+        ex += e;
+    }
+}
+
+__device__ __forceinline__ int wave_min(int v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v = min(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v = max(v, __shfl_xor(v, off));
+    return v;
 }
 
 /* hmm-multinom-semisup.stan:42 -- j0 is 0-based */
@@ -135,38 +162,34 @@ struct Obs {
     double xr; /* real observation (gauss) */
 };
 
-template <int MODEL, bool AUX>
-__device__ __forceinline__ Obs load_obs(const DevArgs &a, const int32_t *xb, const int32_t *ab,
-                                        const double *rb, int64_t off)
-{
-    Obs o;
-    o.x = 1;
-    o.aux = 0;
-    o.xr = 0.0;
-    if constexpr (ModelTraits<MODEL>::kDiscrete)
-        o.x = xb[off];
-    if constexpr (AUX)
-        o.aux = ab[off];
-    if constexpr (ModelTraits<MODEL>::kGauss)
-        o.xr = rb[off];
-    return o;
-}
+/* Per-lane view of one series' observation streams (series-fastest arrays). */
+struct SeriesPtrs {
+    const int32_t *x;
+    const int32_t *aux;
+    const double *xr;
+    int64_t stride; /* N: elements between consecutive time steps */
+};
 
-/* Loads the C observations of chunk [t0, t0+C) (clamped to the lane's length). */
-template <int MODEL, int C, bool AUX = ModelTraits<MODEL>::kAux>
-__device__ __forceinline__ void load_chunk(Obs (&dst)[C], const DevArgs &a, const int32_t *xb,
-                                           const int32_t *ab, const double *rb, int t0, int Tp)
+/* Loads the C observations of chunk [t0, t0+C).  Every load is issued
+ * unconditionally from a time index clamped into [0, Tp-1]: a conditional
+ * load makes hipcc branch around it and drain vmcnt(0) per element
+ * (cdna_hip_programming.md §5, trap (c)); steps past Tp are never consumed. */
+template <int MODEL, int C, bool AUX>
+__device__ __forceinline__ void load_chunk(Obs (&dst)[C], const SeriesPtrs &sp, int t0, int Tp)
 {
 #pragma unroll
     for (int u = 0; u < C; ++u) {
-        const int t = t0 + u;
-        if (t < Tp && t >= 0)
-            dst[u] = load_obs<MODEL, AUX>(a, xb, ab, rb, (int64_t)t * a.N);
-        else {
-            dst[u].x = 1;
-            dst[u].aux = 0;
-            dst[u].xr = 0.0;
-        }
+        const int tc = min(max(t0 + u, 0), Tp - 1);
+        const int64_t off = (int64_t)tc * sp.stride;
+        dst[u].x = 1;
+        dst[u].aux = 0;
+        dst[u].xr = 0.0;
+        if constexpr (!ModelTraits<MODEL>::kGauss)
+            dst[u].x = sp.x[off];
+        if constexpr (AUX)
+            dst[u].aux = sp.aux[off];
+        if constexpr (ModelTraits<MODEL>::kGauss)
+            dst[u].xr = sp.xr[off];
     }
 }
 
@@ -277,11 +300,17 @@ __device__ __forceinline__ double gauss_lpdf(const PairParams<MODEL, K> &pp, dou
     return pp.c0[j] + (-0.5 * z2);
 }
 
-/* Emission probabilities of one step for the linear-space filter.  Gaussian
- * densities are divided by their max over states (added to the log scale). */
+/* Emission of one step for the linear-space filter: e[j] (probabilities,
+ * Gaussian densities divided by their max m over states) and log m. */
+template <int K>
+struct Em {
+    double e[K];
+    double m;
+};
+
 template <int MODEL, int K>
 __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const double2 *slab, int L,
-                                          const Obs &o, double (&e)[K], double &lsc)
+                                          const Obs &o, Em<K> &em)
 {
     if constexpr (ModelTraits<MODEL>::kGauss) {
         double lp[K];
@@ -293,10 +322,11 @@ __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const 
         }
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            e[j] = exp(lp[j] - m);
-        lsc += m;
+            em.e[j] = exp(lp[j] - m);
+        em.m = m;
     } else {
-        read_table<K>(slab, o.x, L, e);
+        read_table<K>(slab, o.x, L, em.e);
+        em.m = 0.0;
     }
 }
 
@@ -332,7 +362,7 @@ __device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL
 #pragma unroll
     for (int j = 0; j < K; ++j)
         al[j] = s[j] * e[j];
-    rescale<K>(al, ex);
+    renorm<K>(al, ex);
 }
 
 /* beta_{t-1} from beta_t and step t's emission / masks. */
@@ -365,13 +395,13 @@ __device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL
 #pragma unroll
     for (int j = 0; j < K; ++j)
         be[j] = s[j];
-    rescale<K>(be, ex);
+    renorm<K>(be, ex);
 }
 
-/* alpha_1 (t = 0). */
+/* alpha_1 (t = 0) from the step-0 observation / emission. */
 template <int MODEL, int K>
-__device__ __forceinline__ void fwd_init(double (&al)[K], const PairParams<MODEL, K> &pp,
-                                         const double2 *slab, int L, const Obs &o, double &lsc, int &ex)
+__device__ __forceinline__ void fwd_init(double (&al)[K], const PairParams<MODEL, K> &pp, const Em<K> &em,
+                                         const Obs &o, double &lsc, int &ex)
 {
     if constexpr (ModelTraits<MODEL>::kGauss) {
         /* hmm.stan:30 -- log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k) (Q2) */
@@ -389,17 +419,15 @@ __device__ __forceinline__ void fwd_init(double (&al)[K], const PairParams<MODEL
             al[k] = pp.p[k];
         lsc += s;
     } else {
-        double e[K];
-        read_table<K>(slab, o.x, L, e);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if constexpr (ModelTraits<MODEL>::kTayal)
-                al[k] = tayal_init_pred(o.aux, k) ? e[k] * pp.p[k] : e[k];
+                al[k] = tayal_init_pred(o.aux, k) ? em.e[k] * pp.p[k] : em.e[k];
             else
-                al[k] = pp.p[k] * e[k];
+                al[k] = pp.p[k] * em.e[k];
         }
     }
-    rescale<K>(al, ex);
+    renorm<K>(al, ex);
 }
 
 __device__ __forceinline__ void pair_coords(const DevArgs &a, int64_t p, int64_t &n, int64_t &d)
@@ -419,9 +447,31 @@ __device__ __forceinline__ int pair_len(const DevArgs &a, int64_t n)
     return min(max(Tp, 1), a.Tmax);
 }
 
+template <int MODEL, bool AUX>
+__device__ __forceinline__ SeriesPtrs series_ptrs(const DevArgs &a, int64_t n)
+{
+    SeriesPtrs sp;
+    sp.stride = a.N;
+    sp.x = a.x ? a.x + n : nullptr;
+    sp.aux = nullptr;
+    if constexpr (AUX && ModelTraits<MODEL>::kSemisup)
+        sp.aux = a.g + n;
+    if constexpr (AUX && ModelTraits<MODEL>::kTayal)
+        sp.aux = a.sign + n;
+    sp.xr = a.xr ? a.xr + n : nullptr;
+    return sp;
+}
+
 /* ------------------------------------------------------------------ */
 /* Forward / backward / posteriors                                       */
 /* ------------------------------------------------------------------ */
+
+/* Output profile of the forward-backward kernel (compile time). */
+enum FbMode {
+    FB_GAMMA = 0, /* loglik + gamma_tk: the hot path, no per-output branches */
+    FB_FULL = 1,  /* any mix of alpha/beta/unalpha/unbeta/ungamma/gamma (+ per-step log scale) */
+    FB_FWD = 2    /* forward only: loglik / alpha / unalpha (tayal-lite, no backward output) */
+};
 
 template <int K>
 __device__ __forceinline__ void store_tk(double *out, const DevArgs &a, int64_t p, int t, const double (&v)[K])
@@ -431,16 +481,22 @@ __device__ __forceinline__ void store_tk(double *out, const DevArgs &a, int64_t 
         out[p + a.P * ((int64_t)t + (int64_t)a.Tout * k)] = v[k];
 }
 
+template <int K>
+__device__ __forceinline__ double vsum(const double (&v)[K])
+{
+    double s = v[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k)
+        s += v[k];
+    return s;
+}
+
 /* Writes the forward-side outputs of step t (alpha, unalpha). */
 template <int K>
 __device__ __forceinline__ void emit_alpha(const DevArgs &a, int64_t p, int t, const double (&al)[K], double lsc)
 {
     if ((a.outputs & HHMM_OUT_ALPHA) && a.alpha) {
-        double s = al[0];
-#pragma unroll
-        for (int k = 1; k < K; ++k)
-            s += al[k];
-        const double r = 1.0 / s;
+        const double r = 1.0 / vsum<K>(al);
         double v[K];
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -456,187 +512,257 @@ __device__ __forceinline__ void emit_alpha(const DevArgs &a, int64_t p, int t, c
     }
 }
 
-/* FWD_ONLY: forward pass writing alpha / unalpha / loglik (tayal-lite, or
- * when no backward-side output is requested).  FULL: track the per-step log
- * scale (needed for unalpha / unbeta). */
-template <int MODEL, int K, bool FWD_ONLY, bool FULL>
+/* Outputs of step t once alpha_t and beta_t are known. */
+template <int K, int MODE>
+__device__ __forceinline__ void emit_posteriors(const DevArgs &a, int64_t p, int t, const double (&al)[K],
+                                                const double (&be)[K], double lsa, double lsb)
+{
+    if constexpr (MODE == FB_GAMMA) {
+        /* gamma = (alpha .* beta) / sum: the normalisations of alpha and beta
+         * cancel, one division per step (hmm.stan:89-96 up to rounding) */
+        double ug[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ug[k] = al[k] * be[k];
+        const double r = 1.0 / vsum<K>(ug);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ug[k] = ug[k] * r;
+        store_tk<K>(a.gamma, a, p, t, ug);
+    } else {
+        const uint32_t o = a.outputs;
+        emit_alpha<K>(a, p, t, al, lsa);
+        const double sb = vsum<K>(be);
+        if ((o & HHMM_OUT_BETA) && a.beta) {
+            const double r = 1.0 / sb;
+            double v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                v[k] = be[k] * r;
+            store_tk<K>(a.beta, a, p, t, v);
+        }
+        if ((o & HHMM_OUT_UNBETA) && a.unbeta) {
+            /* unbeta_tk[T] = 1 (Q1): every unbeta carries +1 */
+            double v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                v[k] = (log(be[k]) + lsb) + 1.0;
+            store_tk<K>(a.unbeta, a, p, t, v);
+        }
+        if (o & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
+            const double ra = 1.0 / vsum<K>(al), rb = 1.0 / sb;
+            double ug[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                ug[k] = (al[k] * ra) * (be[k] * rb);
+            if ((o & HHMM_OUT_UNGAMMA) && a.ungamma)
+                store_tk<K>(a.ungamma, a, p, t, ug);
+            if ((o & HHMM_OUT_GAMMA) && a.gamma) {
+                const double rg = 1.0 / vsum<K>(ug);
+                double v[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    v[k] = ug[k] * rg;
+                store_tk<K>(a.gamma, a, p, t, v);
+            }
+        }
+    }
+}
+
+/* Per-lane state of the forward-backward kernel. */
+template <int MODEL, int K>
+struct FbLane {
+    PairParams<MODEL, K> pp;
+    const double2 *slab;
+    int L;
+    int64_t p;
+    int Tp;
+};
+
+/* One forward chunk [t0, t0+C).  FULLC: every lane of the wave has all C
+ * steps (no per-step predicate).  The emission of step u+1 is fetched before
+ * step u is computed (LDS latency hidden behind the K^2 FMAs). */
+template <int MODEL, int K, int C, int MODE, bool FULLC>
+__device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, K> &ln, int c, const Obs (&cur)[C],
+                                          const Obs &nxt0, Em<K> &ecur, double (&al)[K], double &lsc, int &ex)
+{
+    const int t0 = c * C;
+#pragma unroll
+    for (int u = 0; u < C; ++u) {
+        const int t = t0 + u;
+        Em<K> enx;
+        emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, (u + 1 < C) ? cur[u + 1 < C ? u + 1 : 0] : nxt0, enx);
+        if (FULLC || t < ln.Tp) {
+            if (u == 0 && c == 0) {
+                fwd_init<MODEL, K>(al, ln.pp, ecur, cur[0], lsc, ex);
+            } else {
+                lsc += ecur.m;
+                fwd_step<MODEL, K>(al, ln.pp, ecur.e, cur[u], ex);
+            }
+            if constexpr (MODE == FB_FWD) {
+                emit_alpha<K>(a, ln.p, t, al, lsc + kLn2 * ex);
+            } else if (u == 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    a.ckpt[ln.p + a.P * ((int64_t)c * K + k)] = al[k];
+                if constexpr (MODE == FB_FULL)
+                    a.ckpt_ls[ln.p + a.P * (int64_t)c] = lsc + kLn2 * ex;
+            }
+        }
+        ecur = enx;
+    }
+}
+
+/* One backward chunk: recompute alpha over the chunk from its checkpoint,
+ * then walk t = t0+C-1 .. t0 emitting the posteriors and stepping beta. */
+template <int MODEL, int K, int C, int MODE, bool FULLC>
+__device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, K> &ln, int c, const Obs (&cur)[C],
+                                          const double (&ck)[K], double ck_ls, double (&be)[K], double &blsc,
+                                          int &bex)
+{
+    const int t0 = c * C;
+    double abuf[C][K];
+    double lsbuf[MODE == FB_FULL ? C : 1];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        abuf[0][k] = ck[k];
+    lsbuf[0] = ck_ls;
+    {
+        double lsacc = 0.0;
+        int exb = 0;
+        Em<K> ecur;
+        emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[1 < C ? 1 : 0], ecur);
+#pragma unroll
+        for (int u = 1; u < C; ++u) {
+            Em<K> enx;
+            emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[u + 1 < C ? u + 1 : u], enx);
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                abuf[u][k] = abuf[u - 1][k];
+            if (FULLC || t0 + u < ln.Tp) {
+                lsacc += ecur.m;
+                fwd_step<MODEL, K>(abuf[u], ln.pp, ecur.e, cur[u], exb);
+            }
+            if constexpr (MODE == FB_FULL)
+                lsbuf[u] = ck_ls + (lsacc + kLn2 * exb);
+            ecur = enx;
+        }
+    }
+    Em<K> ecur;
+    emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[C - 1], ecur);
+#pragma unroll
+    for (int u = C - 1; u >= 0; --u) {
+        const int t = t0 + u;
+        Em<K> enx;
+        emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[u > 0 ? u - 1 : 0], enx);
+        if (FULLC || t < ln.Tp) {
+            emit_posteriors<K, MODE>(a, ln.p, t, abuf[u], be, lsbuf[MODE == FB_FULL ? u : 0],
+                                     blsc + kLn2 * bex);
+            if (t > 0) {
+                if constexpr (MODE == FB_FULL)
+                    blsc += ecur.m;
+                bwd_step<MODEL, K>(be, ln.pp, ecur.e, cur[u], bex);
+            }
+        }
+        ecur = enx;
+    }
+}
+
+template <int MODEL, int K, int MODE>
 __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
 {
     constexpr int C = fb_chunk(K);
+    constexpr bool AUX = ModelTraits<MODEL>::kAux;
     HIP_DYNAMIC_SHARED(double2, lds)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.P)
-        return;
+    /* lanes past the last pair redo pair P-1 (identical values, benign
+     * duplicate stores): every lane stays in the wave-wide reductions */
+    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
     int64_t n, d;
     pair_coords(a, p, n, d);
-    const int Tp = pair_len(a, n);
     constexpr int KP = (K + 1) / 2;
-    double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
 
-    PairParams<MODEL, K> pp;
-    load_params<MODEL, K, false>(pp, a, d);
+    FbLane<MODEL, K> ln;
+    ln.p = p;
+    ln.L = a.L;
+    ln.Tp = pair_len(a, n);
+    ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+    load_params<MODEL, K, false>(ln.pp, a, d);
     if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, false>(slab, a, d);
-
-    const int32_t *xb = a.x ? a.x + n : nullptr;
-    const int32_t *ab = nullptr;
-    if constexpr (ModelTraits<MODEL>::kSemisup)
-        ab = a.g + n;
-    if constexpr (ModelTraits<MODEL>::kTayal)
-        ab = a.sign + n;
-    const double *rb = a.xr ? a.xr + n : nullptr;
+        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
+    const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
+    const int Tw_min = wave_min(ln.Tp);
+    const int Tw_max = wave_max(ln.Tp);
+    const int nfull = Tw_min / C;              /* chunks complete for every lane */
+    const int nchunk = (Tw_max + C - 1) / C;   /* chunks any lane needs */
 
     /* ---- forward sweep ---- */
     double al[K];
     double lsc = 0.0; /* log scale excluding the binary exponent */
     int ex = 0;       /* sum of binary exponents removed */
     Obs cur[C];
-    load_chunk<MODEL, C>(cur, a, xb, ab, rb, 0, Tp);
-    const int nchunk = (Tp + C - 1) / C;
+    load_chunk<MODEL, C, AUX>(cur, sp, 0, ln.Tp);
+    Em<K> ecur;
+    emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[0], ecur);
     for (int c = 0; c < nchunk; ++c) {
-        const int t0 = c * C;
         Obs nxt[C];
-        load_chunk<MODEL, C>(nxt, a, xb, ab, rb, t0 + C, Tp);
-#pragma unroll
-        for (int u = 0; u < C; ++u) {
-            const int t = t0 + u;
-            if (t < Tp) {
-                if (u == 0 && c == 0) {
-                    fwd_init<MODEL, K>(al, pp, slab, a.L, cur[0], lsc, ex);
-                } else {
-                    double e[K];
-                    emit_prob<MODEL, K>(pp, slab, a.L, cur[u], e, lsc);
-                    fwd_step<MODEL, K>(al, pp, e, cur[u], ex);
-                }
-                if constexpr (FWD_ONLY) {
-                    emit_alpha<K>(a, p, t, al, lsc + kLn2 * ex);
-                } else if (u == 0) {
-#pragma unroll
-                    for (int k = 0; k < K; ++k)
-                        a.ckpt[p + a.P * ((int64_t)c * K + k)] = al[k];
-                    a.ckpt_ls[p + a.P * (int64_t)c] = lsc + kLn2 * ex;
-                }
-            }
-        }
+        load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C, ln.Tp);
+        if (c < nfull)
+            fwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
+        else
+            fwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
 #pragma unroll
         for (int u = 0; u < C; ++u)
             cur[u] = nxt[u];
     }
-    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik) {
-        double s = al[0];
-#pragma unroll
-        for (int k = 1; k < K; ++k)
-            s += al[k];
-        a.loglik[p] = log(s) + (lsc + kLn2 * ex);
-    }
-    if constexpr (FWD_ONLY)
+    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+        a.loglik[p] = log(vsum<K>(al)) + (lsc + kLn2 * ex);
+    if constexpr (MODE == FB_FWD)
         return;
 
-    /* ---- backward sweep: recompute each chunk's alphas from its checkpoint ---- */
-    const bool want_alpha = (a.outputs & (HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) != 0;
-    const bool want_beta = (a.outputs & (HHMM_OUT_BETA | HHMM_OUT_UNBETA)) != 0;
-    const bool want_gamma = (a.outputs & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) != 0;
+    /* ---- backward sweep, chunk by chunk from the end ---- */
     double be[K];
 #pragma unroll
     for (int k = 0; k < K; ++k)
         be[k] = 1.0;
     double blsc = 0.0;
     int bex = 0;
-    load_chunk<MODEL, C>(cur, a, xb, ab, rb, (nchunk - 1) * C, Tp);
-    for (int c = nchunk - 1; c >= 0; --c) {
-        const int t0 = c * C;
-        Obs nxt[C];
-        load_chunk<MODEL, C>(nxt, a, xb, ab, rb, t0 - C, Tp);
-        double abuf[C][K];
-        double lsbuf[FULL ? C : 1];
-        int exbuf = 0;
-        double ls0 = a.ckpt_ls[p + a.P * (int64_t)c];
+    const int clast = nchunk - 1;
+    load_chunk<MODEL, C, AUX>(cur, sp, clast * C, ln.Tp);
+    const int myc = (ln.Tp - 1) / C; /* this lane's last chunk: its checkpoint exists */
+    double ck[K], ck_ls = 0.0;
+    {
+        const int cc = min(clast, myc);
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            abuf[0][k] = a.ckpt[p + a.P * ((int64_t)c * K + k)];
-        if constexpr (FULL)
-            lsbuf[0] = ls0;
-        double lsacc = 0.0;
+            ck[k] = a.ckpt[p + a.P * ((int64_t)cc * K + k)];
+        if constexpr (MODE == FB_FULL)
+            ck_ls = a.ckpt_ls[p + a.P * (int64_t)cc];
+    }
+    for (int c = clast; c >= 0; --c) {
+        Obs nxt[C];
+        load_chunk<MODEL, C, AUX>(nxt, sp, (c - 1) * C, ln.Tp);
+        double cn[K], cn_ls = 0.0;
+        {
+            const int cc = min(max(c - 1, 0), myc);
 #pragma unroll
-        for (int u = 1; u < C; ++u) {
-            if (t0 + u < Tp) {
-                double e[K];
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    abuf[u][k] = abuf[u - 1][k];
-                emit_prob<MODEL, K>(pp, slab, a.L, cur[u], e, lsacc);
-                fwd_step<MODEL, K>(abuf[u], pp, e, cur[u], exbuf);
-                if constexpr (FULL)
-                    lsbuf[u] = ls0 + (lsacc + kLn2 * exbuf);
-            }
+            for (int k = 0; k < K; ++k)
+                cn[k] = a.ckpt[p + a.P * ((int64_t)cc * K + k)];
+            if constexpr (MODE == FB_FULL)
+                cn_ls = a.ckpt_ls[p + a.P * (int64_t)cc];
         }
-#pragma unroll
-        for (int u = C - 1; u >= 0; --u) {
-            const int t = t0 + u;
-            if (t < Tp) {
-                double lsa = 0.0;
-                if constexpr (FULL)
-                    lsa = lsbuf[u];
-                if (want_alpha)
-                    emit_alpha<K>(a, p, t, abuf[u], lsa);
-                double sb = be[0];
-#pragma unroll
-                for (int k = 1; k < K; ++k)
-                    sb += be[k];
-                if (want_beta) {
-                    if ((a.outputs & HHMM_OUT_BETA) && a.beta) {
-                        const double r = 1.0 / sb;
-                        double v[K];
-#pragma unroll
-                        for (int k = 0; k < K; ++k)
-                            v[k] = be[k] * r;
-                        store_tk<K>(a.beta, a, p, t, v);
-                    }
-                    if ((a.outputs & HHMM_OUT_UNBETA) && a.unbeta) {
-                        /* unbeta_tk[T] = 1 (Q1): every unbeta carries +1 */
-                        double v[K];
-#pragma unroll
-                        for (int k = 0; k < K; ++k)
-                            v[k] = (log(be[k]) + (blsc + kLn2 * bex)) + 1.0;
-                        store_tk<K>(a.unbeta, a, p, t, v);
-                    }
-                }
-                if (want_gamma) {
-                    double sa = abuf[u][0];
-#pragma unroll
-                    for (int k = 1; k < K; ++k)
-                        sa += abuf[u][k];
-                    const double ra = 1.0 / sa, rb2 = 1.0 / sb;
-                    double ug[K];
-                    double sg = 0.0;
-#pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        ug[k] = (abuf[u][k] * ra) * (be[k] * rb2);
-                        sg += ug[k];
-                    }
-                    if ((a.outputs & HHMM_OUT_UNGAMMA) && a.ungamma)
-                        store_tk<K>(a.ungamma, a, p, t, ug);
-                    if ((a.outputs & HHMM_OUT_GAMMA) && a.gamma) {
-                        const double rg = 1.0 / sg;
-                        double v[K];
-#pragma unroll
-                        for (int k = 0; k < K; ++k)
-                            v[k] = ug[k] * rg;
-                        store_tk<K>(a.gamma, a, p, t, v);
-                    }
-                }
-                if (t > 0) {
-                    double e[K];
-                    emit_prob<MODEL, K>(pp, slab, a.L, cur[u], e, blsc);
-                    bwd_step<MODEL, K>(be, pp, e, cur[u], bex);
-                }
-            }
-        }
+        if (c < nfull)
+            bwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, ck, ck_ls, be, blsc, bex);
+        else
+            bwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, ck, ck_ls, be, blsc, bex);
 #pragma unroll
         for (int u = 0; u < C; ++u)
             cur[u] = nxt[u];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ck[k] = cn[k];
+        ck_ls = cn_ls;
     }
 }
 
@@ -658,20 +784,113 @@ __device__ __forceinline__ void emit_log(const PairParams<MODEL, K> &pp, const d
     }
 }
 
+/* Viterbi chunk length: a multiple of the back-pointer steps per word so
+ * that every word boundary falls on a static unrolled slot. */
+constexpr int vit_chunk(int K)
+{
+    return bp_steps_per_word(K) >= 8 ? bp_steps_per_word(K)
+                                      : (8 % bp_steps_per_word(K) == 0 ? 8 : 2 * bp_steps_per_word(K));
+}
+
+/* One max-plus step t >= 1: delta_t(j) = max_i cand(i, j) with the
+ * reference's strict '>' from -inf (first maximising i wins, NaN never
+ * wins); back-pointer i packed into `word` at `slot`. */
 template <int MODEL, int K>
-__global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
+__device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
+                                         const Obs &o, uint32_t &word, int slot)
+{
+    constexpr int BITS = bp_bits(K);
+    constexpr int STEPB = K * BITS;
+    double nd[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double best = dev_ninf();
+        uint32_t arg = 0;
+        bool on = true;
+        if constexpr (ModelTraits<MODEL>::kTayal)
+            on = tayal_pred(o.aux, j);
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            double cand;
+            if constexpr (ModelTraits<MODEL>::kTayal) {
+                /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
+                cand = dl[i] + le[j];
+                cand = on ? cand + pp.A[i][j] : cand;
+            } else {
+                /* (delta + log A) + emission (hmm.stan:111) */
+                cand = (dl[i] + pp.A[i][j]) + le[j];
+            }
+            if (cand > best) {
+                best = cand;
+                arg = (uint32_t)i;
+            }
+        }
+        nd[j] = best;
+        word |= arg << (slot * STEPB + j * BITS);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        dl[j] = nd[j];
+}
+
+template <int MODEL, int K, int CV, bool FULLC>
+__device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, const PairParams<MODEL, K> &pp, const double2 *slab,
+                                              int Tp, int c, const Obs (&cur)[CV], const Obs &nxt0, double (&le)[K],
+                                              double (&dl)[K], uint32_t &word, uint32_t *bpp)
+{
+    constexpr int SPW = bp_steps_per_word(K);
+    const int t0 = c * CV;
+#pragma unroll
+    for (int u = 0; u < CV; ++u) {
+        const int t = t0 + u;
+        double ln[K];
+        emit_log<MODEL, K>(pp, slab, a.L, (u + 1 < CV) ? cur[u + 1 < CV ? u + 1 : 0] : nxt0, ln);
+        if (FULLC || t < Tp) {
+            if (!(u == 0 && c == 0))
+                vit_step<MODEL, K>(dl, pp, le, cur[u], word, u % SPW);
+            if (u % SPW == SPW - 1) {
+                bpp[a.P * (int64_t)(t / SPW)] = word;
+                word = 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            le[k] = ln[k];
+    }
+}
+
+/* Backtrack over chunk c (descending): writes zstar[t] and steps z. */
+template <int K, int CV, bool FULLC>
+__device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int Tp, int c, const uint32_t (&w)[CV / bp_steps_per_word(K)],
+                                               int &z, int32_t *zp)
 {
     constexpr int BITS = bp_bits(K);
     constexpr int SPW = bp_steps_per_word(K);
     constexpr int STEPB = K * BITS;
     constexpr uint32_t MASK = (1u << BITS) - 1u;
-    constexpr int C = 8;
+    const int t0 = c * CV;
+#pragma unroll
+    for (int u = CV - 1; u >= 0; --u) {
+        const int t = t0 + u;
+        if (FULLC || t < Tp) {
+            zp[a.P * (int64_t)t] = z + 1;
+            if (t > 0)
+                z = (int)((w[u / SPW] >> ((u % SPW) * STEPB + z * BITS)) & MASK);
+        }
+    }
+}
+
+template <int MODEL, int K>
+__global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
+{
+    constexpr int SPW = bp_steps_per_word(K);
+    constexpr int CV = vit_chunk(K);
+    constexpr int WPC = CV / SPW; /* words per chunk */
+    constexpr bool VAUX = ModelTraits<MODEL>::kTayal; /* semisup Viterbi is unmasked (Q7) */
     HIP_DYNAMIC_SHARED(double2, lds)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.P)
-        return;
+    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
@@ -682,83 +901,38 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
     load_params<MODEL, K, true>(pp, a, d);
     if constexpr (ModelTraits<MODEL>::kDiscrete)
         fill_table<K, true>(slab, a, d);
+    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, n);
+    const int Tw_min = wave_min(Tp);
+    const int Tw_max = wave_max(Tp);
+    const int nfull = Tw_min / CV;
+    const int nchunk = (Tw_max + CV - 1) / CV;
 
-    const int32_t *xb = a.x ? a.x + n : nullptr;
-    const int32_t *ab = nullptr;
-    if constexpr (ModelTraits<MODEL>::kSemisup)
-        ab = a.g + n;
-    if constexpr (ModelTraits<MODEL>::kTayal)
-        ab = a.sign + n;
-    const double *rb = a.xr ? a.xr + n : nullptr;
-
-    constexpr bool VAUX = ModelTraits<MODEL>::kTayal; /* semisup Viterbi is unmasked (Q7) */
     /* delta_tk[1, K] = emission of j for j = 1..K: only column K is written,
      * the others keep stanc's NaN (Q3, e.g. hmm-multinom.stan:236-237). */
     double dl[K];
-    Obs cur[C];
-    load_chunk<MODEL, C, VAUX>(cur, a, xb, ab, rb, 0, Tp);
-    {
-        double le[K];
-        emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
+    Obs cur[CV];
+    load_chunk<MODEL, CV, VAUX>(cur, sp, 0, Tp);
+    double le[K];
+    emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
 #pragma unroll
-        for (int k = 0; k < K - 1; ++k)
-            dl[k] = dev_nan();
-        dl[K - 1] = le[K - 1];
-    }
+    for (int k = 0; k < K - 1; ++k)
+        dl[k] = dev_nan();
+    dl[K - 1] = le[K - 1];
     uint32_t word = 0;
     uint32_t *bpp = a.bp + p;
-    const int nchunk = (Tp + C - 1) / C;
     for (int c = 0; c < nchunk; ++c) {
-        const int t0 = c * C;
-        Obs nxt[C];
-        load_chunk<MODEL, C, VAUX>(nxt, a, xb, ab, rb, t0 + C, Tp);
+        Obs nxt[CV];
+        load_chunk<MODEL, CV, VAUX>(nxt, sp, (c + 1) * CV, Tp);
+        if (c < nfull)
+            vit_fwd_chunk<MODEL, K, CV, true>(a, pp, slab, Tp, c, cur, nxt[0], le, dl, word, bpp);
+        else
+            vit_fwd_chunk<MODEL, K, CV, false>(a, pp, slab, Tp, c, cur, nxt[0], le, dl, word, bpp);
 #pragma unroll
-        for (int u = 0; u < C; ++u) {
-            const int t = t0 + u;
-            if (t >= 1 && t < Tp) {
-                double le[K];
-                emit_log<MODEL, K>(pp, slab, a.L, cur[u], le);
-                double nd[K];
-                const int slot = t % SPW;
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    double best = dev_ninf();
-                    uint32_t arg = 0;
-                    bool on = true;
-                    if constexpr (ModelTraits<MODEL>::kTayal)
-                        on = tayal_pred(cur[u].aux, j);
-#pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        double cand;
-                        if constexpr (ModelTraits<MODEL>::kTayal) {
-                            /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
-                            cand = dl[i] + le[j];
-                            cand = on ? cand + pp.A[i][j] : cand;
-                        } else {
-                            /* (delta + log A) + emission (hmm.stan:111) */
-                            cand = (dl[i] + pp.A[i][j]) + le[j];
-                        }
-                        if (cand > best) {
-                            best = cand;
-                            arg = (uint32_t)i;
-                        }
-                    }
-                    nd[j] = best;
-                    word |= arg << (slot * STEPB + j * BITS);
-                }
-#pragma unroll
-                for (int j = 0; j < K; ++j)
-                    dl[j] = nd[j];
-                if (slot == SPW - 1 || t == Tp - 1) {
-                    bpp[a.P * (int64_t)(t / SPW)] = word;
-                    word = 0;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < C; ++u)
+        for (int u = 0; u < CV; ++u)
             cur[u] = nxt[u];
     }
+    if ((Tp - 1) % SPW != SPW - 1) /* partial last word */
+        bpp[a.P * (int64_t)((Tp - 1) / SPW)] = word;
 
     /* logp_zstar = max(delta_tk[T]); zstar[T] = LAST j attaining it (hmm.stan:120-124). */
     const double lp = stan_max_vec<K>(dl);
@@ -782,20 +956,25 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
             zp[a.P * (int64_t)t] = 0;
         return;
     }
-    zp[a.P * (int64_t)(Tp - 1)] = z + 1;
-    int wi = (Tp - 1) / SPW;
-    uint32_t w = bpp[a.P * (int64_t)wi];
-    uint32_t wprev = (wi > 0) ? bpp[a.P * (int64_t)(wi - 1)] : 0u;
-    for (int t = Tp - 1; t >= 1; --t) {
-        const int wt = t / SPW;
-        if (wt != wi) {
-            w = wprev;
-            wi = wt;
-            wprev = (wi > 0) ? bpp[a.P * (int64_t)(wi - 1)] : 0u;
-        }
-        const int slot = t % SPW;
-        z = (int)((w >> (slot * STEPB + z * BITS)) & MASK);
-        zp[a.P * (int64_t)(t - 1)] = z + 1;
+    /* backtrack, chunk by chunk, words prefetched one chunk ahead; word
+     * indices are clamped into this lane's range (never read past Tp) */
+    const int wmax = (Tp - 1) / SPW;
+    uint32_t w[WPC], wn[WPC];
+    const int clast = nchunk - 1;
+#pragma unroll
+    for (int i = 0; i < WPC; ++i)
+        w[i] = bpp[a.P * (int64_t)min(clast * WPC + i, wmax)];
+    for (int c = clast; c >= 0; --c) {
+#pragma unroll
+        for (int i = 0; i < WPC; ++i)
+            wn[i] = bpp[a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax)];
+        if (c < nfull)
+            vit_back_chunk<K, CV, true>(a, Tp, c, w, z, zp);
+        else
+            vit_back_chunk<K, CV, false>(a, Tp, c, w, z, zp);
+#pragma unroll
+        for (int i = 0; i < WPC; ++i)
+            w[i] = wn[i];
     }
 }
 
@@ -893,13 +1072,13 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
-    const bool full = (a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) != 0;
+    const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     if (fwd_only)
-        hipLaunchKernelGGL((fb_kernel<MODEL, K, true, false>), s.grid, s.block, s.lds, st, a);
-    else if (full)
-        hipLaunchKernelGGL((fb_kernel<MODEL, K, false, true>), s.grid, s.block, s.lds, st, a);
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FWD>), s.grid, s.block, s.lds, st, a);
+    else if (a.outputs & extra)
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FULL>), s.grid, s.block, s.lds, st, a);
     else
-        hipLaunchKernelGGL((fb_kernel<MODEL, K, false, false>), s.grid, s.block, s.lds, st, a);
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA>), s.grid, s.block, s.lds, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("fb_kernel launch: %s", hipGetErrorString(e));

@@ -1,0 +1,134 @@
+"""CPU: the C-ABI shared library (libhhmm.so) loads, exports every entry point
+include/hhmm.h declares, and its structs have the layout the header gives
+(checked against gcc's offsetof, not just against our own ctypes mirror).
+No compute call needs a GPU here; without one the engine must fail loudly."""
+import ctypes as C
+import pathlib
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from hhmm_amd import _abi, api, synth
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+HEADER = REPO / "include" / "hhmm.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hhmm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for n in ("hhmm_run", "hhmm_run_device", "hhmm_workspace_size", "hhmm_validate", "hhmm_version",
+              "hhmm_last_error", "hhmm_init", "hhmm_shutdown", "hhmm_num_pairs", "hhmm_selftest_cr_log"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol(engine):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(api.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (hhmm_\w+)", out))
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+    for n in declared_functions():
+        getattr(engine, n)  # resolvable through ctypes
+
+
+def _c_layout(tmp_path):
+    fields = {
+        "hhmm_data": [f[0] for f in _abi.Data._fields_],
+        "hhmm_draws": [f[0] for f in _abi.Draws._fields_],
+        "hhmm_request": [f[0] for f in _abi.Request._fields_],
+        "hhmm_result": [f[0] for f in _abi.Result._fields_],
+    }
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "hhmm.h"', "int main(void){"]
+    for st, fs in fields.items():
+        src.append(f'printf("{st} sizeof %zu\\n", sizeof({st}));')
+        for f in fs:
+            src.append(f'printf("{st} {f} %zu\\n", offsetof({st}, {f}));')
+    src.append("return 0;}")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(REPO / "include"), str(c), "-o", str(exe)], check=True)
+    rows = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    return {tuple(r.split()[:2]): int(r.split()[2]) for r in rows if r}
+
+
+def test_struct_layout_matches_header(tmp_path):
+    lay = _c_layout(tmp_path)
+    for cname, cls in (("hhmm_data", _abi.Data), ("hhmm_draws", _abi.Draws), ("hhmm_request", _abi.Request),
+                       ("hhmm_result", _abi.Result)):
+        assert lay[(cname, "sizeof")] == C.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert lay[(cname, f)] == getattr(cls, f).offset, (cname, f)
+
+
+def _prepared(model="hmm-multinom", **kw):
+    data, draws = synth.GENERATORS[model](N=2, S=3, T=10, **kw)
+    return api.PreparedRequest(model, data, draws, synth.PARS[model])
+
+
+def _validate(engine, pr, host=1):
+    return engine.hhmm_validate(C.byref(pr.req), C.byref(pr.res), host)
+
+
+def test_validate_accepts_good_requests(engine):
+    for m in synth.GENERATORS:
+        pr = _prepared(m)
+        assert _validate(engine, pr) == _abi.OK, (m, engine.hhmm_last_error())
+
+
+def test_validate_rejects_out_of_range_data(engine):
+    pr = _prepared()
+    pr.keep[0][0, 3] = 10  # x outside 1..L (int<lower=1, upper=L> x[T])
+    assert _validate(engine, pr) == _abi.ERR_INVALID_ARGUMENT
+    assert b"outside 1..L" in engine.hhmm_last_error()
+    # a device-pointer request is not range-checked on the host
+    assert _validate(engine, pr, host=0) == _abi.OK
+
+
+def test_validate_rejects_bad_requests(engine):
+    pr = _prepared()
+    pr.req.abi_version = 99
+    assert _validate(engine, pr) == _abi.ERR_INVALID_ARGUMENT
+    pr = _prepared()
+    pr.req.outputs |= _abi.OUT["oblik_t"]  # not declared by hmm-multinom.stan
+    assert _validate(engine, pr) == _abi.ERR_INVALID_ARGUMENT
+    pr = _prepared()
+    pr.res.gamma_tk = None
+    assert _validate(engine, pr) == _abi.ERR_INVALID_ARGUMENT
+    pr = _prepared("hhmm-tayal2009")
+    pr.req.data.K = 3
+    assert _validate(engine, pr) == _abi.ERR_INVALID_ARGUMENT
+    pr = _prepared()
+    pr.req.pairing = _abi.PAIR_ZIP  # N=2 series vs S=3 draws
+    assert _validate(engine, pr) == _abi.ERR_INVALID_ARGUMENT
+    assert engine.hhmm_num_pairs(C.byref(pr.req)) == -1
+
+
+def test_workspace_size_positive(engine):
+    pr = _prepared()
+    n = C.c_size_t(0)
+    assert engine.hhmm_workspace_size(C.byref(pr.req), C.byref(n)) == _abi.OK
+    assert n.value > 0
+
+
+def test_no_cpu_fallback_without_gpu(engine):
+    """The product path has no CPU fallback: without a gfx950 device it fails."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    data, draws = synth.hmm_multinom(N=1, S=2, T=5)
+    with pytest.raises(api.HHMMError) as e:
+        api.gqs("hmm-multinom", data, draws, lib=engine)
+    assert e.value.status == _abi.ERR_NO_DEVICE
+
+
+def test_version_string(engine):
+    assert engine.hhmm_version().startswith(b"hhmm-mi355x")

@@ -1,0 +1,77 @@
+"""CPU: the shared correctly rounded log (gsoc17-hhmm_amd/csrc/hhmm_crmath.h).
+
+Stan evaluates every log on the path with the platform libm.  The engine and
+the oracle both use hhmm_cr_log instead, so that Viterbi paths are
+bit-reproducible between CPU and GPU.  These tests pin it:
+  * against a 60-digit decimal logarithm rounded once (correct rounding),
+  * against glibc's log: they agree except where glibc itself misrounds
+    (glibc 2.35 log is documented at < 0.52 ulp, not correctly rounded).
+"""
+import decimal
+import math
+
+import numpy as np
+import pytest
+
+D = decimal.Decimal
+
+
+def _cr_reference(x):
+    with decimal.localcontext() as ctx:
+        ctx.prec = 60
+        return float(D(x).ln())
+
+
+def _samples(n, seed=11):
+    g = np.random.Generator(np.random.Philox(seed))
+    bits = g.integers(1, 0x7FF0000000000000, size=n, dtype=np.int64).view(np.float64)
+    near1 = 1.0 + (g.random(n) - 0.5) * 2.0 ** -5
+    unit = g.random(n)
+    probs = g.dirichlet(np.ones(9), size=n // 9 + 1).ravel()[:n]  # simplex entries, as on the path
+    sub = g.integers(1, 1 << 52, size=n // 10, dtype=np.int64).view(np.float64)  # subnormals
+    return np.concatenate([bits, near1, unit, probs, sub])
+
+
+def test_crlog_is_correctly_rounded(oracle):
+    x = _samples(1500)
+    y = oracle.log_array(x, "cr")
+    ref = np.array([_cr_reference(v) for v in x])
+    bad = np.flatnonzero(y != ref)
+    assert bad.size == 0, [(x[i].hex(), y[i].hex(), ref[i].hex()) for i in bad[:5]]
+
+
+def test_crlog_special_values(oracle):
+    x = np.array([1.0, 0.0, -0.0, -1.0, np.inf, np.nan, 2.0, 0.5, 5e-324, 1.7976931348623157e308,
+                  1 - 2 ** -53, 1 + 2 ** -52])
+    y = oracle.log_array(x, "cr")
+    assert y[0] == 0.0 and math.copysign(1, y[0]) == 1.0
+    assert y[1] == -np.inf and y[2] == -np.inf
+    assert np.isnan(y[3]) and np.isnan(y[5])
+    assert y[4] == np.inf
+    assert y[6] == math.log(2.0) and y[7] == -math.log(2.0)
+    for v, r in zip(x[8:], y[8:]):
+        assert r == _cr_reference(v)
+
+
+def test_crlog_agrees_with_glibc_where_glibc_rounds_correctly(oracle):
+    x = _samples(200_000, seed=5)
+    cr = oracle.log_array(x, "cr")
+    lm = oracle.log_array(x, "libm")
+    diff = np.flatnonzero(cr != lm)
+    rate = diff.size / x.size
+    assert rate < 2e-3, rate
+    # every disagreement is a glibc misrounding: ours equals the correctly rounded value
+    for i in diff[:200]:
+        assert cr[i] == _cr_reference(x[i]), x[i].hex()
+        assert abs(cr[i] - lm[i]) <= np.spacing(abs(cr[i]))
+
+
+@pytest.mark.parametrize("variant", ["cr", "libm"])
+def test_neg_log_sqrt_two_pi_constant(oracle, variant):
+    """Stan's NEG_LOG_SQRT_TWO_PI = -log(sqrt(2 pi)) as baked into the shared header."""
+    import re
+    import pathlib
+    hdr = (pathlib.Path(__file__).resolve().parent.parent / "gsoc17-hhmm_amd" / "csrc" /
+           "hhmm_crlog_table.h").read_text()
+    m = re.search(r"#define HHMM_NEG_LOG_SQRT_TWO_PI (\S+)", hdr)
+    assert float.fromhex(m.group(1)) == -math.log(math.sqrt(2.0 * math.pi))

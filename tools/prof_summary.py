@@ -27,9 +27,8 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 
 
 def short(name):
-    for key in ("fb_kernel", "viterbi_kernel", "cr_log_kernel", "scan_", "ffbs_", "iohmm_"):
-        if key in name:
-            return name.split("(")[0].replace("void ", "")
+    if "hhmm::" in name:
+        return name.split("(")[0].replace("void ", "")
     return None
 
 
