@@ -202,6 +202,9 @@ static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool ho
     REQUIRE(npairs(r) >= 1, "ZIP pairing needs n_series == n_draws (%lld vs %lld)", (long long)d.n_series,
             (long long)w.n_draws);
     REQUIRE(d.T_max >= 1, "T_max must be >= 1 (int<lower=1> T)");
+    /* kernels address rows as uniform base + 32-bit lane offset (8-byte elements) */
+    REQUIRE(npairs(r) <= (int64_t(1) << 28) && d.n_series <= (int64_t(1) << 28) && w.n_draws <= (int64_t(1) << 28),
+            "at most 2^28 pairs / series / draws per call (split larger batches)");
     REQUIRE(d.K >= 1, "K must be >= 1 (int<lower=1> K)");
     const int m = r->model;
     if (is_discrete(m))

@@ -91,6 +91,19 @@ __device__ __forceinline__ double stan_max_vec(const double (&d)[K])
     }
 }
 
+/* Element of a row addressed as (uniform row pointer) + (32-bit lane byte
+ * offset): lets hipcc emit SGPR-base + VGPR-offset global memory ops. */
+template <typename T>
+__device__ __forceinline__ T &at(T *row, uint32_t byte_off)
+{
+    return *reinterpret_cast<T *>(reinterpret_cast<char *>(row) + byte_off);
+}
+template <typename T>
+__device__ __forceinline__ const T &at(const T *row, uint32_t byte_off)
+{
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(row) + byte_off);
+}
+
 /* Lazy power-of-two renormalisation of a K-vector: only when the largest
  * entry's exponent leaves [-255, 256] (rare; a scalar-skipped branch).  The
  * removed exponent is accumulated in `ex`; mx == 0 / NaN leave v unchanged. */
@@ -112,19 +125,22 @@ __device__ __forceinline__ void renorm(double (&v)[K], int &ex)
     }
 }
 
+/* Wave-wide min / max, returned through readfirstlane so that hipcc knows
+ * the result is uniform: every time index derived from it (row pointers of
+ * the per-step loads and stores) is then computed on the scalar unit. */
 __device__ __forceinline__ int wave_min(int v)
 {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
         v = min(v, __shfl_xor(v, off));
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ int wave_max(int v)
 {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
         v = max(v, __shfl_xor(v, off));
-    return v;
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
 /* hmm-multinom-semisup.stan:42 -- j0 is 0-based */
@@ -162,34 +178,39 @@ struct Obs {
     double xr; /* real observation (gauss) */
 };
 
-/* Per-lane view of one series' observation streams (series-fastest arrays). */
+/* Observation streams of one series (series-fastest arrays): uniform base
+ * pointers + this lane's 32-bit series index.  A time row t is the uniform
+ * pointer base + N*t, so hipcc can address it as SGPR base + VGPR offset. */
 struct SeriesPtrs {
     const int32_t *x;
     const int32_t *aux;
     const double *xr;
     int64_t stride; /* N: elements between consecutive time steps */
+    uint32_t n;     /* this lane's series */
+    int tmax;       /* padded time extent of the arrays */
 };
 
 /* Loads the C observations of chunk [t0, t0+C).  Every load is issued
- * unconditionally from a time index clamped into [0, Tp-1]: a conditional
- * load makes hipcc branch around it and drain vmcnt(0) per element
- * (cdna_hip_programming.md §5, trap (c)); steps past Tp are never consumed. */
+ * unconditionally from a wave-uniform time index clamped into [0, Tmax-1]: a
+ * conditional load makes hipcc branch around it and drain vmcnt(0) per
+ * element (cdna_hip_programming.md §5, trap (c)); rows past a lane's own
+ * length are padding that is never consumed. */
 template <int MODEL, int C, bool AUX>
-__device__ __forceinline__ void load_chunk(Obs (&dst)[C], const SeriesPtrs &sp, int t0, int Tp)
+__device__ __forceinline__ void load_chunk(Obs (&dst)[C], const SeriesPtrs &sp, int t0)
 {
 #pragma unroll
     for (int u = 0; u < C; ++u) {
-        const int tc = min(max(t0 + u, 0), Tp - 1);
-        const int64_t off = (int64_t)tc * sp.stride;
+        const int tc = min(max(t0 + u, 0), sp.tmax - 1);
+        const int64_t row = (int64_t)tc * sp.stride;
         dst[u].x = 1;
         dst[u].aux = 0;
         dst[u].xr = 0.0;
         if constexpr (!ModelTraits<MODEL>::kGauss)
-            dst[u].x = sp.x[off];
+            dst[u].x = at(sp.x + row, sp.n * 4u);
         if constexpr (AUX)
-            dst[u].aux = sp.aux[off];
+            dst[u].aux = at(sp.aux + row, sp.n * 4u);
         if constexpr (ModelTraits<MODEL>::kGauss)
-            dst[u].xr = sp.xr[off];
+            dst[u].xr = at(sp.xr + row, sp.n * 8u);
     }
 }
 
@@ -330,10 +351,10 @@ __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const 
     }
 }
 
-/* alpha_t = e_t .* (alpha_{t-1} M_t), with the model's transition masks. */
+/* out = e_t .* (in M_t), with the model's transition masks; in may alias out. */
 template <int MODEL, int K>
-__device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL, K> &pp,
-                                         const double (&e)[K], const Obs &o, int &ex)
+__device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
+                                            const double (&e)[K], const Obs &o, int &ex)
 {
     double s[K];
 #pragma unroll
@@ -361,8 +382,15 @@ __device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL
     }
 #pragma unroll
     for (int j = 0; j < K; ++j)
-        al[j] = s[j] * e[j];
-    renorm<K>(al, ex);
+        out[j] = s[j] * e[j];
+    renorm<K>(out, ex);
+}
+
+template <int MODEL, int K>
+__device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL, K> &pp, const double (&e)[K],
+                                         const Obs &o, int &ex)
+{
+    fwd_step_to<MODEL, K>(al, al, pp, e, o, ex);
 }
 
 /* beta_{t-1} from beta_t and step t's emission / masks. */
@@ -452,13 +480,15 @@ __device__ __forceinline__ SeriesPtrs series_ptrs(const DevArgs &a, int64_t n)
 {
     SeriesPtrs sp;
     sp.stride = a.N;
-    sp.x = a.x ? a.x + n : nullptr;
+    sp.n = (uint32_t)n;
+    sp.tmax = a.Tmax;
+    sp.x = a.x;
     sp.aux = nullptr;
     if constexpr (AUX && ModelTraits<MODEL>::kSemisup)
-        sp.aux = a.g + n;
+        sp.aux = a.g;
     if constexpr (AUX && ModelTraits<MODEL>::kTayal)
-        sp.aux = a.sign + n;
-    sp.xr = a.xr ? a.xr + n : nullptr;
+        sp.aux = a.sign;
+    sp.xr = a.xr;
     return sp;
 }
 
@@ -473,12 +503,26 @@ enum FbMode {
     FB_FWD = 2    /* forward only: loglik / alpha / unalpha (tayal-lite, no backward output) */
 };
 
+/* out[p, t, k] for k = 0..K-1: uniform row pointer out + P*(t + Tout*k)
+ * (SGPR base) plus the lane's 32-bit pair index (P < 2^29 per launch). */
 template <int K>
 __device__ __forceinline__ void store_tk(double *out, const DevArgs &a, int64_t p, int t, const double (&v)[K])
 {
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        out[p + a.P * ((int64_t)t + (int64_t)a.Tout * k)] = v[k];
+        at(out + a.P * ((int64_t)t + (int64_t)a.Tout * k), (uint32_t)p * 8u) = v[k];
+}
+
+/* 1/x to ~1 ulp: v_rcp_f64 + two Newton steps (tolerance 1e-9 outputs only);
+ * IEEE division for x below 2^-1000 where the reciprocal would overflow. */
+__device__ __forceinline__ double fast_rcp(double x)
+{
+    if (__builtin_expect(!(x > 0x1p-1000), 0))
+        return 1.0 / x;
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return r;
 }
 
 template <int K>
@@ -524,7 +568,7 @@ __device__ __forceinline__ void emit_posteriors(const DevArgs &a, int64_t p, int
 #pragma unroll
         for (int k = 0; k < K; ++k)
             ug[k] = al[k] * be[k];
-        const double r = 1.0 / vsum<K>(ug);
+        const double r = fast_rcp(vsum<K>(ug));
 #pragma unroll
         for (int k = 0; k < K; ++k)
             ug[k] = ug[k] * r;
@@ -604,9 +648,9 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
             } else if (u == 0) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    a.ckpt[ln.p + a.P * ((int64_t)c * K + k)] = al[k];
+                    at(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)ln.p * 8u) = al[k];
                 if constexpr (MODE == FB_FULL)
-                    a.ckpt_ls[ln.p + a.P * (int64_t)c] = lsc + kLn2 * ex;
+                    at(a.ckpt_ls + a.P * (int64_t)c, (uint32_t)ln.p * 8u) = lsc + kLn2 * ex;
             }
         }
         ecur = enx;
@@ -636,12 +680,9 @@ __device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, 
         for (int u = 1; u < C; ++u) {
             Em<K> enx;
             emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[u + 1 < C ? u + 1 : u], enx);
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                abuf[u][k] = abuf[u - 1][k];
             if (FULLC || t0 + u < ln.Tp) {
                 lsacc += ecur.m;
-                fwd_step<MODEL, K>(abuf[u], ln.pp, ecur.e, cur[u], exb);
+                fwd_step_to<MODEL, K>(abuf[u - 1], abuf[u], ln.pp, ecur.e, cur[u], exb);
             }
             if constexpr (MODE == FB_FULL)
                 lsbuf[u] = ck_ls + (lsacc + kLn2 * exb);
@@ -702,12 +743,12 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
     double lsc = 0.0; /* log scale excluding the binary exponent */
     int ex = 0;       /* sum of binary exponents removed */
     Obs cur[C];
-    load_chunk<MODEL, C, AUX>(cur, sp, 0, ln.Tp);
+    load_chunk<MODEL, C, AUX>(cur, sp, 0);
     Em<K> ecur;
     emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[0], ecur);
     for (int c = 0; c < nchunk; ++c) {
         Obs nxt[C];
-        load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C, ln.Tp);
+        load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C);
         if (c < nfull)
             fwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
         else
@@ -729,28 +770,29 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
     double blsc = 0.0;
     int bex = 0;
     const int clast = nchunk - 1;
-    load_chunk<MODEL, C, AUX>(cur, sp, clast * C, ln.Tp);
-    const int myc = (ln.Tp - 1) / C; /* this lane's last chunk: its checkpoint exists */
+    load_chunk<MODEL, C, AUX>(cur, sp, clast * C);
+    /* checkpoint rows are wave-uniform: a lane shorter than the wave reads
+     * (unused) slots past its own last chunk, never past the allocation */
     double ck[K], ck_ls = 0.0;
     {
-        const int cc = min(clast, myc);
+        const int cc = clast;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            ck[k] = a.ckpt[p + a.P * ((int64_t)cc * K + k)];
+            ck[k] = at(a.ckpt + a.P * ((int64_t)cc * K + k), (uint32_t)p * 8u);
         if constexpr (MODE == FB_FULL)
-            ck_ls = a.ckpt_ls[p + a.P * (int64_t)cc];
+            ck_ls = at(a.ckpt_ls + a.P * (int64_t)cc, (uint32_t)p * 8u);
     }
     for (int c = clast; c >= 0; --c) {
         Obs nxt[C];
-        load_chunk<MODEL, C, AUX>(nxt, sp, (c - 1) * C, ln.Tp);
+        load_chunk<MODEL, C, AUX>(nxt, sp, (c - 1) * C);
         double cn[K], cn_ls = 0.0;
         {
-            const int cc = min(max(c - 1, 0), myc);
+            const int cc = max(c - 1, 0);
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                cn[k] = a.ckpt[p + a.P * ((int64_t)cc * K + k)];
+                cn[k] = at(a.ckpt + a.P * ((int64_t)cc * K + k), (uint32_t)p * 8u);
             if constexpr (MODE == FB_FULL)
-                cn_ls = a.ckpt_ls[p + a.P * (int64_t)cc];
+                cn_ls = at(a.ckpt_ls + a.P * (int64_t)cc, (uint32_t)p * 8u);
         }
         if (c < nfull)
             bwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, ck, ck_ls, be, blsc, bex);
@@ -834,9 +876,9 @@ __device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL
 }
 
 template <int MODEL, int K, int CV, bool FULLC>
-__device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, const PairParams<MODEL, K> &pp, const double2 *slab,
-                                              int Tp, int c, const Obs (&cur)[CV], const Obs &nxt0, double (&le)[K],
-                                              double (&dl)[K], uint32_t &word, uint32_t *bpp)
+__device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const PairParams<MODEL, K> &pp,
+                                              const double2 *slab, int Tp, int c, const Obs (&cur)[CV],
+                                              const Obs &nxt0, double (&le)[K], double (&dl)[K], uint32_t &word)
 {
     constexpr int SPW = bp_steps_per_word(K);
     const int t0 = c * CV;
@@ -849,7 +891,7 @@ __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, const PairParams
             if (!(u == 0 && c == 0))
                 vit_step<MODEL, K>(dl, pp, le, cur[u], word, u % SPW);
             if (u % SPW == SPW - 1) {
-                bpp[a.P * (int64_t)(t / SPW)] = word;
+                at(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u) = word;
                 word = 0;
             }
         }
@@ -861,8 +903,8 @@ __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, const PairParams
 
 /* Backtrack over chunk c (descending): writes zstar[t] and steps z. */
 template <int K, int CV, bool FULLC>
-__device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int Tp, int c, const uint32_t (&w)[CV / bp_steps_per_word(K)],
-                                               int &z, int32_t *zp)
+__device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int64_t p, int Tp, int c,
+                                               const uint32_t (&w)[CV / bp_steps_per_word(K)], int &z)
 {
     constexpr int BITS = bp_bits(K);
     constexpr int SPW = bp_steps_per_word(K);
@@ -873,7 +915,7 @@ __device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int Tp, int c, 
     for (int u = CV - 1; u >= 0; --u) {
         const int t = t0 + u;
         if (FULLC || t < Tp) {
-            zp[a.P * (int64_t)t] = z + 1;
+            at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = z + 1;
             if (t > 0)
                 z = (int)((w[u / SPW] >> ((u % SPW) * STEPB + z * BITS)) & MASK);
         }
@@ -911,7 +953,7 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
      * the others keep stanc's NaN (Q3, e.g. hmm-multinom.stan:236-237). */
     double dl[K];
     Obs cur[CV];
-    load_chunk<MODEL, CV, VAUX>(cur, sp, 0, Tp);
+    load_chunk<MODEL, CV, VAUX>(cur, sp, 0);
     double le[K];
     emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
 #pragma unroll
@@ -919,20 +961,19 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
         dl[k] = dev_nan();
     dl[K - 1] = le[K - 1];
     uint32_t word = 0;
-    uint32_t *bpp = a.bp + p;
     for (int c = 0; c < nchunk; ++c) {
         Obs nxt[CV];
-        load_chunk<MODEL, CV, VAUX>(nxt, sp, (c + 1) * CV, Tp);
+        load_chunk<MODEL, CV, VAUX>(nxt, sp, (c + 1) * CV);
         if (c < nfull)
-            vit_fwd_chunk<MODEL, K, CV, true>(a, pp, slab, Tp, c, cur, nxt[0], le, dl, word, bpp);
+            vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
         else
-            vit_fwd_chunk<MODEL, K, CV, false>(a, pp, slab, Tp, c, cur, nxt[0], le, dl, word, bpp);
+            vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
 #pragma unroll
         for (int u = 0; u < CV; ++u)
             cur[u] = nxt[u];
     }
     if ((Tp - 1) % SPW != SPW - 1) /* partial last word */
-        bpp[a.P * (int64_t)((Tp - 1) / SPW)] = word;
+        a.bp[p + a.P * (int64_t)((Tp - 1) / SPW)] = word;
 
     /* logp_zstar = max(delta_tk[T]); zstar[T] = LAST j attaining it (hmm.stan:120-124). */
     const double lp = stan_max_vec<K>(dl);
@@ -950,28 +991,28 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
         a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
     if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
         return;
-    int32_t *zp = a.zstar + p;
     if (invalid) {
         for (int t = 0; t < Tp; ++t)
-            zp[a.P * (int64_t)t] = 0;
+            a.zstar[p + a.P * (int64_t)t] = 0;
         return;
     }
-    /* backtrack, chunk by chunk, words prefetched one chunk ahead; word
-     * indices are clamped into this lane's range (never read past Tp) */
-    const int wmax = (Tp - 1) / SPW;
+    /* backtrack, chunk by chunk, words prefetched one chunk ahead; word rows
+     * are wave-uniform, clamped to the allocation (a short lane's extra rows
+     * are never consumed) */
+    const int wmax = a.Tmax / SPW;
     uint32_t w[WPC], wn[WPC];
     const int clast = nchunk - 1;
 #pragma unroll
     for (int i = 0; i < WPC; ++i)
-        w[i] = bpp[a.P * (int64_t)min(clast * WPC + i, wmax)];
+        w[i] = at(a.bp + a.P * (int64_t)min(clast * WPC + i, wmax), (uint32_t)p * 4u);
     for (int c = clast; c >= 0; --c) {
 #pragma unroll
         for (int i = 0; i < WPC; ++i)
-            wn[i] = bpp[a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax)];
+            wn[i] = at(a.bp + a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax), (uint32_t)p * 4u);
         if (c < nfull)
-            vit_back_chunk<K, CV, true>(a, Tp, c, w, z, zp);
+            vit_back_chunk<K, CV, true>(a, p, Tp, c, w, z);
         else
-            vit_back_chunk<K, CV, false>(a, Tp, c, w, z, zp);
+            vit_back_chunk<K, CV, false>(a, p, Tp, c, w, z);
 #pragma unroll
         for (int i = 0; i < WPC; ++i)
             w[i] = wn[i];

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of libhhmm variants in ONE process on ONE device
+(cdna_hip_programming.md §5.4 rule 24: cross-box numbers are not comparable).
+
+  python tools/ab_bench.py NAME=path/to/libhhmm.so [NAME=...] [--rounds 5] [--pairs 1000000] [--T 1000]
+
+Each variant runs the bench.py C2 step (fb_kernel, then viterbi_kernel) on
+the same resident inputs; rounds are interleaved A B C A B C ...; per-kernel
+HIP-event times are reported as median / min over rounds.  Variants also
+cross-check each other's outputs (gamma within 1e-12, zstar exact).
+"""
+import argparse
+import json
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "gsoc17-hhmm_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import hhmm_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--pairs", type=int, default=1_000_000)
+    ap.add_argument("--T", type=int, default=1000)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    libs = {}
+    for v in a.variants:
+        name, path = v.split("=", 1)
+        libs[name] = hhmm_amd.load_library(path)
+    x, draws = bench.make_batch(a.pairs, a.T, 9000, dev)
+    runs = {n: bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev) for n, lib in libs.items()}
+    times = {n: {"fb": [], "vit": []} for n in runs}
+    ref = None
+    for r in range(a.rounds + 1):
+        for n, run in runs.items():
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            torch.cuda.synchronize()
+            ev[0].record()
+            run.launch("fb")
+            ev[1].record()
+            run.launch("viterbi")
+            ev[2].record()
+            torch.cuda.synchronize()
+            if r == 0:  # warm-up round; compare outputs
+                g = run.out["gamma_tk"][:, :, :4096].cpu()
+                z = run.out["zstar_t"][:, :4096].cpu()
+                if ref is None:
+                    ref = (g, z)
+                else:
+                    dg = float((g - ref[0]).abs().max())
+                    same = bool(torch.equal(z, ref[1]))
+                    print(f"{n}: max |dgamma| vs first variant {dg:.3e}, zstar identical {same}", flush=True)
+                continue
+            times[n]["fb"].append(ev[0].elapsed_time(ev[1]))
+            times[n]["vit"].append(ev[1].elapsed_time(ev[2]))
+    out = {}
+    for n, t in times.items():
+        out[n] = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for k, v in t.items()}
+        print(n, json.dumps(out[n]), flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
