@@ -155,8 +155,7 @@ static uint32_t available_outputs(int m)
 /* Models with a gfx950 path in this build. */
 static bool device_supported(int m)
 {
-    return m == HHMM_MODEL_HMM_GAUSS || m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ||
-           m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE;
+    return m >= HHMM_MODEL_HMM_GAUSS && m <= HHMM_MODEL_TAYAL_LITE;
 }
 
 static int64_t npairs(const hhmm_request *r)

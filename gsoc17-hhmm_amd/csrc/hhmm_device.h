@@ -1,0 +1,255 @@
+/*
+ * hhmm_device.h -- device helpers shared by the gfx950 kernels
+ * (hhmm_kernels.hip: HMM / semisup / Tayal; hhmm_iohmm.hip: IOHMM).
+ * Not part of the public ABI.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "hhmm_internal.h"
+
+#ifndef HHMM_MATH_FN
+#define HHMM_MATH_FN static __device__ __forceinline__
+#define HHMM_MATH_TABLE static __constant__
+#endif
+#include "hhmm_crmath.h"
+
+namespace hhmm {
+
+constexpr double kLn2 = 0x1.62e42fefa39efp-1;
+
+/* ------------------------------------------------------------------ */
+/* Small device helpers                                                  */
+/* ------------------------------------------------------------------ */
+
+__device__ __forceinline__ double dev_nan() { return __builtin_nan(""); }
+__device__ __forceinline__ double dev_ninf() { return -__builtin_inf(); }
+
+/* max(std::vector<double>) of Stan Math on x86-64 (Eigen SSE2 maxCoeff):
+ * identical to stan_max_vec in oracle/hhmm_oracle.c.  NaN-aware order. */
+__device__ __forceinline__ double sse_max(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double std_max(double a, double b) { return a < b ? b : a; }
+template <int K>
+__device__ __forceinline__ double stan_max_vec(const double (&d)[K])
+{
+    if constexpr (K < 2) {
+        return d[0];
+    } else {
+        constexpr int aligned = K & ~1, aligned2 = K & ~3;
+        double r0a = d[0], r0b = d[1];
+        if constexpr (aligned > 2) {
+            double r1a = d[2], r1b = d[3];
+#pragma unroll
+            for (int i = 4; i < aligned2; i += 4) {
+                r0a = sse_max(r0a, d[i]);
+                r0b = sse_max(r0b, d[i + 1]);
+                r1a = sse_max(r1a, d[i + 2]);
+                r1b = sse_max(r1b, d[i + 3]);
+            }
+            r0a = sse_max(r0a, r1a);
+            r0b = sse_max(r0b, r1b);
+            if constexpr (aligned > aligned2) {
+                r0a = sse_max(r0a, d[aligned2]);
+                r0b = sse_max(r0b, d[aligned2 + 1]);
+            }
+        }
+        double res = sse_max(r0a, r0b);
+#pragma unroll
+        for (int i = aligned; i < K; ++i)
+            res = std_max(res, d[i]);
+        return res;
+    }
+}
+
+/* Element of a row addressed as (uniform row pointer) + (32-bit lane byte
+ * offset): lets hipcc emit SGPR-base + VGPR-offset global memory ops. */
+template <typename T>
+__device__ __forceinline__ T &at(T *row, uint32_t byte_off)
+{
+    return *reinterpret_cast<T *>(reinterpret_cast<char *>(row) + byte_off);
+}
+template <typename T>
+__device__ __forceinline__ const T &at(const T *row, uint32_t byte_off)
+{
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(row) + byte_off);
+}
+
+/* Power-of-two renormalisation of a K-vector after every step: the largest
+ * entry is brought into [0.5, 1) by an exact ldexp and the removed exponent
+ * is accumulated in `ex`.  Keeping the max near 1 (rather than letting it
+ * drift) keeps every component down to 1e-300 of the max a NORMAL double, so
+ * posteriors down to the 1e-250 tolerance floor keep full precision.
+ * mx == 0 / inf / NaN: frexp_exp returns 0 and v is unchanged. */
+template <int K>
+__device__ __forceinline__ void renorm(double (&v)[K], int &ex)
+{
+    double mx = v[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k)
+        mx = fmax(mx, v[k]);
+    const int e = __builtin_amdgcn_frexp_exp(mx);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        v[k] = ldexp(v[k], -e);
+    ex += e;
+}
+
+/* Wave-wide min / max, returned through readfirstlane so that hipcc knows
+ * the result is uniform: every time index derived from it (row pointers of
+ * the per-step loads and stores) is then computed on the scalar unit. */
+__device__ __forceinline__ int wave_min(int v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v = min(v, __shfl_xor(v, off));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v = max(v, __shfl_xor(v, off));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ void pair_coords(const DevArgs &a, int64_t p, int64_t &n, int64_t &d)
+{
+    if (a.pairing == HHMM_PAIR_ZIP) {
+        n = p;
+        d = p;
+    } else {
+        n = p / a.S;
+        d = p - n * a.S;
+    }
+}
+
+__device__ __forceinline__ int pair_len(const DevArgs &a, int64_t n)
+{
+    int Tp = a.T ? a.T[n] : a.Tmax;
+    return min(max(Tp, 1), a.Tmax);
+}
+
+/* out[p, t, k] for k = 0..K-1: uniform row pointer out + P*(t + Tout*k)
+ * (SGPR base) plus the lane's 32-bit pair index (P < 2^29 per launch). */
+template <int K>
+__device__ __forceinline__ void store_tk(double *out, const DevArgs &a, int64_t p, int t, const double (&v)[K])
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        at(out + a.P * ((int64_t)t + (int64_t)a.Tout * k), (uint32_t)p * 8u) = v[k];
+}
+
+/* 1/x to ~1 ulp: v_rcp_f64 + two Newton steps (tolerance 1e-9 outputs only);
+ * IEEE division for x below 2^-1000 where the reciprocal would overflow. */
+__device__ __forceinline__ double fast_rcp(double x)
+{
+    if (__builtin_expect(!(x > 0x1p-1000), 0))
+        return 1.0 / x;
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return r;
+}
+
+template <int K>
+__device__ __forceinline__ double vsum(const double (&v)[K])
+{
+    double s = v[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k)
+        s += v[k];
+    return s;
+}
+
+/* Viterbi chunk length: a multiple of the back-pointer steps per word so
+ * that every word boundary falls on a static unrolled slot. */
+constexpr int vit_chunk(int K)
+{
+    return bp_steps_per_word(K) >= 8 ? bp_steps_per_word(K)
+                                      : (8 % bp_steps_per_word(K) == 0 ? 8 : 2 * bp_steps_per_word(K));
+}
+
+/* Backtrack over chunk c (descending): writes zstar[t] and steps z. */
+template <int K, int CV, bool FULLC>
+__device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int64_t p, int Tp, int c,
+                                               const uint32_t (&w)[CV / bp_steps_per_word(K)], int &z)
+{
+    constexpr int BITS = bp_bits(K);
+    constexpr int SPW = bp_steps_per_word(K);
+    constexpr int STEPB = K * BITS;
+    constexpr uint32_t MASK = (1u << BITS) - 1u;
+    const int t0 = c * CV;
+#pragma unroll
+    for (int u = CV - 1; u >= 0; --u) {
+        const int t = t0 + u;
+        if (FULLC || t < Tp) {
+            at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = z + 1;
+            if (t > 0)
+                z = (int)((w[u / SPW] >> ((u % SPW) * STEPB + z * BITS)) & MASK);
+        }
+    }
+}
+
+/* Viterbi epilogue shared by every Viterbi pass: flushes the partial last
+ * back-pointer word, logp_zstar = max(delta_T) with Eigen's SSE2 maxCoeff NaN
+ * rule, zstar_T = the LAST j attaining it (e.g. hmm/stan/hmm.stan:120-124),
+ * pair_status, then the backtrack chunk by chunk with the words prefetched one
+ * chunk ahead (hmm.stan:126-128). */
+template <int K>
+__device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, int Tp, int Tw_min, int Tw_max,
+                                                 const double (&dl)[K], uint32_t word)
+{
+    constexpr int SPW = bp_steps_per_word(K);
+    constexpr int CV = vit_chunk(K);
+    constexpr int WPC = CV / SPW; /* words per chunk */
+    const int nfull = Tw_min / CV;
+    const int nchunk = (Tw_max + CV - 1) / CV;
+    if ((Tp - 1) % SPW != SPW - 1) /* partial last word */
+        a.bp[p + a.P * (int64_t)((Tp - 1) / SPW)] = word;
+
+    /* logp_zstar = max(delta_tk[T]); zstar[T] = LAST j attaining it (hmm.stan:120-124). */
+    const double lp = stan_max_vec<K>(dl);
+    int z = -1;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (dl[j] == lp)
+            z = j;
+    /* Backtracking reads an unset back-pointer exactly when zstar[T] is unset
+     * (NaN row at T = 1) or every delta_T is -inf. */
+    const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
+    if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
+        a.logp_zstar[p] = lp;
+    if (a.pair_status)
+        a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+    if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
+        return;
+    if (invalid) {
+        for (int t = 0; t < Tp; ++t)
+            a.zstar[p + a.P * (int64_t)t] = 0;
+        return;
+    }
+    /* backtrack, chunk by chunk, words prefetched one chunk ahead; word rows
+     * are wave-uniform, clamped to the allocation (a short lane's extra rows
+     * are never consumed) */
+    const int wmax = a.Tmax / SPW;
+    uint32_t w[WPC], wn[WPC];
+    const int clast = nchunk - 1;
+#pragma unroll
+    for (int i = 0; i < WPC; ++i)
+        w[i] = at(a.bp + a.P * (int64_t)min(clast * WPC + i, wmax), (uint32_t)p * 4u);
+    for (int c = clast; c >= 0; --c) {
+#pragma unroll
+        for (int i = 0; i < WPC; ++i)
+            wn[i] = at(a.bp + a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax), (uint32_t)p * 4u);
+        if (c < nfull)
+            vit_back_chunk<K, CV, true>(a, p, Tp, c, w, z);
+        else
+            vit_back_chunk<K, CV, false>(a, p, Tp, c, w, z);
+#pragma unroll
+        for (int i = 0; i < WPC; ++i)
+            w[i] = wn[i];
+    }
+}
+
+} // namespace hhmm

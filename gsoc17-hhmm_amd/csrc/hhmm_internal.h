@@ -40,10 +40,16 @@ struct DevArgs {
     int32_t *zstar;
     double *logp_zstar;
     int32_t *pair_status;
+    double *oblik;      /* [P, Tout, K] oblik_tk */
+    double *oblik_t;    /* [P, Tout]    oblik_t */
+    double *logA;       /* [P, Tout, K] A_ij (reg / mix) or logA_ij (hmix / lite) */
+    int32_t *z_ffbs;    /* [P, Tout]    FFBS draw */
+    const double *ffbs_u; /* [P, Tmax]  caller uniforms */
     /* workspace */
     double *ckpt;       /* [nchunk][K][P] forward checkpoints */
     double *ckpt_ls;    /* [nchunk][P]    log scale at each checkpoint */
     uint32_t *bp;       /* [nword][P]     packed Viterbi back-pointers */
+    double *lam;        /* [Tmax][P]      IOHMM: running sum of log c_t (unbeta pass) */
 };
 
 /* Time steps between forward checkpoints kept for the backward sweep. */
@@ -66,6 +72,10 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos);
 /* Launches every kernel the request needs on `stream` (device pointers). */
 hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws,
                        hipStream_t stream);
+
+/* IOHMM family (iohmm-reg / -mix / -hmix / -hmix-lite), hhmm_iohmm.hip. */
+hhmm_status launch_iohmm(const DevArgs &a, hipStream_t stream);
+bool iohmm_supported(int K, int M, int L, char *why, size_t why_len);
 
 /* Device self-test of the correctly rounded log (host arrays). */
 hhmm_status selftest_cr_log(const double *in, double *out, int64_t n);

@@ -1,0 +1,551 @@
+/*
+ * hhmm_iohmm.hip -- gfx950 kernel for the input-output HMM family:
+ *   iohmm-reg/stan/iohmm-reg.stan        (regression emission)
+ *   iohmm-mix/stan/iohmm-mix.stan        (Gaussian-mixture emission)
+ *   iohmm-mix/stan/iohmm-hmix.stan       (+ oblik_t, fixed Viterbi init)
+ *   iohmm-mix/stan/iohmm-hmix-lite.stan  (forward + oblik_t only)
+ * SURVEY.md §8 rows A3 (regression emission), A4 (mixture emission), A5
+ * (softmax input-driven transitions), A6-A9 (forward / backward / gamma),
+ * A10 (oblik_t), A11 (Viterbi), A14 (FFBS).
+ *
+ * Structure of the reference's IOHMM recursions: the
+ * "transition" is a K-vector A_t = softmax(u_t' w_j) that depends only on the
+ * step, indexed by the PREVIOUS state i in the forward pass and Viterbi
+ * (iohmm-reg.stan:70,163) and by the NEXT state i in the backward pass
+ * (:94).  Two consequences this kernel is built on:
+ *   * forward: unalpha_t(j) = LSE_i(unalpha_{t-1}(i) + log A_t(i)) + oblik_t(j),
+ *     i.e. in linear space f_t = e_t * s_t with ONE scalar s_t = sum_i f_{t-1}(i) A_t(i);
+ *   * backward: the accumulator (:94) does not depend on j, so every unbeta_t
+ *     row is one repeated scalar B_t, beta_t = softmax(unbeta_t) = 1/K exactly,
+ *     and B_{t-1} = B_t + log c_t with c_t = sum_i A_t(i) exp(oblik_t(i)).
+ * So forward, loglik, alpha, beta, gamma, oblik_t and Viterbi all come out of
+ * ONE sweep over t that computes each step's transcendentals once; only the
+ * unbeta output needs a second (cheap) sweep, for B_t = 1 + (Lambda_T - Lambda_t).
+ *
+ * One LANE = one (series, draw) pair.  Layout as hhmm_kernels.hip: every
+ * per-step load/store is a coalesced wave transaction (pair-fastest), and in
+ * GRID pairing the 64 lanes of a wave share one series, so x_t / u_t are
+ * broadcast loads.  w_km (and b_km) live in registers; the mixture tables
+ * (log lambda, mu, 1/s, NEG_LOG_SQRT_TWO_PI - log s) in a per-lane LDS slab.
+ *
+ * Exactness: Viterbi paths are bit-exact with the oracle, so whenever zstar /
+ * logp_zstar / FFBS draws are requested (EXACT), every transcendental the
+ * Viterbi or FFBS consumes -- the softmax exps, log A, the mixture LSE, the
+ * log(sigma) of normal_lpdf -- is the shared correctly rounded hhmm_cr_exp /
+ * hhmm_cr_log, in the reference's operation order (Eigen SSE2 dot order,
+ * sequential softmax sum, Stan's log_sum_exp).  Otherwise the device libm
+ * (within the 1e-9 tolerance of the float outputs) is used.
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+
+#include "hhmm_device.h"
+
+namespace hhmm {
+
+constexpr int kIoLmax = 8; /* mixture components per state on the device path */
+
+enum IoFam { IO_REG = 0, IO_MIX = 1 };
+
+template <bool EXACT>
+__device__ __forceinline__ double io_exp(double x)
+{
+    if constexpr (EXACT)
+        return hhmm_cr_exp(x);
+    else
+        return exp(x);
+}
+template <bool EXACT>
+__device__ __forceinline__ double io_log(double x)
+{
+    if constexpr (EXACT)
+        return hhmm_cr_log(x);
+    else
+        return log(x);
+}
+
+/* row_vector * vector as Eigen evaluates it on x86-64 SSE2 (oracle stan_dot):
+ * two 2-wide partial sums over blocks of 4, one more packet, horizontal add,
+ * scalar tail.  n <= MMAX is wave-uniform (scalar branches). */
+template <int MMAX>
+__device__ __forceinline__ double sse_dot(const double (&a)[MMAX], const double (&b)[MMAX], int n)
+{
+    static_assert(MMAX >= 4 && MMAX % 4 == 0, "MMAX is 4 or 8");
+    if (n < 2)
+        return n == 1 ? a[0] * b[0] : 0.0;
+    const int aligned = n & ~1, aligned2 = n & ~3;
+    double r0a = a[0] * b[0], r0b = a[1] * b[1];
+    if (aligned > 2) {
+        double r1a = a[2] * b[2], r1b = a[3] * b[3];
+#pragma unroll
+        for (int i = 4; i + 4 <= MMAX; i += 4) {
+            if (i < aligned2) {
+                r0a = r0a + a[i] * b[i];
+                r0b = r0b + a[i + 1] * b[i + 1];
+                r1a = r1a + a[i + 2] * b[i + 2];
+                r1b = r1b + a[i + 3] * b[i + 3];
+            }
+        }
+        r0a = r0a + r1a;
+        r0b = r0b + r1b;
+        if (aligned > aligned2) {
+#pragma unroll
+            for (int q = 4; q + 2 <= MMAX; q += 4) {
+                if (q == aligned2) {
+                    r0a = r0a + a[q] * b[q];
+                    r0b = r0b + a[q + 1] * b[q + 1];
+                }
+            }
+        }
+    }
+    double res = r0a + r0b;
+#pragma unroll
+    for (int i = 2; i < MMAX; ++i)
+        if (i >= aligned && i < n)
+            res = res + a[i] * b[i];
+    return res;
+}
+
+/* Stan Math softmax(v): theta = exp(v - max v); theta / sequential sum. */
+template <int K, bool EXACT>
+__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K])
+{
+    double mx = v[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i)
+        if (v[i] > mx)
+            mx = v[i];
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        th[i] = io_exp<EXACT>(v[i] - mx);
+        sum += th[i];
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        th[i] = th[i] / sum;
+}
+
+/* Per-lane mixture table entry (j, l): (mu, 1/s) and (log lambda, C - log s). */
+__device__ __forceinline__ const double2 *mix_row(const double2 *slab, int L, int j, int l, int f)
+{
+    return slab + ((j * L + l) * 2 + f) * 64;
+}
+
+/* Per-lane parameters. */
+template <int FAM, int K, int MMAX>
+struct IoParams {
+    double p[K];
+    double w[K][MMAX];
+    double b[FAM == IO_REG ? K : 1][MMAX];
+    double isig[FAM == IO_REG ? K : 1];
+    double c0[FAM == IO_REG ? K : 1];
+};
+
+/* One step's per-state quantities. */
+template <int K>
+struct IoStep {
+    double o[K];  /* oblik_tk[t] */
+    double A[K];  /* A_ij[t] (t = 0: p_1k filler) */
+    double lA[K]; /* log A_ij[t] (t = 0: log p_1k) */
+};
+
+/* Emission oblik_t(j).
+ * reg: normal_lpdf(x_t | u_t' b_j, s_j)          (iohmm-reg.stan:51-57)
+ * mix: LSE_l(log lambda_jl + normal_lpdf(x_t | mu_jl, s_jl))
+ *                                                 (iohmm-mix.stan:53-65; hmix :50-62; lite :46-58)
+ * normal_lpdf = ((NEG_LOG_SQRT_TWO_PI - log s) + (-0.5 * z^2)), z = (x - mu) * (1/s);
+ * log_sum_exp(std::vector): max by '>', sum of exp(x - max) over x != -inf
+ * in order, max + log(sum). */
+template <int FAM, int K, int MMAX, bool EXACT>
+__device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, const double2 *slab, int L, int M,
+                                            double x, const double (&u)[MMAX], double (&o)[K])
+{
+    if constexpr (FAM == IO_REG) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const double mu = sse_dot<MMAX>(u, pp.b[j], M);
+            const double z = (x - mu) * pp.isig[j];
+            const double z2 = z * z;
+            o[j] = pp.c0[j] + (-0.5 * z2);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            double acc[kIoLmax];
+            double mx = dev_ninf();
+#pragma unroll
+            for (int l = 0; l < kIoLmax; ++l) {
+                if (l < L) {
+                    const double2 ms = *mix_row(slab, L, j, l, 0);
+                    const double2 lc = *mix_row(slab, L, j, l, 1);
+                    const double z = (x - ms.x) * ms.y;
+                    const double z2 = z * z;
+                    acc[l] = lc.x + (lc.y + (-0.5 * z2));
+                    if (acc[l] > mx)
+                        mx = acc[l];
+                }
+            }
+            double sum = 0.0;
+#pragma unroll
+            for (int l = 0; l < kIoLmax; ++l)
+                if (l < L && acc[l] != dev_ninf())
+                    sum += io_exp<EXACT>(acc[l] - mx);
+            o[j] = mx + io_log<EXACT>(sum);
+        }
+    }
+}
+
+/* Transition vector of step t >= 1: A_t = softmax(u_t' w_j), log A_t
+ * (iohmm-reg.stan:40-49; iohmm-mix.stan:42-51, :69; iohmm-hmix.stan:36-48). */
+template <int FAM, int K, int MMAX, bool EXACT>
+__device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, int M, const double (&u)[MMAX],
+                                              IoStep<K> &st)
+{
+    double v[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        v[j] = sse_dot<MMAX>(u, pp.w[j], M);
+    stan_softmax<K, EXACT>(v, st.A);
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        st.lA[j] = io_log<EXACT>(st.A[j]);
+}
+
+/* Loads x_t and u_t[0..M) of one series (clamped, unconditional). */
+template <int MMAX>
+__device__ __forceinline__ void io_load(const DevArgs &a, uint32_t n, int t, double &x, double (&u)[MMAX])
+{
+    const int tc = min(max(t, 0), a.Tmax - 1);
+    x = at(a.xr + a.N * (int64_t)tc, n * 8u);
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) {
+        u[m] = 0.0;
+        if (m < a.M)
+            u[m] = at(a.u + a.N * ((int64_t)tc + (int64_t)a.Tmax * m), n * 8u);
+    }
+}
+
+template <int FAM, int K, int MMAX, bool EXACT>
+__global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
+{
+    HIP_DYNAMIC_SHARED(double2, lds)
+    constexpr int BITS = bp_bits(K);
+    constexpr int SPW = bp_steps_per_word(K);
+    constexpr int STEPB = K * BITS;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int M = a.M, L = a.L;
+    const uint32_t out = a.outputs;
+    const bool want_vit = EXACT && (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR));
+    const bool fixed_init = (a.model == HHMM_MODEL_IOHMM_HMIX); /* iohmm-hmix.stan:166-167 */
+    const bool log_A_out = (a.model == HHMM_MODEL_IOHMM_HMIX || a.model == HHMM_MODEL_IOHMM_HMIX_LITE);
+
+    /* ---- per-pair parameters ---- */
+    IoParams<FAM, K, MMAX> pp;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        pp.p[k] = a.p_1k[d + a.S * k];
+#pragma unroll
+        for (int m = 0; m < MMAX; ++m) {
+            pp.w[k][m] = (m < M) ? a.w_km[d + a.S * ((int64_t)k + (int64_t)K * m)] : 0.0;
+            if constexpr (FAM == IO_REG)
+                pp.b[k][m] = (m < M) ? a.b_km[d + a.S * ((int64_t)k + (int64_t)K * m)] : 0.0;
+        }
+        if constexpr (FAM == IO_REG) {
+            const double s = a.s_k[d + a.S * k];
+            pp.isig[k] = 1.0 / s;
+            pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - io_log<EXACT>(s);
+        }
+    }
+    double2 *slab = lds + (size_t)wave * K * L * 2 * 64 + lane;
+    if constexpr (FAM == IO_MIX) {
+        /* loglambda_kl = log(lambda_kl) (iohmm-mix.stan:55) */
+        for (int j = 0; j < K; ++j)
+            for (int l = 0; l < L; ++l) {
+                const int64_t ix = d + a.S * ((int64_t)j + (int64_t)K * l);
+                const double s = a.s_kl[ix];
+                *const_cast<double2 *>(mix_row(slab, L, j, l, 0)) = make_double2(a.mu_kl[ix], 1.0 / s);
+                *const_cast<double2 *>(mix_row(slab, L, j, l, 1)) =
+                    make_double2(io_log<EXACT>(a.lambda_kl[ix]), HHMM_NEG_LOG_SQRT_TWO_PI - io_log<EXACT>(s));
+            }
+    }
+    const int Tw_min = wave_min(Tp);
+    const int Tw_max = wave_max(Tp);
+
+    /* ---- the sweep ---- */
+    double f[K];         /* scaled linear-space forward state */
+    double lsc = 0.0;    /* log scale, excluding the binary exponent ex */
+    int ex = 0;
+    double lam = 0.0;    /* Lambda_t = sum_{2 <= tau <= t} log c_tau (unbeta pass) */
+    double dl[K];        /* Viterbi delta */
+    uint32_t word = 0;
+    double x, xn;
+    double u[MMAX], un[MMAX];
+    io_load<MMAX>(a, (uint32_t)n, 0, x, u);
+    for (int t = 0; t < Tw_max; ++t) {
+        io_load<MMAX>(a, (uint32_t)n, t + 1, xn, un); /* one step ahead */
+        if (t < Tp) {
+            IoStep<K> st;
+            io_emission<FAM, K, MMAX, EXACT>(pp, slab, L, M, x, u, st.o);
+            if (t == 0) {
+                /* A_ij[1] = p_1k (filler, iohmm-reg.stan:41-42); logA_ij[1] = log(p_1k) (iohmm-hmix.stan:40) */
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    st.A[k] = pp.p[k];
+                    st.lA[k] = log_A_out ? io_log<EXACT>(pp.p[k]) : 0.0;
+                }
+            } else {
+                io_transition<FAM, K, MMAX, EXACT>(pp, M, u, st);
+            }
+            if ((out & HHMM_OUT_OBLIK_TK) && a.oblik)
+                store_tk<K>(a.oblik, a, p, t, st.o);
+            if ((out & HHMM_OUT_LOGA) && a.logA)
+                store_tk<K>(a.logA, a, p, t, log_A_out ? st.lA : st.A);
+
+            /* forward (iohmm-reg.stan:59-78): f_t = e_t * sum_i f_{t-1}(i) A_t(i) */
+            double m = st.o[0];
+#pragma unroll
+            for (int k = 1; k < K; ++k)
+                m = fmax(m, st.o[k]);
+            if (m == dev_ninf())
+                m = 0.0; /* every emission impossible: f_t = 0, alpha = NaN as in Stan */
+            double e[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                e[k] = exp(st.o[k] - m);
+            /* unalpha in log space, so that a state whose emission underflows
+             * exp(o - m) keeps Stan's finite value:
+             *   t = 0: log(p_1k[j]) + oblik_1(j)                    (iohmm-reg.stan:62-63)
+             *   t > 0: oblik_t(j) + log(s_t) + log-scale of f_{t-1}   (:65-74) */
+            double ua_base;
+            if (t == 0) {
+                ua_base = 0.0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    f[k] = pp.p[k] * e[k];
+            } else {
+                double s = f[0] * st.A[0];
+#pragma unroll
+                for (int i = 1; i < K; ++i)
+                    s = fma(f[i], st.A[i], s);
+                ua_base = log(s) + (lsc + kLn2 * ex);
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    f[k] = e[k] * s;
+                /* log c_t = m + log sum_i A_t(i) e_t(i) (backward accumulator, :94) */
+                if (out & HHMM_OUT_UNBETA) {
+                    double c = st.A[0] * e[0];
+#pragma unroll
+                    for (int i = 1; i < K; ++i)
+                        c = fma(st.A[i], e[i], c);
+                    lam += m + log(c);
+                    at(a.lam + a.P * (int64_t)t, (uint32_t)p * 8u) = lam;
+                }
+            }
+            lsc += m;
+            renorm<K>(f, ex);
+
+            /* posteriors of step t */
+            const double fs = vsum<K>(f);
+            const double rfs = 1.0 / fs;
+            if ((out & HHMM_OUT_ALPHA) && a.alpha) {
+                double v[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    v[k] = f[k] * rfs;
+                store_tk<K>(a.alpha, a, p, t, v);
+            }
+            if ((out & HHMM_OUT_UNALPHA) && a.unalpha) {
+                double v[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    v[k] = (t == 0) ? log(pp.p[k]) + st.o[k] : st.o[k] + ua_base;
+                store_tk<K>(a.unalpha, a, p, t, v);
+            }
+            if ((out & HHMM_OUT_BETA) && a.beta) { /* softmax of a repeated scalar */
+                double v[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    v[k] = 1.0 / K;
+                store_tk<K>(a.beta, a, p, t, v);
+            }
+            if ((out & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) && (a.gamma || a.ungamma)) {
+                /* ungamma = alpha .* (1/K); gamma = normalize(ungamma) = alpha */
+                double v[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    v[k] = f[k] * rfs;
+                if ((out & HHMM_OUT_GAMMA) && a.gamma)
+                    store_tk<K>(a.gamma, a, p, t, v);
+                if ((out & HHMM_OUT_UNGAMMA) && a.ungamma) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        v[k] = v[k] * (1.0 / K);
+                    store_tk<K>(a.ungamma, a, p, t, v);
+                }
+            }
+            if ((out & HHMM_OUT_OBLIK_T) && a.oblik_t) {
+                /* oblik_t = LSE(log(alpha_t) + oblik_t) = m + log(sum_j f_j e_j / sum_j f_j)
+                 * (iohmm-hmix.stan:118-121; lite :78-81) */
+                double num = f[0] * e[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k)
+                    num = fma(f[k], e[k], num);
+                at(a.oblik_t + a.P * (int64_t)t, (uint32_t)p * 8u) = m + log(num * rfs);
+            }
+
+            /* Viterbi (iohmm-reg.stan:150-181; iohmm-mix.stan:164-195; iohmm-hmix.stan:160-193) */
+            if (want_vit) {
+                if (t == 0) {
+                    if (fixed_init) {
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            dl[k] = st.o[k];
+                    } else { /* delta_tk[1, K] = oblik_tk[1][j] for j = 1..K (Q3) */
+#pragma unroll
+                        for (int k = 0; k < K - 1; ++k)
+                            dl[k] = dev_nan();
+                        dl[K - 1] = st.o[K - 1];
+                    }
+                } else {
+                    /* logp = (delta_{t-1}(i) + log A_t(i)) + oblik_t(j); strict '>' from -inf */
+                    double ai[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+                        ai[i] = dl[i] + st.lA[i];
+                    const int slot = t % SPW;
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        double best = dev_ninf();
+                        uint32_t arg = 0;
+#pragma unroll
+                        for (int i = 0; i < K; ++i) {
+                            const double cand = ai[i] + st.o[j];
+                            if (cand > best) {
+                                best = cand;
+                                arg = (uint32_t)i;
+                            }
+                        }
+                        dl[j] = best;
+                        word |= arg << (slot * STEPB + j * BITS);
+                    }
+                    if (slot == SPW - 1) {
+                        a.bp[p + a.P * (int64_t)(t / SPW)] = word;
+                        word = 0;
+                    }
+                }
+            }
+        }
+        x = xn;
+#pragma unroll
+        for (int m2 = 0; m2 < MMAX; ++m2)
+            u[m2] = un[m2];
+    }
+    if ((out & HHMM_OUT_LOGLIK) && a.loglik) /* target += log_sum_exp(unalpha_tk[T]) (iohmm-reg.stan:120) */
+        a.loglik[p] = log(vsum<K>(f)) + (lsc + kLn2 * ex);
+
+    /* unbeta_tk: B_T = 1 (Q1); B_t = 1 + (Lambda_T - Lambda_t) (iohmm-reg.stan:80-98) */
+    if ((out & HHMM_OUT_UNBETA) && a.unbeta) {
+        const double lamT = lam;
+        for (int t = 0; t < Tp; ++t) {
+            const double lt = (t == 0) ? 0.0 : a.lam[p + a.P * (int64_t)t];
+            double v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                v[k] = 1.0 + (lamT - lt);
+            store_tk<K>(a.unbeta, a, p, t, v);
+        }
+    }
+    if (want_vit)
+        viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dl, word);
+}
+
+/* ------------------------------------------------------------------ */
+/* Host-side launch                                                      */
+/* ------------------------------------------------------------------ */
+
+bool iohmm_supported(int K, int M, int L, char *why, size_t why_len)
+{
+    if (K < 1 || K > kMaxK) {
+        snprintf(why, why_len, "IOHMM device path supports K = 1..%d (got %d)", kMaxK, K);
+        return false;
+    }
+    if (M < 1 || M > 8) {
+        snprintf(why, why_len, "IOHMM device path supports M = 1..8 (got %d)", M);
+        return false;
+    }
+    if (L > kIoLmax) {
+        snprintf(why, why_len, "IOHMM mixture device path supports L <= %d (got %d)", kIoLmax, L);
+        return false;
+    }
+    return true;
+}
+
+template <int FAM, int K, int MMAX, bool EXACT>
+static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
+{
+    const size_t per_wave = (FAM == IO_MIX) ? (size_t)K * a.L * 2 * 64 * sizeof(double2) : 0;
+    int waves = 4;
+    while (per_wave > 0 && waves > 1 && per_wave * waves > kLdsLimit)
+        --waves;
+    if (per_wave * waves > kLdsLimit) {
+        set_error("IOHMM mixture table K*L = %d*%d does not fit in LDS", K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const int threads = 64 * waves;
+    const dim3 grid((unsigned)((a.P + threads - 1) / threads));
+    hipLaunchKernelGGL((iohmm_kernel<FAM, K, MMAX, EXACT>), grid, dim3(threads), per_wave * waves, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("iohmm_kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+template <int FAM, int K>
+static hhmm_status launch_io3(const DevArgs &a, hipStream_t st)
+{
+    const bool exact = (a.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR | HHMM_OUT_FFBS)) != 0;
+    if (a.M <= 4)
+        return exact ? launch_io4<FAM, K, 4, true>(a, st) : launch_io4<FAM, K, 4, false>(a, st);
+    return exact ? launch_io4<FAM, K, 8, true>(a, st) : launch_io4<FAM, K, 8, false>(a, st);
+}
+
+template <int FAM>
+static hhmm_status launch_io2(const DevArgs &a, hipStream_t st)
+{
+    switch (a.K) {
+    case 1: return launch_io3<FAM, 1>(a, st);
+    case 2: return launch_io3<FAM, 2>(a, st);
+    case 3: return launch_io3<FAM, 3>(a, st);
+    case 4: return launch_io3<FAM, 4>(a, st);
+    case 5: return launch_io3<FAM, 5>(a, st);
+    case 6: return launch_io3<FAM, 6>(a, st);
+    case 7: return launch_io3<FAM, 7>(a, st);
+    case 8: return launch_io3<FAM, 8>(a, st);
+    default:
+        set_error("K = %d not supported (1..%d)", a.K, kMaxK);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+}
+
+hhmm_status launch_iohmm(const DevArgs &a, hipStream_t st)
+{
+    char why[160];
+    if (!iohmm_supported(a.K, a.M, a.model == HHMM_MODEL_IOHMM_REG ? 1 : a.L, why, sizeof(why))) {
+        set_error("%s", why);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    if (a.model == HHMM_MODEL_IOHMM_REG)
+        return launch_io2<IO_REG>(a, st);
+    return launch_io2<IO_MIX>(a, st);
+}
+
+} // namespace hhmm

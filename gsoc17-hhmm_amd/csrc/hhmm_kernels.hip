@@ -16,8 +16,8 @@
  * Kernels:
  *   fb_kernel      A2/A1 emissions, A6 forward + loglik, A7 alpha, A8 backward,
  *                  A9 gamma, A12/A13 masks.  LINEAR-space scaled recursion
- *                  (K^2 FMAs per step, a power-of-two renormalisation only when
- *                  the exponent drifts; no exp/log in the discrete loop);
+ *                  (K^2 FMAs per step, an exact power-of-two renormalisation
+ *                  per step; no exp/log in the discrete loop);
  *                  forward checkpoints every C steps, recomputed chunk by chunk
  *                  in the backward sweep.  Tolerance 1e-9 rel.
  * Latency rules used throughout (the kernels are latency-, not issue-bound at
@@ -38,110 +38,10 @@
 #include <stdio.h>
 #include <string.h>
 
-#include "hhmm_internal.h"
-
-#define HHMM_MATH_FN static __device__ __forceinline__
-#define HHMM_MATH_TABLE static __constant__
-#include "hhmm_crmath.h"
+#include "hhmm_device.h"
 
 namespace hhmm {
 
-constexpr double kLn2 = 0x1.62e42fefa39efp-1;
-
-/* ------------------------------------------------------------------ */
-/* Small device helpers                                                  */
-/* ------------------------------------------------------------------ */
-
-__device__ __forceinline__ double dev_nan() { return __builtin_nan(""); }
-__device__ __forceinline__ double dev_ninf() { return -__builtin_inf(); }
-
-/* max(std::vector<double>) of Stan Math on x86-64 (Eigen SSE2 maxCoeff):
- * identical to stan_max_vec in oracle/hhmm_oracle.c.  NaN-aware order. */
-__device__ __forceinline__ double sse_max(double a, double b) { return a > b ? a : b; }
-__device__ __forceinline__ double std_max(double a, double b) { return a < b ? b : a; }
-template <int K>
-__device__ __forceinline__ double stan_max_vec(const double (&d)[K])
-{
-    if constexpr (K < 2) {
-        return d[0];
-    } else {
-        constexpr int aligned = K & ~1, aligned2 = K & ~3;
-        double r0a = d[0], r0b = d[1];
-        if constexpr (aligned > 2) {
-            double r1a = d[2], r1b = d[3];
-#pragma unroll
-            for (int i = 4; i < aligned2; i += 4) {
-                r0a = sse_max(r0a, d[i]);
-                r0b = sse_max(r0b, d[i + 1]);
-                r1a = sse_max(r1a, d[i + 2]);
-                r1b = sse_max(r1b, d[i + 3]);
-            }
-            r0a = sse_max(r0a, r1a);
-            r0b = sse_max(r0b, r1b);
-            if constexpr (aligned > aligned2) {
-                r0a = sse_max(r0a, d[aligned2]);
-                r0b = sse_max(r0b, d[aligned2 + 1]);
-            }
-        }
-        double res = sse_max(r0a, r0b);
-#pragma unroll
-        for (int i = aligned; i < K; ++i)
-            res = std_max(res, d[i]);
-        return res;
-    }
-}
-
-/* Element of a row addressed as (uniform row pointer) + (32-bit lane byte
- * offset): lets hipcc emit SGPR-base + VGPR-offset global memory ops. */
-template <typename T>
-__device__ __forceinline__ T &at(T *row, uint32_t byte_off)
-{
-    return *reinterpret_cast<T *>(reinterpret_cast<char *>(row) + byte_off);
-}
-template <typename T>
-__device__ __forceinline__ const T &at(const T *row, uint32_t byte_off)
-{
-    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(row) + byte_off);
-}
-
-/* Lazy power-of-two renormalisation of a K-vector: only when the largest
- * entry's exponent leaves [-255, 256] (rare; a scalar-skipped branch).  The
- * removed exponent is accumulated in `ex`; mx == 0 / NaN leave v unchanged. */
-template <int K>
-__device__ __forceinline__ void renorm(double (&v)[K], int &ex)
-{
-    double mx = v[0];
-#pragma unroll
-    for (int k = 1; k < K; ++k)
-        mx = fmax(mx, v[k]);
-    const uint32_t hi = (uint32_t)((uint64_t)__double_as_longlong(mx) >> 32);
-    const uint32_t eb = (hi >> 20) & 0x7ffu;
-    if (__builtin_expect(eb - (1023u - 255u) > 511u, 0)) {
-        const int e = __builtin_amdgcn_frexp_exp(mx);
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            v[k] = ldexp(v[k], -e);
-        ex += e;
-    }
-}
-
-/* Wave-wide min / max, returned through readfirstlane so that hipcc knows
- * the result is uniform: every time index derived from it (row pointers of
- * the per-step loads and stores) is then computed on the scalar unit. */
-__device__ __forceinline__ int wave_min(int v)
-{
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-        v = min(v, __shfl_xor(v, off));
-    return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ int wave_max(int v)
-{
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-        v = max(v, __shfl_xor(v, off));
-    return __builtin_amdgcn_readfirstlane(v);
-}
 
 /* hmm-multinom-semisup.stan:42 -- j0 is 0-based */
 __device__ __forceinline__ bool semisup_mask(int g, int j0)
@@ -458,22 +358,6 @@ __device__ __forceinline__ void fwd_init(double (&al)[K], const PairParams<MODEL
     renorm<K>(al, ex);
 }
 
-__device__ __forceinline__ void pair_coords(const DevArgs &a, int64_t p, int64_t &n, int64_t &d)
-{
-    if (a.pairing == HHMM_PAIR_ZIP) {
-        n = p;
-        d = p;
-    } else {
-        n = p / a.S;
-        d = p - n * a.S;
-    }
-}
-
-__device__ __forceinline__ int pair_len(const DevArgs &a, int64_t n)
-{
-    int Tp = a.T ? a.T[n] : a.Tmax;
-    return min(max(Tp, 1), a.Tmax);
-}
 
 template <int MODEL, bool AUX>
 __device__ __forceinline__ SeriesPtrs series_ptrs(const DevArgs &a, int64_t n)
@@ -503,37 +387,6 @@ enum FbMode {
     FB_FWD = 2    /* forward only: loglik / alpha / unalpha (tayal-lite, no backward output) */
 };
 
-/* out[p, t, k] for k = 0..K-1: uniform row pointer out + P*(t + Tout*k)
- * (SGPR base) plus the lane's 32-bit pair index (P < 2^29 per launch). */
-template <int K>
-__device__ __forceinline__ void store_tk(double *out, const DevArgs &a, int64_t p, int t, const double (&v)[K])
-{
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        at(out + a.P * ((int64_t)t + (int64_t)a.Tout * k), (uint32_t)p * 8u) = v[k];
-}
-
-/* 1/x to ~1 ulp: v_rcp_f64 + two Newton steps (tolerance 1e-9 outputs only);
- * IEEE division for x below 2^-1000 where the reciprocal would overflow. */
-__device__ __forceinline__ double fast_rcp(double x)
-{
-    if (__builtin_expect(!(x > 0x1p-1000), 0))
-        return 1.0 / x;
-    double r = __builtin_amdgcn_rcp(x);
-    r = fma(fma(-x, r, 1.0), r, r);
-    r = fma(fma(-x, r, 1.0), r, r);
-    return r;
-}
-
-template <int K>
-__device__ __forceinline__ double vsum(const double (&v)[K])
-{
-    double s = v[0];
-#pragma unroll
-    for (int k = 1; k < K; ++k)
-        s += v[k];
-    return s;
-}
 
 /* Writes the forward-side outputs of step t (alpha, unalpha). */
 template <int K>
@@ -826,13 +679,6 @@ __device__ __forceinline__ void emit_log(const PairParams<MODEL, K> &pp, const d
     }
 }
 
-/* Viterbi chunk length: a multiple of the back-pointer steps per word so
- * that every word boundary falls on a static unrolled slot. */
-constexpr int vit_chunk(int K)
-{
-    return bp_steps_per_word(K) >= 8 ? bp_steps_per_word(K)
-                                      : (8 % bp_steps_per_word(K) == 0 ? 8 : 2 * bp_steps_per_word(K));
-}
 
 /* One max-plus step t >= 1: delta_t(j) = max_i cand(i, j) with the
  * reference's strict '>' from -inf (first maximising i wins, NaN never
@@ -901,27 +747,6 @@ __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const
     }
 }
 
-/* Backtrack over chunk c (descending): writes zstar[t] and steps z. */
-template <int K, int CV, bool FULLC>
-__device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int64_t p, int Tp, int c,
-                                               const uint32_t (&w)[CV / bp_steps_per_word(K)], int &z)
-{
-    constexpr int BITS = bp_bits(K);
-    constexpr int SPW = bp_steps_per_word(K);
-    constexpr int STEPB = K * BITS;
-    constexpr uint32_t MASK = (1u << BITS) - 1u;
-    const int t0 = c * CV;
-#pragma unroll
-    for (int u = CV - 1; u >= 0; --u) {
-        const int t = t0 + u;
-        if (FULLC || t < Tp) {
-            at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = z + 1;
-            if (t > 0)
-                z = (int)((w[u / SPW] >> ((u % SPW) * STEPB + z * BITS)) & MASK);
-        }
-    }
-}
-
 template <int MODEL, int K>
 __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
 {
@@ -972,51 +797,7 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
         for (int u = 0; u < CV; ++u)
             cur[u] = nxt[u];
     }
-    if ((Tp - 1) % SPW != SPW - 1) /* partial last word */
-        a.bp[p + a.P * (int64_t)((Tp - 1) / SPW)] = word;
-
-    /* logp_zstar = max(delta_tk[T]); zstar[T] = LAST j attaining it (hmm.stan:120-124). */
-    const double lp = stan_max_vec<K>(dl);
-    int z = -1;
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        if (dl[j] == lp)
-            z = j;
-    /* Backtracking reads an unset back-pointer exactly when zstar[T] is unset
-     * (NaN row at T = 1) or every delta_T is -inf. */
-    const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
-    if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
-        a.logp_zstar[p] = lp;
-    if (a.pair_status)
-        a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
-    if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
-        return;
-    if (invalid) {
-        for (int t = 0; t < Tp; ++t)
-            a.zstar[p + a.P * (int64_t)t] = 0;
-        return;
-    }
-    /* backtrack, chunk by chunk, words prefetched one chunk ahead; word rows
-     * are wave-uniform, clamped to the allocation (a short lane's extra rows
-     * are never consumed) */
-    const int wmax = a.Tmax / SPW;
-    uint32_t w[WPC], wn[WPC];
-    const int clast = nchunk - 1;
-#pragma unroll
-    for (int i = 0; i < WPC; ++i)
-        w[i] = at(a.bp + a.P * (int64_t)min(clast * WPC + i, wmax), (uint32_t)p * 4u);
-    for (int c = clast; c >= 0; --c) {
-#pragma unroll
-        for (int i = 0; i < WPC; ++i)
-            wn[i] = at(a.bp + a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax), (uint32_t)p * 4u);
-        if (c < nfull)
-            vit_back_chunk<K, CV, true>(a, p, Tp, c, w, z);
-        else
-            vit_back_chunk<K, CV, false>(a, p, Tp, c, w, z);
-#pragma unroll
-        for (int i = 0; i < WPC; ++i)
-            w[i] = wn[i];
-    }
+    viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dl, word);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1045,6 +826,12 @@ static bool needs_backward(int model, uint32_t out)
            (out & (HHMM_OUT_UNBETA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
 }
 
+static bool is_iohmm_model(int model)
+{
+    return model == HHMM_MODEL_IOHMM_REG || model == HHMM_MODEL_IOHMM_MIX || model == HHMM_MODEL_IOHMM_HMIX ||
+           model == HHMM_MODEL_IOHMM_HMIX_LITE;
+}
+
 static int nchunk_of(int K, int T) { return (T + fb_chunk(K) - 1) / fb_chunk(K); }
 static int nword_of(int K, int T) { return T / bp_steps_per_word(K) + 1; }
 
@@ -1061,6 +848,8 @@ size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t
         const int Tv = (model == HHMM_MODEL_TAYAL_LITE) ? Toos : Tmax;
         bytes += align256((size_t)nword_of(K, Tv) * P * sizeof(uint32_t));
     }
+    if (is_iohmm_model(model) && (outputs & HHMM_OUT_UNBETA))
+        bytes += align256((size_t)Tmax * P * sizeof(double));
     return bytes + 256;
 }
 
@@ -1076,10 +865,14 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos)
         a.ckpt_ls = (double *)b;
         b += align256((size_t)nchunk_of(a.K, Tmax) * a.P * sizeof(double));
     }
+    a.lam = nullptr;
     if (a.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
         a.bp = (uint32_t *)b;
+        b += align256((size_t)nword_of(a.K, a.model == HHMM_MODEL_TAYAL_LITE ? Toos : Tmax) * a.P *
+                      sizeof(uint32_t));
     }
-    (void)Toos;
+    if (is_iohmm_model(a.model) && (a.outputs & HHMM_OUT_UNBETA))
+        a.lam = (double *)b;
 }
 
 struct LaunchShape {
@@ -1267,6 +1060,11 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
     a.zstar = res->zstar_t;
     a.logp_zstar = res->logp_zstar;
     a.pair_status = res->pair_status;
+    a.oblik = res->oblik_tk;
+    a.oblik_t = res->oblik_t;
+    a.logA = res->logA_ij;
+    a.z_ffbs = res->z_ffbs;
+    a.ffbs_u = req->ffbs_u;
     return a;
 }
 
@@ -1285,6 +1083,10 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
     case HHMM_MODEL_HMM_MULTINOM_SEMISUP: return run_model<HHMM_MODEL_HMM_MULTINOM_SEMISUP>(a, req, res, st);
     case HHMM_MODEL_TAYAL: return run_model<HHMM_MODEL_TAYAL>(a, req, res, st);
     case HHMM_MODEL_TAYAL_LITE: return run_model<HHMM_MODEL_TAYAL_LITE>(a, req, res, st);
+    case HHMM_MODEL_IOHMM_REG:
+    case HHMM_MODEL_IOHMM_MIX:
+    case HHMM_MODEL_IOHMM_HMIX:
+    case HHMM_MODEL_IOHMM_HMIX_LITE: return launch_iohmm(a, st);
     default:
         set_error("model %d has no device path in this build", req->model);
         return HHMM_ERR_UNSUPPORTED;

@@ -192,10 +192,21 @@ def _iohmm_states(g, u, w, p1):
     return z
 
 
+def _pad(a, shape, fill):
+    """The reference's K = 3..4 / M = 4 / L = 3 values, extended deterministically to larger shapes."""
+    out = np.empty(shape)
+    out[...] = fill(np.indices(shape))
+    sl = tuple(slice(0, min(n, m)) for n, m in zip(shape, a.shape))
+    out[sl] = a[sl]
+    return out
+
+
 def iohmm_reg(N=1, S=8, T=64, K=3, M=4, seed=SEED):
     g = rng(seed, 5)
-    w, b, s = W_REG[:K, :M], B_REG[:K, :M], S_REG[:K]
-    p1 = P1_REG[:K].copy()
+    w = _pad(W_REG, (K, M), lambda ix: np.where(ix[0] == ix[1] % K, 1.2, 0.1))
+    b = _pad(B_REG, (K, M), lambda ix: 2.0 * np.cos(1.0 + ix[0] * 1.7 + ix[1] * 0.9))
+    s = _pad(S_REG, (K,), lambda ix: 0.5 + 0.3 * ix[0])
+    p1 = _pad(P1_REG, (K,), lambda ix: 0.1 + 0 * ix[0])
     p1 = np.where(p1 > 0, p1, 0.1)
     p1 /= p1.sum()
     u = g.normal(0, 1, (N, T, M))
@@ -216,19 +227,22 @@ def _mix_true(K, L):
     wv = [1.2, 0.5, 0.3, 0.1, 0.5, 1.2, 0.3, 0.1, 0.5, 0.1, 1.2, 0.1]
     w = np.array([wv[i % 12] for i in range(16)]).reshape(4, 4)
     lam = np.array([[2, 0.1, 0.5], [1.2, 0.3, 1.6], [0.1, 0.5, 0.5], [0.1, 1.2, 0.1]])
-    lam = lam / lam.sum(axis=1, keepdims=True)
     mu = np.arange(1, 13, dtype=np.float64).reshape(4, 3)
     s = np.tile([0.1, 0.3, 0.5], (4, 1))
     p1 = np.array([0.25, 0.10, 0.45, 0.15])
-    p1 = p1 / p1.sum()
-    return w[:K], lam[:K, :L], mu[:K, :L], s[:K, :L], p1[:K] / p1[:K].sum()
+    lam = _pad(lam, (K, L), lambda ix: 0.3 + 0.2 * ((ix[0] + ix[1]) % 3))
+    lam = lam / lam.sum(axis=1, keepdims=True)
+    mu = _pad(mu, (K, L), lambda ix: 1.0 + 3 * ix[0] + ix[1])
+    s = _pad(s, (K, L), lambda ix: 0.1 + 0.2 * (ix[1] % 3))
+    p1 = _pad(p1, (K,), lambda ix: 0.1 + 0 * ix[0])
+    return w[:K], lam, mu, s, p1 / p1.sum()
 
 
 def iohmm_mix(N=1, S=8, T=64, K=4, L=3, M=4, seed=SEED):
     """iohmm-mix / iohmm-hmix / iohmm-hmix-lite inputs (same data and parameters)."""
     g = rng(seed, 6)
     w, lam, mu, s, p1 = _mix_true(K, L)
-    w = w[:, :M]
+    w = _pad(w, (K, M), lambda ix: np.where(ix[0] == ix[1] % K, 1.2, 0.1))
     u = g.normal(0, 1, (N, T, M))
     z = _iohmm_states(g, u, w, p1)
     comp = _categorical(g, lam, z) - 1

@@ -20,9 +20,10 @@
  * (tests/oracle_numpy.py), analytic known-answer tests, and committed
  * fixtures (tests/golden/).
  *
- * Transcendentals: `log` is hhmm_cr_log (correctly rounded; identical code
- * on the GPU) unless built with -DHHMM_ORACLE_LIBM_LOG, which uses the host
- * libm `log` exactly as Stan would; `exp` is the host libm in both builds.
+ * Transcendentals: `log` and `exp` are hhmm_cr_log / hhmm_cr_exp (correctly
+ * rounded; the identical code runs on the GPU wherever a bit-exact result
+ * depends on them) unless built with -DHHMM_ORACLE_LIBM_LOG, which uses the
+ * host libm `log` and `exp` exactly as Stan would.
  */
 #include <limits.h>
 #include <math.h>
@@ -43,10 +44,11 @@
 
 #ifdef HHMM_ORACLE_LIBM_LOG
 #define OR_LOG(x) log(x)
+#define OR_EXP(x) exp(x)
 #else
 #define OR_LOG(x) hhmm_cr_log(x)
+#define OR_EXP(x) hhmm_cr_exp(x)
 #endif
-#define OR_EXP(x) exp(x)
 
 #define NEG_INF (-INFINITY)
 #define STAN_INT_UNSET INT_MIN /* stanc 2.x fills local ints with INT_MIN */

@@ -12,7 +12,14 @@ from tolerances import compare, compare_all
 
 pytestmark = pytest.mark.gpu
 
-DEVICE_MODELS = ["hmm", "hmm-multinom", "hmm-multinom-semisup", "hhmm-tayal2009", "hhmm-tayal2009-lite"]
+DEVICE_MODELS = ["hmm", "hmm-multinom", "hmm-multinom-semisup", "hhmm-tayal2009", "hhmm-tayal2009-lite",
+                 "iohmm-reg", "iohmm-mix", "iohmm-hmix", "iohmm-hmix-lite"]
+
+# the hot-path outputs of each program (what a batch caller asks for)
+HOT_PARS = {m: ["loglik", "gamma_tk", "zstar_t", "logp_zstar"] for m in DEVICE_MODELS}
+HOT_PARS["hhmm-tayal2009-lite"] = ["loglik", "alpha_tk", "alpha_tk_oos", "zstar_t", "logp_zstar"]
+HOT_PARS["iohmm-hmix"] = ["loglik", "gamma_tk", "oblik_t", "zstar_t", "logp_zstar"]
+HOT_PARS["iohmm-hmix-lite"] = ["loglik", "unalpha_tk", "oblik_t"]
 
 
 def run_both(engine, oracle, model, data, draws, pars, pairing="grid"):
@@ -45,6 +52,11 @@ CASES = [
     ("hmm-multinom", dict(K=1, L=3)), ("hmm-multinom", dict(K=2, L=5)), ("hmm-multinom", dict(K=3, L=5)),
     ("hmm-multinom", dict(K=4, L=9)), ("hmm-multinom", dict(K=5, L=7)), ("hmm-multinom", dict(K=8, L=9)),
     ("hmm-multinom-semisup", dict(K=4, L=9)), ("hhmm-tayal2009", dict()), ("hhmm-tayal2009-lite", dict()),
+    ("iohmm-reg", dict(K=1, M=1)), ("iohmm-reg", dict(K=2, M=3)), ("iohmm-reg", dict(K=3, M=4)),
+    ("iohmm-reg", dict(K=4, M=4)), ("iohmm-reg", dict(K=6, M=7)),
+    ("iohmm-mix", dict(K=4, L=3, M=4)), ("iohmm-mix", dict(K=3, L=1, M=2)), ("iohmm-mix", dict(K=5, L=6, M=8)),
+    ("iohmm-hmix", dict(K=4, L=3, M=4)), ("iohmm-hmix", dict(K=2, L=2, M=5)),
+    ("iohmm-hmix-lite", dict(K=4, L=3, M=4)),
 ]
 
 
@@ -62,8 +74,7 @@ def test_parity_grid(engine, oracle, model, kw, T):
 def test_parity_zip_many_pairs(engine, oracle, model):
     N = 1000
     data, draws = synth.GENERATORS[model](N=N, S=N, T=64)
-    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"] if model != "hhmm-tayal2009-lite" else \
-        ["loglik", "alpha_tk", "alpha_tk_oos", "zstar_t", "logp_zstar"]
+    pars = HOT_PARS[model]
     got, ref = run_both(engine, oracle, model, data, draws, pars, pairing="zip")
     compare_all(got, ref, pars + ["pair_status"])
 
