@@ -75,7 +75,7 @@ static void *pool_get(int dev, size_t bytes)
             p.free_blocks[dev].clear();
         }
         for (void *q : drop)
-            hipFree(q);
+            (void)hipFree(q);
         (void)hipGetLastError();
         if (hipMalloc(&ptr, bytes) != hipSuccess) {
             (void)hipGetLastError();
@@ -105,9 +105,9 @@ static void pool_release_all()
     Pool &p = pool();
     std::lock_guard<std::mutex> g(p.mu);
     for (auto &dv : p.free_blocks) {
-        hipSetDevice(dv.first);
+        (void)hipSetDevice(dv.first);
         for (auto &kv : dv.second)
-            hipFree(kv.second);
+            (void)hipFree(kv.second);
     }
     p.free_blocks.clear();
 }
@@ -130,18 +130,21 @@ static uint32_t available_outputs(int m)
 {
     const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
                         HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA | HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+    /* FFBS (the engine's contract, §8 A14) is offered wherever the program has
+     * a forward filter over the full series and a backward pass */
     switch (m) {
     case HHMM_MODEL_HMM_GAUSS:
     case HHMM_MODEL_HMM_MULTINOM:
     case HHMM_MODEL_HMM_MULTINOM_SEMISUP:
     case HHMM_MODEL_TAYAL:
-        return fb;
+        return fb | HHMM_OUT_FFBS;
     case HHMM_MODEL_IOHMM_REG:
     case HHMM_MODEL_IOHMM_MIX:
-        return fb | HHMM_OUT_OBLIK_TK | HHMM_OUT_LOGA;
+        return fb | HHMM_OUT_OBLIK_TK | HHMM_OUT_LOGA | HHMM_OUT_FFBS;
     case HHMM_MODEL_IOHMM_HMIX:
         return HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_GAMMA |
-               HHMM_OUT_OBLIK_TK | HHMM_OUT_OBLIK_T | HHMM_OUT_LOGA | HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+               HHMM_OUT_OBLIK_TK | HHMM_OUT_OBLIK_T | HHMM_OUT_LOGA | HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR |
+               HHMM_OUT_FFBS;
     case HHMM_MODEL_IOHMM_HMIX_LITE:
         return HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_OBLIK_TK | HHMM_OUT_OBLIK_T | HHMM_OUT_LOGA;
     case HHMM_MODEL_TAYAL_LITE:
@@ -405,7 +408,7 @@ hhmm_status hhmm_init(int ndev)
     if (s != HHMM_OK)
         return s;
     int n = 0;
-    hipGetDeviceCount(&n);
+    (void)hipGetDeviceCount(&n);
     if (ndev > n) {
         set_error("%d devices requested, %d visible", ndev, n);
         return HHMM_ERR_NO_DEVICE;
@@ -526,7 +529,7 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
         return HHMM_ERR_OUT_OF_MEMORY;
     }
     owned.push_back(dstatus);
-    hipMemset(dstatus, 0, (size_t)P * sizeof(int32_t));
+    (void)hipMemset(dstatus, 0, (size_t)P * sizeof(int32_t));
     dres.pair_status = (int32_t *)dstatus;
 
     size_t wsb = workspace_bytes(req->model, req->data.K, req->data.T_max, req->data.T_oos_max, P, req->outputs);

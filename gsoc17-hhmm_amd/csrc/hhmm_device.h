@@ -162,6 +162,31 @@ __device__ __forceinline__ double vsum(const double (&v)[K])
     return s;
 }
 
+/* cat(w, u): Stan's categorical_rng(w / sum(w)) with the caller's uniform u
+ * (Stan Math: cumulative_sum of theta, `while (c > cum[b]) b++`), bounded to
+ * K - 1; sequential sum, IEEE divisions.  Returns the 0-based state, or -1
+ * when sum(w) is not a positive finite number.  FFBS contract, DESIGN.md §5. */
+template <int K>
+__device__ __forceinline__ int ffbs_cat(const double (&w)[K], double u)
+{
+    double sum = w[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i)
+        sum = sum + w[i];
+    if (!(sum > 0.0) || !__builtin_isfinite(sum))
+        return -1;
+    int b = 0;
+    double cum = w[0] / sum;
+#pragma unroll
+    for (int i = 1; i < K; ++i) {
+        if (b == i - 1 && u > cum) {
+            b = i;
+            cum = cum + w[i] / sum;
+        }
+    }
+    return b;
+}
+
 /* Viterbi chunk length: a multiple of the back-pointer steps per word so
  * that every word boundary falls on a static unrolled slot. */
 constexpr int vit_chunk(int K)

@@ -73,8 +73,22 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos);
 hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws,
                        hipStream_t stream);
 
+/* HMM family, one translation unit per model / K range (hhmm_m_*.hip). */
+hhmm_status run_gauss_lo(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+hhmm_status run_gauss_hi(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+hhmm_status run_multinom_lo(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+hhmm_status run_multinom_hi(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+hhmm_status run_semisup_lo(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+hhmm_status run_semisup_hi(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+hhmm_status run_tayal(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+hhmm_status run_tayal_lite(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+
 /* IOHMM family (iohmm-reg / -mix / -hmix / -hmix-lite), hhmm_iohmm.hip. */
 hhmm_status launch_iohmm(const DevArgs &a, hipStream_t stream);
+hhmm_status run_io_reg_lo(const DevArgs &a, hipStream_t st);
+hhmm_status run_io_reg_hi(const DevArgs &a, hipStream_t st);
+hhmm_status run_io_mix_lo(const DevArgs &a, hipStream_t st);
+hhmm_status run_io_mix_hi(const DevArgs &a, hipStream_t st);
 bool iohmm_supported(int K, int M, int L, char *why, size_t why_len);
 
 /* Device self-test of the correctly rounded log (host arrays). */

@@ -1,5 +1,6 @@
 /*
- * hhmm_iohmm.hip -- gfx950 kernel for the input-output HMM family:
+ * hhmm_iohmm.h -- gfx950 kernel for the input-output HMM family (templates;
+ * hhmm_io_*.hip instantiate one family / K range each):
  *   iohmm-reg/stan/iohmm-reg.stan        (regression emission)
  *   iohmm-mix/stan/iohmm-mix.stan        (Gaussian-mixture emission)
  *   iohmm-mix/stan/iohmm-hmix.stan       (+ oblik_t, fixed Viterbi init)
@@ -36,6 +37,7 @@
  * sequential softmax sum, Stan's log_sum_exp).  Otherwise the device libm
  * (within the 1e-9 tolerance of the float outputs) is used.
  */
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
@@ -243,6 +245,7 @@ __global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
     const int M = a.M, L = a.L;
     const uint32_t out = a.outputs;
     const bool want_vit = EXACT && (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR));
+    const bool want_ffbs = EXACT && (out & HHMM_OUT_FFBS) && a.z_ffbs;
     const bool fixed_init = (a.model == HHMM_MODEL_IOHMM_HMIX); /* iohmm-hmix.stan:166-167 */
     const bool log_A_out = (a.model == HHMM_MODEL_IOHMM_HMIX || a.model == HHMM_MODEL_IOHMM_HMIX_LITE);
 
@@ -285,6 +288,8 @@ __global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
     double lam = 0.0;    /* Lambda_t = sum_{2 <= tau <= t} log c_tau (unbeta pass) */
     double dl[K];        /* Viterbi delta */
     uint32_t word = 0;
+    double vprev[K];     /* FFBS: v_{t-1} (p .* e_0 at t = 0, e_t after) */
+    double uprev = 0.5;  /* FFBS: the uniform of step t - 1 */
     double x, xn;
     double u[MMAX], un[MMAX];
     io_load<MMAX>(a, (uint32_t)n, 0, x, u);
@@ -316,9 +321,30 @@ __global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
             if (m == dev_ninf())
                 m = 0.0; /* every emission impossible: f_t = 0, alpha = NaN as in Stan */
             double e[K];
+            if (EXACT && want_ffbs) { /* the FFBS contract's e_t (correctly rounded exp) */
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                e[k] = exp(st.o[k] - m);
+                for (int k = 0; k < K; ++k)
+                    e[k] = hhmm_cr_exp(st.o[k] - m);
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    e[k] = exp(st.o[k] - m);
+            }
+            /* FFBS: the K-vector transition does not depend on the
+             * next state, so z_{t-1} = cat(v_{t-1} .* A_t, u_{t-1}) is drawn here */
+            if (want_ffbs) {
+                if (t > 0) {
+                    double w[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        w[k] = vprev[k] * st.A[k];
+                    at(a.z_ffbs + a.P * (int64_t)(t - 1), (uint32_t)p * 4u) = ffbs_cat<K>(w, uprev) + 1;
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    vprev[k] = (t == 0) ? pp.p[k] * e[k] : e[k];
+                uprev = at(a.ffbs_u + a.P * (int64_t)t, (uint32_t)p * 8u);
+            }
             /* unalpha in log space, so that a state whose emission underflows
              * exp(o - m) keeps Stan's finite value:
              *   t = 0: log(p_1k[j]) + oblik_1(j)                    (iohmm-reg.stan:62-63)
@@ -447,6 +473,8 @@ __global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
         for (int m2 = 0; m2 < MMAX; ++m2)
             u[m2] = un[m2];
     }
+    if (want_ffbs)
+        at(a.z_ffbs + a.P * (int64_t)(Tp - 1), (uint32_t)p * 4u) = ffbs_cat<K>(vprev, uprev) + 1;
     if ((out & HHMM_OUT_LOGLIK) && a.loglik) /* target += log_sum_exp(unalpha_tk[T]) (iohmm-reg.stan:120) */
         a.loglik[p] = log(vsum<K>(f)) + (lsc + kLn2 * ex);
 
@@ -469,23 +497,6 @@ __global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
 /* ------------------------------------------------------------------ */
 /* Host-side launch                                                      */
 /* ------------------------------------------------------------------ */
-
-bool iohmm_supported(int K, int M, int L, char *why, size_t why_len)
-{
-    if (K < 1 || K > kMaxK) {
-        snprintf(why, why_len, "IOHMM device path supports K = 1..%d (got %d)", kMaxK, K);
-        return false;
-    }
-    if (M < 1 || M > 8) {
-        snprintf(why, why_len, "IOHMM device path supports M = 1..8 (got %d)", M);
-        return false;
-    }
-    if (L > kIoLmax) {
-        snprintf(why, why_len, "IOHMM mixture device path supports L <= %d (got %d)", kIoLmax, L);
-        return false;
-    }
-    return true;
-}
 
 template <int FAM, int K, int MMAX, bool EXACT>
 static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
@@ -518,34 +529,18 @@ static hhmm_status launch_io3(const DevArgs &a, hipStream_t st)
     return exact ? launch_io4<FAM, K, 8, true>(a, st) : launch_io4<FAM, K, 8, false>(a, st);
 }
 
-template <int FAM>
-static hhmm_status launch_io2(const DevArgs &a, hipStream_t st)
+/* Dispatch on K for the K values [KK, KHI] this translation unit instantiates. */
+template <int FAM, int KK, int KHI>
+static hhmm_status launch_io_range(const DevArgs &a, hipStream_t st)
 {
-    switch (a.K) {
-    case 1: return launch_io3<FAM, 1>(a, st);
-    case 2: return launch_io3<FAM, 2>(a, st);
-    case 3: return launch_io3<FAM, 3>(a, st);
-    case 4: return launch_io3<FAM, 4>(a, st);
-    case 5: return launch_io3<FAM, 5>(a, st);
-    case 6: return launch_io3<FAM, 6>(a, st);
-    case 7: return launch_io3<FAM, 7>(a, st);
-    case 8: return launch_io3<FAM, 8>(a, st);
-    default:
-        set_error("K = %d not supported (1..%d)", a.K, kMaxK);
+    if constexpr (KK > KHI) {
+        set_error("K = %d not supported by this IOHMM build", a.K);
         return HHMM_ERR_UNSUPPORTED;
+    } else {
+        if (a.K == KK)
+            return launch_io3<FAM, KK>(a, st);
+        return launch_io_range<FAM, KK + 1, KHI>(a, st);
     }
-}
-
-hhmm_status launch_iohmm(const DevArgs &a, hipStream_t st)
-{
-    char why[160];
-    if (!iohmm_supported(a.K, a.M, a.model == HHMM_MODEL_IOHMM_REG ? 1 : a.L, why, sizeof(why))) {
-        set_error("%s", why);
-        return HHMM_ERR_UNSUPPORTED;
-    }
-    if (a.model == HHMM_MODEL_IOHMM_REG)
-        return launch_io2<IO_REG>(a, st);
-    return launch_io2<IO_MIX>(a, st);
 }
 
 } // namespace hhmm

@@ -1,804 +1,51 @@
 /*
- * hhmm_kernels.hip -- gfx950 kernels for the HMM-family path.
- *
- * Layout in HBM (include/hhmm.h): every array is pair-/series-/draw-fastest,
- * so one wave of 64 lanes = 64 consecutive pairs reads and writes 64
- * consecutive elements per (t, k): every global access below is a fully
- * coalesced 256 B (int32) or 512 B (fp64) wave transaction.
- *
- * One LANE owns one (series, draw) PAIR for the whole sequence; the K-state
- * vectors live in registers.  Per-pair emission tables (phi_k and log phi_k,
- * K*L doubles) live in LDS, one slab per wave, laid out
- *     slab[(l * KP + kp) * 64 + lane]  (double2: states 2kp, 2kp+1)
- * so a 16-lane ds_read_b128 group touches 16 consecutive 16-B slots = all 64
- * banks once: conflict-free for any per-lane symbol.
- *
- * Kernels:
- *   fb_kernel      A2/A1 emissions, A6 forward + loglik, A7 alpha, A8 backward,
- *                  A9 gamma, A12/A13 masks.  LINEAR-space scaled recursion
- *                  (K^2 FMAs per step, an exact power-of-two renormalisation
- *                  per step; no exp/log in the discrete loop);
- *                  forward checkpoints every C steps, recomputed chunk by chunk
- *                  in the backward sweep.  Tolerance 1e-9 rel.
- * Latency rules used throughout (the kernels are latency-, not issue-bound at
- * the 2 waves/SIMD the LDS tables allow): observation loads are issued
- * unconditionally (clamped index) one chunk ahead, checkpoints and
- * back-pointer words one chunk ahead, and each step's LDS emission row is
- * fetched one step ahead.
- *   viterbi_kernel A11 max-plus recursion in LOG space with exactly the
- *                  reference's operation order and tie rules, log tables from
- *                  the correctly rounded hhmm_cr_log (bit-identical to the
- *                  oracle); back-pointers packed 2 bits/state to HBM, backtrack
- *                  in the same kernel.  Bit-exact.
- * Build with -ffp-contract=off: the Viterbi sums must round exactly as written.
+ * hhmm_kernels.hip -- host-side launch plumbing of libhhmm.so: workspace
+ * sizing and carving, request -> DevArgs, per-model dispatch to the
+ * translation units that instantiate the kernels (hhmm_m_*.hip for the HMM
+ * family, hhmm_iohmm*.hip for the IOHMM family), and the device self-test of
+ * the correctly rounded log.
  */
 #include <hip/hip_runtime.h>
-#include <math.h>
-#include <stdarg.h>
-#include <stdio.h>
 #include <string.h>
+
+#include <stdio.h>
 
 #include "hhmm_device.h"
 
 namespace hhmm {
 
+constexpr int kIoLmax = 8; /* mixture components per state on the IOHMM device path (hhmm_iohmm.h) */
 
-/* hmm-multinom-semisup.stan:42 -- j0 is 0-based */
-__device__ __forceinline__ bool semisup_mask(int g, int j0)
+bool iohmm_supported(int K, int M, int L, char *why, size_t why_len)
 {
-    const int j = j0 + 1;
-    return (g == 1 && (j == 1 || j == 4)) || (g == 2 && (j == 2 || j == 3));
-}
-/* hhmm-tayal2009.stan:62 / :109 / :144 */
-__device__ __forceinline__ bool tayal_pred(int s, int j0)
-{
-    const int j = j0 + 1;
-    return (s == 1 && (j == 2 || j == 3)) || (s == 2 && (j == 1 || j == 4));
-}
-/* hhmm-tayal2009.stan:51 */
-__device__ __forceinline__ bool tayal_init_pred(int s, int j0)
-{
-    const int j = j0 + 1;
-    return (s == 1 && j == 3) || (s == 2 && j == 1);
-}
-
-template <int MODEL>
-struct ModelTraits {
-    static constexpr bool kGauss = (MODEL == HHMM_MODEL_HMM_GAUSS);
-    static constexpr bool kSemisup = (MODEL == HHMM_MODEL_HMM_MULTINOM_SEMISUP);
-    static constexpr bool kTayal = (MODEL == HHMM_MODEL_TAYAL || MODEL == HHMM_MODEL_TAYAL_LITE);
-    static constexpr bool kDiscrete = !kGauss;
-    static constexpr bool kAux = kSemisup || kTayal; /* needs g[] or sign[] per step */
-};
-
-/* One observation step of a series. */
-struct Obs {
-    int x;     /* symbol 1..L (discrete models) */
-    int aux;   /* g (semisup) or sign (tayal) */
-    double xr; /* real observation (gauss) */
-};
-
-/* Observation streams of one series (series-fastest arrays): uniform base
- * pointers + this lane's 32-bit series index.  A time row t is the uniform
- * pointer base + N*t, so hipcc can address it as SGPR base + VGPR offset. */
-struct SeriesPtrs {
-    const int32_t *x;
-    const int32_t *aux;
-    const double *xr;
-    int64_t stride; /* N: elements between consecutive time steps */
-    uint32_t n;     /* this lane's series */
-    int tmax;       /* padded time extent of the arrays */
-};
-
-/* Loads the C observations of chunk [t0, t0+C).  Every load is issued
- * unconditionally from a wave-uniform time index clamped into [0, Tmax-1]: a
- * conditional load makes hipcc branch around it and drain vmcnt(0) per
- * element (cdna_hip_programming.md §5, trap (c)); rows past a lane's own
- * length are padding that is never consumed. */
-template <int MODEL, int C, bool AUX>
-__device__ __forceinline__ void load_chunk(Obs (&dst)[C], const SeriesPtrs &sp, int t0)
-{
-#pragma unroll
-    for (int u = 0; u < C; ++u) {
-        const int tc = min(max(t0 + u, 0), sp.tmax - 1);
-        const int64_t row = (int64_t)tc * sp.stride;
-        dst[u].x = 1;
-        dst[u].aux = 0;
-        dst[u].xr = 0.0;
-        if constexpr (!ModelTraits<MODEL>::kGauss)
-            dst[u].x = at(sp.x + row, sp.n * 4u);
-        if constexpr (AUX)
-            dst[u].aux = at(sp.aux + row, sp.n * 4u);
-        if constexpr (ModelTraits<MODEL>::kGauss)
-            dst[u].xr = at(sp.xr + row, sp.n * 8u);
+    if (K < 1 || K > kMaxK) {
+        snprintf(why, why_len, "IOHMM device path supports K = 1..%d (got %d)", kMaxK, K);
+        return false;
     }
+    if (M < 1 || M > 8) {
+        snprintf(why, why_len, "IOHMM device path supports M = 1..8 (got %d)", M);
+        return false;
+    }
+    if (L > kIoLmax) {
+        snprintf(why, why_len, "IOHMM mixture device path supports L <= %d (got %d)", kIoLmax, L);
+        return false;
+    }
+    return true;
 }
 
-/* Per-pair parameters held in registers. */
-template <int MODEL, int K>
-struct PairParams {
-    double A[K][K];  /* probability (FB) or log (Viterbi) */
-    double p[K];
-    double mu[K], isig[K], lsig[K], c0[K]; /* gauss: 1/sigma, log sigma, NEG_LOG_SQRT_TWO_PI - log sigma */
-};
-
-template <int K>
-__device__ __forceinline__ double draw1(const double *arr, const DevArgs &a, int64_t d, int k)
+hhmm_status launch_iohmm(const DevArgs &a, hipStream_t st)
 {
-    return arr[d + a.S * (int64_t)k];
-}
-template <int K>
-__device__ __forceinline__ double draw2(const double *arr, const DevArgs &a, int64_t d, int i, int j, int I)
-{
-    return arr[d + a.S * ((int64_t)i + (int64_t)I * j)];
-}
-
-/* Loads p_1k, A_ij (Tayal: expands p_11 / A_row, hhmm-tayal2009.stan:30-44)
- * and the Gaussian constants.  LOG = true puts log A in params.A. */
-template <int MODEL, int K, bool LOG>
-__device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevArgs &a, int64_t d)
-{
-    if constexpr (ModelTraits<MODEL>::kTayal) {
-        static_assert(K == 4, "tayal is a K = 4 model");
-        const double p11 = a.p_11[d];
-        const double r00 = a.A_row[d + a.S * 0], r10 = a.A_row[d + a.S * 1];
-        const double r01 = a.A_row[d + a.S * 2], r11 = a.A_row[d + a.S * 3];
-        double A[4][4] = {{0, r00, r01, 0}, {1, 0, 0, 0}, {r10, 0, 0, r11}, {0, 0, 1, 0}};
-        pp.p[0] = p11;
-        pp.p[1] = 0;
-        pp.p[2] = 1 - p11;
-        pp.p[3] = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                pp.A[i][j] = LOG ? hhmm_cr_log(A[i][j]) : A[i][j];
-    } else {
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            pp.p[k] = draw1<K>(a.p_1k, a, d, k);
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const double v = draw2<K>(a.A_ij, a, d, i, j, K);
-                pp.A[i][j] = LOG ? hhmm_cr_log(v) : v;
-            }
+    char why[160];
+    if (!iohmm_supported(a.K, a.M, a.model == HHMM_MODEL_IOHMM_REG ? 1 : a.L, why, sizeof(why))) {
+        set_error("%s", why);
+        return HHMM_ERR_UNSUPPORTED;
     }
-    if constexpr (ModelTraits<MODEL>::kGauss) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double sg = draw1<K>(a.sigma_k, a, d, k);
-            pp.mu[k] = draw1<K>(a.mu_k, a, d, k);
-            pp.isig[k] = 1.0 / sg;
-            pp.lsig[k] = hhmm_cr_log(sg);
-            pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - pp.lsig[k];
-        }
-    }
+    const bool lo = a.K <= 4;
+    if (a.model == HHMM_MODEL_IOHMM_REG)
+        return lo ? run_io_reg_lo(a, st) : run_io_reg_hi(a, st);
+    return lo ? run_io_mix_lo(a, st) : run_io_mix_hi(a, st);
 }
 
-/* Fills this lane's LDS slab with phi_k (LOG: log phi_k). */
-template <int K, bool LOG>
-__device__ __forceinline__ void fill_table(double2 *slab, const DevArgs &a, int64_t d)
-{
-    constexpr int KP = (K + 1) / 2;
-    for (int l = 0; l < a.L; ++l) {
-#pragma unroll
-        for (int kp = 0; kp < KP; ++kp) {
-            double v0 = draw2<K>(a.phi_k, a, d, 2 * kp, l, K);
-            double v1 = (2 * kp + 1 < K) ? draw2<K>(a.phi_k, a, d, 2 * kp + 1, l, K) : 0.0;
-            if (LOG) {
-                v0 = hhmm_cr_log(v0);
-                v1 = hhmm_cr_log(v1);
-            }
-            slab[(l * KP + kp) * 64] = make_double2(v0, v1);
-        }
-    }
-}
-
-template <int K>
-__device__ __forceinline__ void read_table(const double2 *slab, int x, int L, double (&e)[K])
-{
-    constexpr int KP = (K + 1) / 2;
-    const int row = min(max(x, 1), L) - 1;
-    const double2 *r = slab + row * KP * 64;
-#pragma unroll
-    for (int kp = 0; kp < KP; ++kp) {
-        const double2 v = r[kp * 64];
-        e[2 * kp] = v.x;
-        if (2 * kp + 1 < K)
-            e[2 * kp + 1] = v.y;
-    }
-}
-
-/* Stan's scalar normal_lpdf(y | mu_j, sigma_j) with cached c0 = C - log(sigma),
- * isig = 1/sigma: ((C - log sigma) + (-0.5 * z*z)), z = (y - mu) * isig. */
-template <int MODEL, int K>
-__device__ __forceinline__ double gauss_lpdf(const PairParams<MODEL, K> &pp, double y, int j)
-{
-    const double z = (y - pp.mu[j]) * pp.isig[j];
-    const double z2 = z * z;
-    return pp.c0[j] + (-0.5 * z2);
-}
-
-/* Emission of one step for the linear-space filter: e[j] (probabilities,
- * Gaussian densities divided by their max m over states) and log m. */
-template <int K>
-struct Em {
-    double e[K];
-    double m;
-};
-
-template <int MODEL, int K>
-__device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const double2 *slab, int L,
-                                          const Obs &o, Em<K> &em)
-{
-    if constexpr (ModelTraits<MODEL>::kGauss) {
-        double lp[K];
-        double m = dev_ninf();
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            lp[j] = gauss_lpdf<MODEL, K>(pp, o.xr, j);
-            m = fmax(m, lp[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            em.e[j] = exp(lp[j] - m);
-        em.m = m;
-    } else {
-        read_table<K>(slab, o.x, L, em.e);
-        em.m = 0.0;
-    }
-}
-
-/* out = e_t .* (in M_t), with the model's transition masks; in may alias out. */
-template <int MODEL, int K>
-__device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
-                                            const double (&e)[K], const Obs &o, int &ex)
-{
-    double s[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        double acc = al[0] * pp.A[0][j];
-#pragma unroll
-        for (int i = 1; i < K; ++i)
-            acc = fma(al[i], pp.A[i][j], acc);
-        s[j] = acc;
-    }
-    if constexpr (ModelTraits<MODEL>::kAux) {
-        double tot = al[0];
-#pragma unroll
-        for (int i = 1; i < K; ++i)
-            tot += al[i];
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            bool on;
-            if constexpr (ModelTraits<MODEL>::kSemisup)
-                on = semisup_mask(o.aux, j);
-            else
-                on = tayal_pred(o.aux, j);
-            s[j] = on ? s[j] : tot;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        out[j] = s[j] * e[j];
-    renorm<K>(out, ex);
-}
-
-template <int MODEL, int K>
-__device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL, K> &pp, const double (&e)[K],
-                                         const Obs &o, int &ex)
-{
-    fwd_step_to<MODEL, K>(al, al, pp, e, o, ex);
-}
-
-/* beta_{t-1} from beta_t and step t's emission / masks. */
-template <int MODEL, int K>
-__device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL, K> &pp,
-                                         const double (&e)[K], const Obs &o, int &ex)
-{
-    double b[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-        b[i] = e[i] * be[i];
-    double s[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        double acc = pp.A[j][0] * b[0];
-#pragma unroll
-        for (int i = 1; i < K; ++i)
-            acc = fma(pp.A[j][i], b[i], acc);
-        s[j] = acc;
-    }
-    if constexpr (ModelTraits<MODEL>::kTayal) { /* predicate on the PREVIOUS state j (Q6) */
-        double tot = b[0];
-#pragma unroll
-        for (int i = 1; i < K; ++i)
-            tot += b[i];
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            s[j] = tayal_pred(o.aux, j) ? s[j] : tot;
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        be[j] = s[j];
-    renorm<K>(be, ex);
-}
-
-/* alpha_1 (t = 0) from the step-0 observation / emission. */
-template <int MODEL, int K>
-__device__ __forceinline__ void fwd_init(double (&al)[K], const PairParams<MODEL, K> &pp, const Em<K> &em,
-                                         const Obs &o, double &lsc, int &ex)
-{
-    if constexpr (ModelTraits<MODEL>::kGauss) {
-        /* hmm.stan:30 -- log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k) (Q2) */
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double z = (o.xr - pp.mu[k]) * pp.isig[k];
-            const double z2 = z * z;
-            s += HHMM_NEG_LOG_SQRT_TWO_PI;
-            s -= pp.lsig[k];
-            s += -0.5 * z2;
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            al[k] = pp.p[k];
-        lsc += s;
-    } else {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if constexpr (ModelTraits<MODEL>::kTayal)
-                al[k] = tayal_init_pred(o.aux, k) ? em.e[k] * pp.p[k] : em.e[k];
-            else
-                al[k] = pp.p[k] * em.e[k];
-        }
-    }
-    renorm<K>(al, ex);
-}
-
-
-template <int MODEL, bool AUX>
-__device__ __forceinline__ SeriesPtrs series_ptrs(const DevArgs &a, int64_t n)
-{
-    SeriesPtrs sp;
-    sp.stride = a.N;
-    sp.n = (uint32_t)n;
-    sp.tmax = a.Tmax;
-    sp.x = a.x;
-    sp.aux = nullptr;
-    if constexpr (AUX && ModelTraits<MODEL>::kSemisup)
-        sp.aux = a.g;
-    if constexpr (AUX && ModelTraits<MODEL>::kTayal)
-        sp.aux = a.sign;
-    sp.xr = a.xr;
-    return sp;
-}
-
-/* ------------------------------------------------------------------ */
-/* Forward / backward / posteriors                                       */
-/* ------------------------------------------------------------------ */
-
-/* Output profile of the forward-backward kernel (compile time). */
-enum FbMode {
-    FB_GAMMA = 0, /* loglik + gamma_tk: the hot path, no per-output branches */
-    FB_FULL = 1,  /* any mix of alpha/beta/unalpha/unbeta/ungamma/gamma (+ per-step log scale) */
-    FB_FWD = 2    /* forward only: loglik / alpha / unalpha (tayal-lite, no backward output) */
-};
-
-
-/* Writes the forward-side outputs of step t (alpha, unalpha). */
-template <int K>
-__device__ __forceinline__ void emit_alpha(const DevArgs &a, int64_t p, int t, const double (&al)[K], double lsc)
-{
-    if ((a.outputs & HHMM_OUT_ALPHA) && a.alpha) {
-        const double r = 1.0 / vsum<K>(al);
-        double v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            v[k] = al[k] * r;
-        store_tk<K>(a.alpha, a, p, t, v);
-    }
-    if ((a.outputs & HHMM_OUT_UNALPHA) && a.unalpha) {
-        double v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            v[k] = log(al[k]) + lsc;
-        store_tk<K>(a.unalpha, a, p, t, v);
-    }
-}
-
-/* Outputs of step t once alpha_t and beta_t are known. */
-template <int K, int MODE>
-__device__ __forceinline__ void emit_posteriors(const DevArgs &a, int64_t p, int t, const double (&al)[K],
-                                                const double (&be)[K], double lsa, double lsb)
-{
-    if constexpr (MODE == FB_GAMMA) {
-        /* gamma = (alpha .* beta) / sum: the normalisations of alpha and beta
-         * cancel, one division per step (hmm.stan:89-96 up to rounding) */
-        double ug[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            ug[k] = al[k] * be[k];
-        const double r = fast_rcp(vsum<K>(ug));
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            ug[k] = ug[k] * r;
-        store_tk<K>(a.gamma, a, p, t, ug);
-    } else {
-        const uint32_t o = a.outputs;
-        emit_alpha<K>(a, p, t, al, lsa);
-        const double sb = vsum<K>(be);
-        if ((o & HHMM_OUT_BETA) && a.beta) {
-            const double r = 1.0 / sb;
-            double v[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                v[k] = be[k] * r;
-            store_tk<K>(a.beta, a, p, t, v);
-        }
-        if ((o & HHMM_OUT_UNBETA) && a.unbeta) {
-            /* unbeta_tk[T] = 1 (Q1): every unbeta carries +1 */
-            double v[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                v[k] = (log(be[k]) + lsb) + 1.0;
-            store_tk<K>(a.unbeta, a, p, t, v);
-        }
-        if (o & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
-            const double ra = 1.0 / vsum<K>(al), rb = 1.0 / sb;
-            double ug[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                ug[k] = (al[k] * ra) * (be[k] * rb);
-            if ((o & HHMM_OUT_UNGAMMA) && a.ungamma)
-                store_tk<K>(a.ungamma, a, p, t, ug);
-            if ((o & HHMM_OUT_GAMMA) && a.gamma) {
-                const double rg = 1.0 / vsum<K>(ug);
-                double v[K];
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    v[k] = ug[k] * rg;
-                store_tk<K>(a.gamma, a, p, t, v);
-            }
-        }
-    }
-}
-
-/* Per-lane state of the forward-backward kernel. */
-template <int MODEL, int K>
-struct FbLane {
-    PairParams<MODEL, K> pp;
-    const double2 *slab;
-    int L;
-    int64_t p;
-    int Tp;
-};
-
-/* One forward chunk [t0, t0+C).  FULLC: every lane of the wave has all C
- * steps (no per-step predicate).  The emission of step u+1 is fetched before
- * step u is computed (LDS latency hidden behind the K^2 FMAs). */
-template <int MODEL, int K, int C, int MODE, bool FULLC>
-__device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, K> &ln, int c, const Obs (&cur)[C],
-                                          const Obs &nxt0, Em<K> &ecur, double (&al)[K], double &lsc, int &ex)
-{
-    const int t0 = c * C;
-#pragma unroll
-    for (int u = 0; u < C; ++u) {
-        const int t = t0 + u;
-        Em<K> enx;
-        emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, (u + 1 < C) ? cur[u + 1 < C ? u + 1 : 0] : nxt0, enx);
-        if (FULLC || t < ln.Tp) {
-            if (u == 0 && c == 0) {
-                fwd_init<MODEL, K>(al, ln.pp, ecur, cur[0], lsc, ex);
-            } else {
-                lsc += ecur.m;
-                fwd_step<MODEL, K>(al, ln.pp, ecur.e, cur[u], ex);
-            }
-            if constexpr (MODE == FB_FWD) {
-                emit_alpha<K>(a, ln.p, t, al, lsc + kLn2 * ex);
-            } else if (u == 0) {
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    at(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)ln.p * 8u) = al[k];
-                if constexpr (MODE == FB_FULL)
-                    at(a.ckpt_ls + a.P * (int64_t)c, (uint32_t)ln.p * 8u) = lsc + kLn2 * ex;
-            }
-        }
-        ecur = enx;
-    }
-}
-
-/* One backward chunk: recompute alpha over the chunk from its checkpoint,
- * then walk t = t0+C-1 .. t0 emitting the posteriors and stepping beta. */
-template <int MODEL, int K, int C, int MODE, bool FULLC>
-__device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, K> &ln, int c, const Obs (&cur)[C],
-                                          const double (&ck)[K], double ck_ls, double (&be)[K], double &blsc,
-                                          int &bex)
-{
-    const int t0 = c * C;
-    double abuf[C][K];
-    double lsbuf[MODE == FB_FULL ? C : 1];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        abuf[0][k] = ck[k];
-    lsbuf[0] = ck_ls;
-    {
-        double lsacc = 0.0;
-        int exb = 0;
-        Em<K> ecur;
-        emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[1 < C ? 1 : 0], ecur);
-#pragma unroll
-        for (int u = 1; u < C; ++u) {
-            Em<K> enx;
-            emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[u + 1 < C ? u + 1 : u], enx);
-            if (FULLC || t0 + u < ln.Tp) {
-                lsacc += ecur.m;
-                fwd_step_to<MODEL, K>(abuf[u - 1], abuf[u], ln.pp, ecur.e, cur[u], exb);
-            }
-            if constexpr (MODE == FB_FULL)
-                lsbuf[u] = ck_ls + (lsacc + kLn2 * exb);
-            ecur = enx;
-        }
-    }
-    Em<K> ecur;
-    emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[C - 1], ecur);
-#pragma unroll
-    for (int u = C - 1; u >= 0; --u) {
-        const int t = t0 + u;
-        Em<K> enx;
-        emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[u > 0 ? u - 1 : 0], enx);
-        if (FULLC || t < ln.Tp) {
-            emit_posteriors<K, MODE>(a, ln.p, t, abuf[u], be, lsbuf[MODE == FB_FULL ? u : 0],
-                                     blsc + kLn2 * bex);
-            if (t > 0) {
-                if constexpr (MODE == FB_FULL)
-                    blsc += ecur.m;
-                bwd_step<MODEL, K>(be, ln.pp, ecur.e, cur[u], bex);
-            }
-        }
-        ecur = enx;
-    }
-}
-
-template <int MODEL, int K, int MODE>
-__global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
-{
-    constexpr int C = fb_chunk(K);
-    constexpr bool AUX = ModelTraits<MODEL>::kAux;
-    HIP_DYNAMIC_SHARED(double2, lds)
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    /* lanes past the last pair redo pair P-1 (identical values, benign
-     * duplicate stores): every lane stays in the wave-wide reductions */
-    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
-    int64_t n, d;
-    pair_coords(a, p, n, d);
-    constexpr int KP = (K + 1) / 2;
-
-    FbLane<MODEL, K> ln;
-    ln.p = p;
-    ln.L = a.L;
-    ln.Tp = pair_len(a, n);
-    ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
-    load_params<MODEL, K, false>(ln.pp, a, d);
-    if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
-    const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
-    const int Tw_min = wave_min(ln.Tp);
-    const int Tw_max = wave_max(ln.Tp);
-    const int nfull = Tw_min / C;              /* chunks complete for every lane */
-    const int nchunk = (Tw_max + C - 1) / C;   /* chunks any lane needs */
-
-    /* ---- forward sweep ---- */
-    double al[K];
-    double lsc = 0.0; /* log scale excluding the binary exponent */
-    int ex = 0;       /* sum of binary exponents removed */
-    Obs cur[C];
-    load_chunk<MODEL, C, AUX>(cur, sp, 0);
-    Em<K> ecur;
-    emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[0], ecur);
-    for (int c = 0; c < nchunk; ++c) {
-        Obs nxt[C];
-        load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C);
-        if (c < nfull)
-            fwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
-        else
-            fwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
-#pragma unroll
-        for (int u = 0; u < C; ++u)
-            cur[u] = nxt[u];
-    }
-    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
-        a.loglik[p] = log(vsum<K>(al)) + (lsc + kLn2 * ex);
-    if constexpr (MODE == FB_FWD)
-        return;
-
-    /* ---- backward sweep, chunk by chunk from the end ---- */
-    double be[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        be[k] = 1.0;
-    double blsc = 0.0;
-    int bex = 0;
-    const int clast = nchunk - 1;
-    load_chunk<MODEL, C, AUX>(cur, sp, clast * C);
-    /* checkpoint rows are wave-uniform: a lane shorter than the wave reads
-     * (unused) slots past its own last chunk, never past the allocation */
-    double ck[K], ck_ls = 0.0;
-    {
-        const int cc = clast;
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            ck[k] = at(a.ckpt + a.P * ((int64_t)cc * K + k), (uint32_t)p * 8u);
-        if constexpr (MODE == FB_FULL)
-            ck_ls = at(a.ckpt_ls + a.P * (int64_t)cc, (uint32_t)p * 8u);
-    }
-    for (int c = clast; c >= 0; --c) {
-        Obs nxt[C];
-        load_chunk<MODEL, C, AUX>(nxt, sp, (c - 1) * C);
-        double cn[K], cn_ls = 0.0;
-        {
-            const int cc = max(c - 1, 0);
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                cn[k] = at(a.ckpt + a.P * ((int64_t)cc * K + k), (uint32_t)p * 8u);
-            if constexpr (MODE == FB_FULL)
-                cn_ls = at(a.ckpt_ls + a.P * (int64_t)cc, (uint32_t)p * 8u);
-        }
-        if (c < nfull)
-            bwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, ck, ck_ls, be, blsc, bex);
-        else
-            bwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, ck, ck_ls, be, blsc, bex);
-#pragma unroll
-        for (int u = 0; u < C; ++u)
-            cur[u] = nxt[u];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            ck[k] = cn[k];
-        ck_ls = cn_ls;
-    }
-}
-
-/* ------------------------------------------------------------------ */
-/* Viterbi                                                                */
-/* ------------------------------------------------------------------ */
-
-/* Log emission of state j at one step, bit-identical to the reference. */
-template <int MODEL, int K>
-__device__ __forceinline__ void emit_log(const PairParams<MODEL, K> &pp, const double2 *slab, int L,
-                                         const Obs &o, double (&le)[K])
-{
-    if constexpr (ModelTraits<MODEL>::kGauss) {
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            le[j] = gauss_lpdf<MODEL, K>(pp, o.xr, j);
-    } else {
-        read_table<K>(slab, o.x, L, le);
-    }
-}
-
-
-/* One max-plus step t >= 1: delta_t(j) = max_i cand(i, j) with the
- * reference's strict '>' from -inf (first maximising i wins, NaN never
- * wins); back-pointer i packed into `word` at `slot`. */
-template <int MODEL, int K>
-__device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
-                                         const Obs &o, uint32_t &word, int slot)
-{
-    constexpr int BITS = bp_bits(K);
-    constexpr int STEPB = K * BITS;
-    double nd[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        double best = dev_ninf();
-        uint32_t arg = 0;
-        bool on = true;
-        if constexpr (ModelTraits<MODEL>::kTayal)
-            on = tayal_pred(o.aux, j);
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            double cand;
-            if constexpr (ModelTraits<MODEL>::kTayal) {
-                /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
-                cand = dl[i] + le[j];
-                cand = on ? cand + pp.A[i][j] : cand;
-            } else {
-                /* (delta + log A) + emission (hmm.stan:111) */
-                cand = (dl[i] + pp.A[i][j]) + le[j];
-            }
-            if (cand > best) {
-                best = cand;
-                arg = (uint32_t)i;
-            }
-        }
-        nd[j] = best;
-        word |= arg << (slot * STEPB + j * BITS);
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        dl[j] = nd[j];
-}
-
-template <int MODEL, int K, int CV, bool FULLC>
-__device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const PairParams<MODEL, K> &pp,
-                                              const double2 *slab, int Tp, int c, const Obs (&cur)[CV],
-                                              const Obs &nxt0, double (&le)[K], double (&dl)[K], uint32_t &word)
-{
-    constexpr int SPW = bp_steps_per_word(K);
-    const int t0 = c * CV;
-#pragma unroll
-    for (int u = 0; u < CV; ++u) {
-        const int t = t0 + u;
-        double ln[K];
-        emit_log<MODEL, K>(pp, slab, a.L, (u + 1 < CV) ? cur[u + 1 < CV ? u + 1 : 0] : nxt0, ln);
-        if (FULLC || t < Tp) {
-            if (!(u == 0 && c == 0))
-                vit_step<MODEL, K>(dl, pp, le, cur[u], word, u % SPW);
-            if (u % SPW == SPW - 1) {
-                at(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u) = word;
-                word = 0;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            le[k] = ln[k];
-    }
-}
-
-template <int MODEL, int K>
-__global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
-{
-    constexpr int SPW = bp_steps_per_word(K);
-    constexpr int CV = vit_chunk(K);
-    constexpr int WPC = CV / SPW; /* words per chunk */
-    constexpr bool VAUX = ModelTraits<MODEL>::kTayal; /* semisup Viterbi is unmasked (Q7) */
-    HIP_DYNAMIC_SHARED(double2, lds)
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
-    int64_t n, d;
-    pair_coords(a, p, n, d);
-    const int Tp = pair_len(a, n);
-    constexpr int KP = (K + 1) / 2;
-    double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
-
-    PairParams<MODEL, K> pp;
-    load_params<MODEL, K, true>(pp, a, d);
-    if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, true>(slab, a, d);
-    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, n);
-    const int Tw_min = wave_min(Tp);
-    const int Tw_max = wave_max(Tp);
-    const int nfull = Tw_min / CV;
-    const int nchunk = (Tw_max + CV - 1) / CV;
-
-    /* delta_tk[1, K] = emission of j for j = 1..K: only column K is written,
-     * the others keep stanc's NaN (Q3, e.g. hmm-multinom.stan:236-237). */
-    double dl[K];
-    Obs cur[CV];
-    load_chunk<MODEL, CV, VAUX>(cur, sp, 0);
-    double le[K];
-    emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
-#pragma unroll
-    for (int k = 0; k < K - 1; ++k)
-        dl[k] = dev_nan();
-    dl[K - 1] = le[K - 1];
-    uint32_t word = 0;
-    for (int c = 0; c < nchunk; ++c) {
-        Obs nxt[CV];
-        load_chunk<MODEL, CV, VAUX>(nxt, sp, (c + 1) * CV);
-        if (c < nfull)
-            vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
-        else
-            vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
-#pragma unroll
-        for (int u = 0; u < CV; ++u)
-            cur[u] = nxt[u];
-    }
-    viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dl, word);
-}
 
 /* ------------------------------------------------------------------ */
 /* Self-test kernel                                                       */
@@ -810,20 +57,18 @@ __global__ void cr_log_kernel(const double *in, double *out, int64_t n)
         out[i] = hhmm_cr_log(in[i]);
 }
 
+
 /* ------------------------------------------------------------------ */
-/* Host-side launch plumbing                                             */
+/* Workspace                                                              */
 /* ------------------------------------------------------------------ */
 
-static bool model_has_backward(int model)
-{
-    return model == HHMM_MODEL_HMM_GAUSS || model == HHMM_MODEL_HMM_MULTINOM ||
-           model == HHMM_MODEL_HMM_MULTINOM_SEMISUP || model == HHMM_MODEL_TAYAL;
-}
 
-static bool needs_backward(int model, uint32_t out)
+static bool needs_ckpt(int model, uint32_t out)
 {
-    return model_has_backward(model) &&
-           (out & (HHMM_OUT_UNBETA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
+    const bool hmm_bwd = model == HHMM_MODEL_HMM_GAUSS || model == HHMM_MODEL_HMM_MULTINOM ||
+                         model == HHMM_MODEL_HMM_MULTINOM_SEMISUP || model == HHMM_MODEL_TAYAL;
+    return hmm_bwd &&
+           (out & (HHMM_OUT_UNBETA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA | HHMM_OUT_FFBS)) != 0;
 }
 
 static bool is_iohmm_model(int model)
@@ -840,7 +85,7 @@ static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs)
 {
     size_t bytes = 0;
-    if (needs_backward(model, outputs)) {
+    if (needs_ckpt(model, outputs)) {
         bytes += align256((size_t)nchunk_of(K, Tmax) * K * P * sizeof(double));
         bytes += align256((size_t)nchunk_of(K, Tmax) * P * sizeof(double));
     }
@@ -859,7 +104,7 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos)
     a.ckpt = nullptr;
     a.ckpt_ls = nullptr;
     a.bp = nullptr;
-    if (needs_backward(a.model, a.outputs)) {
+    if (needs_ckpt(a.model, a.outputs)) {
         a.ckpt = (double *)b;
         b += align256((size_t)nchunk_of(a.K, Tmax) * a.K * a.P * sizeof(double));
         a.ckpt_ls = (double *)b;
@@ -873,145 +118,6 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos)
     }
     if (is_iohmm_model(a.model) && (a.outputs & HHMM_OUT_UNBETA))
         a.lam = (double *)b;
-}
-
-struct LaunchShape {
-    dim3 grid, block;
-    size_t lds;
-};
-
-static bool shape_for(const DevArgs &a, bool discrete, LaunchShape &s)
-{
-    const int KP = (a.K + 1) / 2;
-    size_t per_wave = discrete ? (size_t)a.L * KP * 64 * sizeof(double2) : 0;
-    int waves = 4;
-    if (per_wave > 0) {
-        while (waves > 0 && per_wave * waves > kLdsLimit)
-            --waves;
-        if (waves == 0)
-            return false;
-    }
-    const int threads = 64 * waves;
-    s.block = dim3(threads);
-    s.grid = dim3((unsigned)((a.P + threads - 1) / threads));
-    s.lds = per_wave * waves;
-    return true;
-}
-
-template <int MODEL, int K>
-static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
-{
-    LaunchShape s;
-    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
-        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
-        return HHMM_ERR_UNSUPPORTED;
-    }
-    const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
-    if (fwd_only)
-        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FWD>), s.grid, s.block, s.lds, st, a);
-    else if (a.outputs & extra)
-        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FULL>), s.grid, s.block, s.lds, st, a);
-    else
-        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA>), s.grid, s.block, s.lds, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error("fb_kernel launch: %s", hipGetErrorString(e));
-        return HHMM_ERR_HIP;
-    }
-    return HHMM_OK;
-}
-
-template <int MODEL, int K>
-static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
-{
-    LaunchShape s;
-    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
-        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
-        return HHMM_ERR_UNSUPPORTED;
-    }
-    hipLaunchKernelGGL((viterbi_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error("viterbi_kernel launch: %s", hipGetErrorString(e));
-        return HHMM_ERR_HIP;
-    }
-    return HHMM_OK;
-}
-
-template <int MODEL, int K>
-static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const hhmm_result *res,
-                               hipStream_t st)
-{
-    hhmm_status s = HHMM_OK;
-    const uint32_t out = a.outputs;
-    if (MODEL == HHMM_MODEL_TAYAL_LITE) {
-        /* in-sample forward: alpha_tk / unalpha_tk / loglik (hhmm-tayal2009-lite.stan:216-258) */
-        if (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) {
-            s = launch_fb<MODEL, K>(a, true, st);
-            if (s != HHMM_OK)
-                return s;
-        }
-        /* out-of-sample forward and Viterbi on (x_oos, sign_oos) (:260-324) */
-        DevArgs o = a;
-        o.Tmax = req->data.T_oos_max;
-        o.Tout = req->data.T_oos_max;
-        o.T = req->data.T_oos;
-        o.x = req->data.x_oos;
-        o.sign = req->data.sign_oos;
-        o.loglik = nullptr;
-        o.alpha = res->alpha_tk_oos;
-        o.unalpha = res->unalpha_tk_oos;
-        o.outputs = out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR);
-        if (out & HHMM_OUT_ALPHA_OOS)
-            o.outputs |= HHMM_OUT_ALPHA;
-        if (out & HHMM_OUT_UNALPHA_OOS)
-            o.outputs |= HHMM_OUT_UNALPHA;
-        if (o.outputs & (HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) {
-            s = launch_fb<MODEL, K>(o, true, st);
-            if (s != HHMM_OK)
-                return s;
-        }
-        if (o.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
-            s = launch_viterbi<MODEL, K>(o, st);
-        return s;
-    }
-    const bool any_fwd = (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA |
-                                 HHMM_OUT_UNBETA | HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) != 0;
-    if (any_fwd) {
-        s = launch_fb<MODEL, K>(a, !needs_backward(MODEL, out), st);
-        if (s != HHMM_OK)
-            return s;
-    }
-    if (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
-        s = launch_viterbi<MODEL, K>(a, st);
-    return s;
-}
-
-template <int MODEL>
-static hhmm_status run_model(const DevArgs &a, const hhmm_request *req, const hhmm_result *res,
-                             hipStream_t st)
-{
-    if constexpr (ModelTraits<MODEL>::kTayal) {
-        if (a.K != 4) {
-            set_error("the Tayal model is defined for K = 4 (got %d)", a.K);
-            return HHMM_ERR_INVALID_ARGUMENT;
-        }
-        return run_model_k<MODEL, 4>(a, req, res, st);
-    } else {
-        switch (a.K) {
-        case 1: return run_model_k<MODEL, 1>(a, req, res, st);
-        case 2: return run_model_k<MODEL, 2>(a, req, res, st);
-        case 3: return run_model_k<MODEL, 3>(a, req, res, st);
-        case 4: return run_model_k<MODEL, 4>(a, req, res, st);
-        case 5: return run_model_k<MODEL, 5>(a, req, res, st);
-        case 6: return run_model_k<MODEL, 6>(a, req, res, st);
-        case 7: return run_model_k<MODEL, 7>(a, req, res, st);
-        case 8: return run_model_k<MODEL, 8>(a, req, res, st);
-        default:
-            set_error("K = %d not supported (1..%d)", a.K, kMaxK);
-            return HHMM_ERR_UNSUPPORTED;
-        }
-    }
 }
 
 DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
@@ -1077,12 +183,14 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
         /* the OOS Viterbi is the only workspace user of tayal-lite */
         a.bp = (uint32_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
     }
+    const bool lo = a.K <= 4;
     switch (req->model) {
-    case HHMM_MODEL_HMM_GAUSS: return run_model<HHMM_MODEL_HMM_GAUSS>(a, req, res, st);
-    case HHMM_MODEL_HMM_MULTINOM: return run_model<HHMM_MODEL_HMM_MULTINOM>(a, req, res, st);
-    case HHMM_MODEL_HMM_MULTINOM_SEMISUP: return run_model<HHMM_MODEL_HMM_MULTINOM_SEMISUP>(a, req, res, st);
-    case HHMM_MODEL_TAYAL: return run_model<HHMM_MODEL_TAYAL>(a, req, res, st);
-    case HHMM_MODEL_TAYAL_LITE: return run_model<HHMM_MODEL_TAYAL_LITE>(a, req, res, st);
+    case HHMM_MODEL_HMM_GAUSS: return lo ? run_gauss_lo(a, req, res, st) : run_gauss_hi(a, req, res, st);
+    case HHMM_MODEL_HMM_MULTINOM: return lo ? run_multinom_lo(a, req, res, st) : run_multinom_hi(a, req, res, st);
+    case HHMM_MODEL_HMM_MULTINOM_SEMISUP:
+        return lo ? run_semisup_lo(a, req, res, st) : run_semisup_hi(a, req, res, st);
+    case HHMM_MODEL_TAYAL: return run_tayal(a, req, res, st);
+    case HHMM_MODEL_TAYAL_LITE: return run_tayal_lite(a, req, res, st);
     case HHMM_MODEL_IOHMM_REG:
     case HHMM_MODEL_IOHMM_MIX:
     case HHMM_MODEL_IOHMM_HMIX:
@@ -1098,7 +206,7 @@ hhmm_status selftest_cr_log(const double *in, double *out, int64_t n)
     double *din = nullptr, *dout = nullptr;
     const size_t bytes = (size_t)(n > 0 ? n : 1) * sizeof(double);
     if (hipMalloc(&din, bytes) != hipSuccess || hipMalloc(&dout, bytes) != hipSuccess) {
-        hipFree(din);
+        (void)hipFree(din);
         set_error("hipMalloc failed in selftest");
         return HHMM_ERR_OUT_OF_MEMORY;
     }
@@ -1109,8 +217,8 @@ hhmm_status selftest_cr_log(const double *in, double *out, int64_t n)
     }
     if (e == hipSuccess)
         e = hipMemcpy(out, dout, (size_t)n * sizeof(double), hipMemcpyDeviceToHost);
-    hipFree(din);
-    hipFree(dout);
+    (void)hipFree(din);
+    (void)hipFree(dout);
     if (e != hipSuccess) {
         set_error("selftest: %s", hipGetErrorString(e));
         return HHMM_ERR_HIP;

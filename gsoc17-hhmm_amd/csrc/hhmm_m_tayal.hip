@@ -1,0 +1,11 @@
+/* tayal2009/stan/hhmm-tayal2009.stan, K = 4..4: instantiates the HMM-family kernels of hhmm_hmm.h. */
+#include "hhmm_hmm.h"
+
+namespace hhmm {
+
+hhmm_status run_tayal(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st)
+{
+    return run_model_range<HHMM_MODEL_TAYAL, 4, 4>(a, req, res, st);
+}
+
+} // namespace hhmm

@@ -73,7 +73,7 @@ def _series_array(a, N, kind):
 class PreparedRequest:
     """A request plus the numpy buffers it points at (kept alive together)."""
 
-    def __init__(self, model, data, draws, pars, pairing="grid", device=-1):
+    def __init__(self, model, data, draws, pars, pairing="grid", device=-1, uniforms=None):
         if model not in _abi.MODELS:
             raise ValueError(f"unknown model {model!r}; one of {sorted(_abi.MODELS)}")
         self.model = model
@@ -152,6 +152,13 @@ class PreparedRequest:
             arr = self._alloc(dt, shape)
             self.out[name] = arr
             setattr(res, name, arr.ctypes.data)
+        if "z_ffbs" in self.pars:
+            if uniforms is None:
+                raise ValueError("z_ffbs (FFBS) needs uniforms of shape (P, T_max)")
+            uu = _f64(uniforms)
+            if uu.shape != (self.P, Tmax):
+                raise ValueError(f"uniforms must have shape {(self.P, Tmax)}, got {uu.shape}")
+            req.ffbs_u = self._ptr(uu)
         self.status = np.zeros(self.P, dtype=np.int32)
         res.pair_status = self.status.ctypes.data
         self.req, self.res = req, res
@@ -169,13 +176,15 @@ class PreparedRequest:
         return np.zeros(shape, dtype=np.int32, order="F")
 
 
-def gqs(model, data, draws, pars=None, pairing="grid", device=-1, lib=None, return_status=False):
+def gqs(model, data, draws, pars=None, pairing="grid", device=-1, lib=None, return_status=False, uniforms=None):
     """Evaluates the model's TP/GQ outputs for every (series, draw) pair on the GPU.
 
     Returns {name: array} with pair-major shapes (P, T, K) / (P, T) / (P,);
-    pair p = s + S*n under "grid" pairing (see reshape_pairs)."""
+    pair p = s + S*n under "grid" pairing (see reshape_pairs).  "z_ffbs" (a
+    forward-filtering backward-sampling draw) consumes the
+    caller's uniforms, shape (P, T_max), values in (0, 1)."""
     lib = lib or load_library()
-    pr = PreparedRequest(model, data, draws, pars, pairing, device)
+    pr = PreparedRequest(model, data, draws, pars, pairing, device, uniforms)
     st = lib.hhmm_run(C.byref(pr.req), C.byref(pr.res))
     if st < 0:
         raise HHMMError(st, lib.hhmm_last_error().decode())

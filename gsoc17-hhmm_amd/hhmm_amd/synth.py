@@ -259,6 +259,12 @@ def iohmm_mix(N=1, S=8, T=64, K=4, L=3, M=4, seed=SEED):
     return data, draws
 
 
+def ffbs_uniforms(P, T, seed=SEED):
+    """Caller-supplied FFBS uniforms in (0, 1), shape (P, T) (Philox stream 7)."""
+    u = rng(seed, 7).random((P, T))
+    return np.where(u > 0.0, u, 0.5)
+
+
 GENERATORS = {
     "hmm": hmm_gauss,
     "hmm-multinom": hmm_multinom,

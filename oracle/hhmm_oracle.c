@@ -252,6 +252,10 @@ typedef struct pair_ctx {
     double *unalpha_oos, *alpha_oos;
     double loglik, logp_zstar;
     int status;
+    /* FFBS (contract of §8 A14, see ffbs_contract below) */
+    double *ffbs_u;     /* [T] caller uniforms of this pair */
+    int32_t *zf;        /* [T] draws, 1-based (0 = undefined) */
+    double *ff;         /* [T*K] filter f_t */
 } pair_ctx;
 
 static void *xmalloc(size_t n)
@@ -308,6 +312,9 @@ static void ctx_alloc(pair_ctx *c, int K, int L, int M, int Tm, int Toos)
     c->oblik_t = xmalloc(sizeof(double) * TT);
     c->unalpha_oos = xmalloc(sizeof(double) * tk);
     c->alpha_oos = xmalloc(sizeof(double) * tk);
+    c->ffbs_u = xmalloc(sizeof(double) * TT);
+    c->zf = xmalloc(sizeof(int32_t) * TT);
+    c->ff = xmalloc(sizeof(double) * tk);
 }
 
 static void ctx_free(pair_ctx *c)
@@ -316,7 +323,7 @@ static void ctx_free(pair_ctx *c)
                     c->mu, c->sigma, c->w, c->b, c->sk, c->lambda, c->mukl, c->skl,
                     c->unalpha, c->alpha, c->unbeta, c->beta, c->ungamma, c->gamma, c->oblik,
                     c->Arow, c->logA, c->delta, c->acc, c->tmp, c->bp, c->zstar, c->oblik_t,
-                    c->unalpha_oos, c->alpha_oos};
+                    c->unalpha_oos, c->alpha_oos, c->ffbs_u, c->zf, c->ff};
     for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i)
         free(ptrs[i]);
 }
@@ -870,6 +877,162 @@ static void model_tayal_lite(pair_ctx *c)
 }
 
 /* ------------------------------------------------------------------ */
+/* FFBS -- forward filtering, backward sampling        */
+/* ------------------------------------------------------------------ */
+/*
+ * The reference has no FFBS: techreview/Rmd/hmm.Rmd:193-221 describes it in
+ * prose (z_T ~ alpha_T, then z_t | z_{t+1} ~ p(z_t | z_{t+1}, x_{1:t})) and
+ * stops at "= \dots" (:213).  This is the engine's CONTRACT, stated in the
+ * exact arithmetic the gfx950 kernels perform, so that draws are bit-exact
+ * given the caller's uniforms u[t] in (0, 1):
+ *
+ *   filter f_t (K-vector, linear space, renormalised each step):
+ *     e_t(j) = emission: phi_k[j, x_t] (multinomial / semisup / Tayal);
+ *              cr_exp(lpdf_j - m) with m = fmax over j (hmm.stan Gaussian);
+ *              cr_exp(oblik_t(j) - m), m = fmax over j (0 if -inf) (IOHMM)
+ *     f_0(j) = p_j * e_0(j); hmm.stan: p_j (Q2, the summed emission cancels);
+ *              Tayal: e_0(j) * p_j only where the init predicate holds, else e_0(j)
+ *     f_t(j) = s_t(j) * e_t(j), s_t(j) = f(0) A(0,j), then fma(f(i), A(i,j), s) for i = 1..K-1;
+ *              a masked transition (semisup g_t / Tayal sign_t, as in the model's
+ *              FORWARD pass) replaces s_t(j) by ((f(0) + f(1)) + ...) + f(K-1)
+ *     renorm: f <- ldexp(f, -E), E = frexp exponent of fmax_j f(j) (0 if 0/inf/NaN)
+ *   sampling, cat(w, u) = Stan's categorical_rng(w / sum w) with the caller's
+ *     uniform: sum = ((w0 + w1) + ...); theta_i = w_i / sum; b = 0, c = theta_0;
+ *     while (b < K-1 && u > c) c = c + theta_{++b};  draw b + 1
+ *     (0 and every earlier draw 0 if sum is not a positive finite number)
+ *     z_{T-1} = cat(f_{T-1}, u_{T-1});
+ *     z_t     = cat(w, u_t), w_i = f_t(i) * A(i, z_{t+1}), or w_i = f_t(i) where the
+ *               model's forward mask switches the transition off at (t+1, z_{t+1})
+ *   IOHMM (Q5: the transition K-vector A_t does not depend on the next state,
+ *     so f_t is proportional to e_t for t >= 1 and the draws decouple):
+ *     v_0 = p .* e_0, v_t = e_t (t >= 1); z_t = cat(v_t .* A_{t+1}, u_t); z_{T-1} = cat(v_{T-1}, u_{T-1}).
+ */
+static void ffbs_renorm(double *v, int K)
+{
+    double mx = v[0];
+    for (int k = 1; k < K; ++k)
+        mx = fmax(mx, v[k]);
+    int e = 0;
+    if (isfinite(mx) && mx != 0.0)
+        (void)frexp(mx, &e);
+    for (int k = 0; k < K; ++k)
+        v[k] = ldexp(v[k], -e);
+}
+
+static int ffbs_cat(const double *w, int K, double u)
+{
+    double sum = w[0];
+    for (int i = 1; i < K; ++i)
+        sum = sum + w[i];
+    if (!(sum > 0.0) || !isfinite(sum))
+        return 0;
+    int b = 0;
+    double cum = w[0] / sum;
+    while (b < K - 1 && u > cum) {
+        ++b;
+        cum = cum + w[b] / sum;
+    }
+    return b + 1;
+}
+
+/* e_t for the HMM family (discrete tables exact; Gaussian normalised by the max). */
+static void ffbs_emission_hmm(const pair_ctx *c, int gauss, const int32_t *x, int t, double *e)
+{
+    const int K = c->K;
+    if (gauss) {
+        double m = NEG_INF;
+        for (int j = 0; j < K; ++j) {
+            e[j] = stan_normal_lpdf(c->xr[t], c->mu[j], c->sigma[j]);
+            m = fmax(m, e[j]);
+        }
+        for (int j = 0; j < K; ++j)
+            e[j] = OR_EXP(e[j] - m);
+    } else {
+        for (int j = 0; j < K; ++j)
+            e[j] = PHI(j, x[t] - 1);
+    }
+}
+
+static int ffbs_mask(int model, const pair_ctx *c, int t, int j1)
+{
+    if (model == HHMM_MODEL_HMM_MULTINOM_SEMISUP)
+        return semisup_mask(c->g[t], j1);
+    if (model == HHMM_MODEL_TAYAL)
+        return tayal_pred(c->sgn[t], j1);
+    return 1;
+}
+
+static void ffbs_contract(pair_ctx *c, int model)
+{
+    const int K = c->K, T = c->T;
+    double *e = c->acc, *w = c->tmp;
+    const int iohmm = (model == HHMM_MODEL_IOHMM_REG || model == HHMM_MODEL_IOHMM_MIX ||
+                       model == HHMM_MODEL_IOHMM_HMIX);
+    if (iohmm) {
+        if (model == HHMM_MODEL_IOHMM_HMIX)
+            iohmm_transitions(c); /* the softmax values A_t (hmix keeps only their log) */
+        for (int t = 0; t < T; ++t) {
+            double m = TK(c->oblik, t, 0);
+            for (int k = 1; k < K; ++k)
+                m = fmax(m, TK(c->oblik, t, k));
+            if (m == NEG_INF)
+                m = 0.0;
+            for (int k = 0; k < K; ++k) {
+                e[k] = OR_EXP(TK(c->oblik, t, k) - m);
+                TK(c->ff, t, k) = (t == 0) ? c->p[k] * e[k] : e[k];
+            }
+        }
+        for (int t = 0; t < T; ++t) {
+            for (int i = 0; i < K; ++i)
+                w[i] = (t + 1 < T) ? TK(c->ff, t, i) * TK(c->Arow, t + 1, i) : TK(c->ff, t, i);
+            c->zf[t] = ffbs_cat(w, K, c->ffbs_u[t]);
+        }
+        return;
+    }
+    const int gauss = (model == HHMM_MODEL_HMM_GAUSS);
+    /* forward filter */
+    ffbs_emission_hmm(c, gauss, c->x, 0, e);
+    for (int j = 0; j < K; ++j) {
+        if (gauss)
+            TK(c->ff, 0, j) = c->p[j];
+        else if (model == HHMM_MODEL_TAYAL)
+            TK(c->ff, 0, j) = tayal_init_pred(c->sgn[0], j + 1) ? e[j] * c->p[j] : e[j];
+        else
+            TK(c->ff, 0, j) = c->p[j] * e[j];
+    }
+    ffbs_renorm(&TK(c->ff, 0, 0), K);
+    for (int t = 1; t < T; ++t) {
+        ffbs_emission_hmm(c, gauss, c->x, t, e);
+        const double *fp = &TK(c->ff, t - 1, 0);
+        double tot = fp[0];
+        for (int i = 1; i < K; ++i)
+            tot = tot + fp[i];
+        for (int j = 0; j < K; ++j) {
+            double s = fp[0] * c->A[0 * K + j];
+            for (int i = 1; i < K; ++i)
+                s = fma(fp[i], c->A[i * K + j], s);
+            if (!ffbs_mask(model, c, t, j + 1))
+                s = tot;
+            TK(c->ff, t, j) = s * e[j];
+        }
+        ffbs_renorm(&TK(c->ff, t, 0), K);
+    }
+    /* backward sampling */
+    c->zf[T - 1] = ffbs_cat(&TK(c->ff, T - 1, 0), K, c->ffbs_u[T - 1]);
+    for (int t = T - 2; t >= 0; --t) {
+        const int zn = c->zf[t + 1];
+        if (zn == 0) {
+            c->zf[t] = 0;
+            continue;
+        }
+        const int on = ffbs_mask(model, c, t + 1, zn);
+        for (int i = 0; i < K; ++i)
+            w[i] = on ? TK(c->ff, t, i) * c->A[i * K + (zn - 1)] : TK(c->ff, t, i);
+        c->zf[t] = ffbs_cat(w, K, c->ffbs_u[t]);
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* Batch driver                                                         */
 /* ------------------------------------------------------------------ */
 
@@ -896,6 +1059,11 @@ static void gather(pair_ctx *c, const hhmm_request *r, int64_t n, int64_t s)
         if (d->u)
             for (int m = 0; m < M; ++m)
                 c->u[(size_t)t * M + m] = d->u[(size_t)n + (size_t)N * ((size_t)t + (size_t)Tm * m)];
+    }
+    if (r->ffbs_u) {
+        const size_t P = (size_t)num_pairs(r), pp = (size_t)(r->pairing == HHMM_PAIR_ZIP ? n : s + S * n);
+        for (int t = 0; t < c->T; ++t)
+            c->ffbs_u[t] = r->ffbs_u[pp + P * (size_t)t];
     }
     for (int t = 0; t < c->T_oos; ++t) {
         const size_t ix = (size_t)n + (size_t)N * t;
@@ -969,6 +1137,9 @@ static void scatter(const pair_ctx *c, const hhmm_request *r, hhmm_result *o, in
                 for (int k = 0; k < K; ++k)
                     PTK(o->unalpha_tk_oos, t, k, To) = c->unalpha_oos[(size_t)t * K + k];
     }
+    if ((out & HHMM_OUT_FFBS) && o->z_ffbs)
+        for (int t = 0; t < T; ++t)
+            o->z_ffbs[(size_t)p + (size_t)P * t] = c->zf[t];
     if (o->pair_status)
         o->pair_status[p] = c->status;
 #undef PUT_TK
@@ -989,6 +1160,8 @@ static void run_pair(pair_ctx *c, const hhmm_request *r)
     case HHMM_MODEL_TAYAL_LITE: model_tayal_lite(c); break;
     default: break;
     }
+    if ((r->outputs & HHMM_OUT_FFBS) && r->ffbs_u)
+        ffbs_contract(c, r->model);
 }
 
 /* Runs pairs [p0, p1) of the request; nthreads <= 0 uses the OpenMP default.

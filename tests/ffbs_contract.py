@@ -1,0 +1,213 @@
+"""Independent pure-Python transcription of the engine's FFBS contract.
+
+TEST INFRASTRUCTURE ONLY.  The reference has no FFBS (techreview/Rmd/hmm.Rmd:193-221
+describes it in prose and stops at "= \\dots", :213), so the contract is the
+engine's own, written out in oracle/hhmm_oracle.c (ffbs_contract) and
+DESIGN.md.  This file restates it from that text, sharing no code with the C
+oracle: fma via exact rational arithmetic, transcendentals from Python's
+math (host libm), so it is compared bit-for-bit with the oracle's libm build.
+Emissions and IOHMM transitions come from the Stan transcription
+(tests/oracle_numpy.py).
+"""
+import math
+from fractions import Fraction
+
+import numpy as np
+
+import oracle_numpy as onp
+
+NINF = float("-inf")
+
+
+def fma(a, b, c):
+    """Exactly rounded a * b + c (finite arguments)."""
+    if not (math.isfinite(a) and math.isfinite(b) and math.isfinite(c)):
+        return a * b + c
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def fmax(a, b):
+    if math.isnan(a):
+        return b
+    if math.isnan(b):
+        return a
+    return a if a > b else b
+
+
+def renorm(v):
+    mx = v[0]
+    for a in v[1:]:
+        mx = fmax(mx, a)
+    e = 0
+    if math.isfinite(mx) and mx != 0.0:
+        e = math.frexp(mx)[1]
+    return [math.ldexp(a, -e) for a in v]
+
+
+def cat(w, u):
+    s = w[0]
+    for a in w[1:]:
+        s = s + a
+    if not (s > 0.0) or not math.isfinite(s):
+        return 0
+    b = 0
+    c = w[0] / s
+    while b < len(w) - 1 and u > c:
+        b += 1
+        c = c + w[b] / s
+    return b + 1
+
+
+def _semisup_on(g, j1):
+    return (g == 1 and j1 in (1, 4)) or (g == 2 and j1 in (2, 3))
+
+
+def _tayal_on(s, j1):
+    return (s == 1 and j1 in (2, 3)) or (s == 2 and j1 in (1, 4))
+
+
+def hmm_family(model, T, K, x, p, A, uu, phi=None, mu=None, sigma=None, aux=None):
+    """Draws z[0..T) (1-based) for hmm / hmm-multinom / semisup / tayal."""
+    def emission(t):
+        if model == "hmm":
+            lp = [onp.normal_lpdf(float(x[t]), float(mu[j]), float(sigma[j])) for j in range(K)]
+            m = NINF
+            for a in lp:
+                m = fmax(m, a)
+            return [math.exp(a - m) for a in lp]
+        return [float(phi[j][int(x[t]) - 1]) for j in range(K)]
+
+    def on(t, j1):
+        if model == "hmm-multinom-semisup":
+            return _semisup_on(int(aux[t]), j1)
+        if model == "hhmm-tayal2009":
+            return _tayal_on(int(aux[t]), j1)
+        return True
+
+    f = [None] * T
+    e = emission(0)
+    if model == "hmm":
+        f0 = [float(p[j]) for j in range(K)]
+    elif model == "hhmm-tayal2009":
+        f0 = [e[j] * float(p[j]) if ((aux[0] == 1 and j == 2) or (aux[0] == 2 and j == 0)) else e[j]
+              for j in range(K)]
+    else:
+        f0 = [float(p[j]) * e[j] for j in range(K)]
+    f[0] = renorm(f0)
+    for t in range(1, T):
+        e = emission(t)
+        fp = f[t - 1]
+        tot = fp[0]
+        for a in fp[1:]:
+            tot = tot + a
+        nf = []
+        for j in range(K):
+            s = fp[0] * float(A[0][j])
+            for i in range(1, K):
+                s = fma(fp[i], float(A[i][j]), s)
+            if not on(t, j + 1):
+                s = tot
+            nf.append(s * e[j])
+        f[t] = renorm(nf)
+    z = [0] * T
+    z[T - 1] = cat(f[T - 1], float(uu[T - 1]))
+    for t in range(T - 2, -1, -1):
+        zn = z[t + 1]
+        if zn == 0:
+            continue
+        o = on(t + 1, zn)
+        w = [f[t][i] * float(A[i][zn - 1]) if o else f[t][i] for i in range(K)]
+        z[t] = cat(w, float(uu[t]))
+    return z
+
+
+def iohmm(T, K, p, oblik, Arows, uu):
+    """Draws for the IOHMM programs; oblik[t][k], Arows[t][k] 0-based (Arows[0] = p filler)."""
+    v = []
+    for t in range(T):
+        m = oblik[t][0]
+        for a in oblik[t][1:]:
+            m = fmax(m, a)
+        if m == NINF:
+            m = 0.0
+        e = [math.exp(a - m) for a in oblik[t]]
+        v.append([float(p[k]) * e[k] for k in range(K)] if t == 0 else e)
+    z = []
+    for t in range(T):
+        w = [v[t][i] * Arows[t + 1][i] for i in range(K)] if t + 1 < T else v[t]
+        z.append(cat(w, float(uu[t])))
+    return z
+
+
+def run(model, data, draws, uniforms):
+    """z_ffbs per pair (GRID pairing, p = s + S*n), as lists of length T."""
+    xkey = "x_t" if model.startswith("iohmm") else "x"
+    x = np.atleast_2d(np.asarray(data[xkey]))
+    N, Tm = x.shape
+    S = next(np.asarray(v).shape[0] for v in draws.values())
+    Ts = np.asarray(data["T"]).reshape(N) if "T" in data else np.full(N, Tm)
+    K = int(data["K"])
+    rows = onp.run(model, data, draws) if model.startswith("iohmm") else None
+    out = []
+    for p in range(N * S):
+        n, s = p // S, p % S
+        T = int(Ts[n])
+        d = {k: np.asarray(v)[s] for k, v in draws.items()}
+        uu = np.asarray(uniforms)[p, :T]
+        if model.startswith("iohmm"):
+            u = np.asarray(data["u_tm"]).reshape(N, Tm, -1)[n, :T]
+            A, _ = onp._iohmm_common(T, K, int(data["M"]), [list(r) for r in u], d["w_km"], d["p_1k"], False)
+            ob = rows[p]["oblik_tk"]
+            out.append(iohmm(T, K, d["p_1k"], [list(map(float, r)) for r in ob], A[1:], uu))
+        elif model == "hhmm-tayal2009":
+            p1, A = onp.tayal_expand(float(d["p_11"]), d["A_row"])
+            out.append(hmm_family(model, T, K, x[n], p1, A, uu, phi=d["phi_k"], aux=np.asarray(data["sign"])[n]))
+        else:
+            aux = np.asarray(data["g"])[n] if "g" in data else None
+            out.append(hmm_family(model, T, K, x[n], d["p_1k"], d["A_ij"], uu, phi=d.get("phi_k"),
+                                  mu=d.get("mu_k"), sigma=d.get("sigma_k"), aux=aux))
+    return out
+
+
+def exact_marginals(model, T, K, x, p, A, phi=None, mu=None, sigma=None, aux=None, Arows=None, oblik=None):
+    """P(z_t = k) under the joint the contract samples from (numpy, normalised
+    forward-backward over the forward pass's factors), shape (T, K)."""
+    def fac(t):  # K x K transition factor of step t (rows: previous state)
+        if Arows is not None:
+            return np.tile(np.asarray(Arows[t], dtype=float)[:, None], (1, K))
+        F = np.array(A, dtype=float).copy()
+        for j in range(K):
+            if model == "hmm-multinom-semisup" and not _semisup_on(int(aux[t]), j + 1):
+                F[:, j] = 1.0
+            if model == "hhmm-tayal2009" and not _tayal_on(int(aux[t]), j + 1):
+                F[:, j] = 1.0
+        return F
+
+    def emis(t):
+        if oblik is not None:
+            o = np.asarray(oblik[t], dtype=float)
+            return np.exp(o - o.max())
+        if model == "hmm":
+            lp = np.array([onp.normal_lpdf(float(x[t]), float(mu[j]), float(sigma[j])) for j in range(K)])
+            return np.exp(lp - lp.max())
+        return np.array([float(phi[j][int(x[t]) - 1]) for j in range(K)])
+
+    e0 = emis(0)
+    if model == "hmm":
+        a0 = np.array(p, dtype=float)
+    elif model == "hhmm-tayal2009":
+        a0 = np.array([e0[j] * p[j] if ((aux[0] == 1 and j == 2) or (aux[0] == 2 and j == 0)) else e0[j]
+                       for j in range(K)])
+    else:
+        a0 = np.array(p, dtype=float) * e0
+    al = [a0 / a0.sum()]
+    for t in range(1, T):
+        a = (al[-1] @ fac(t)) * emis(t)
+        al.append(a / a.sum())
+    be = [None] * T
+    be[T - 1] = np.ones(K)
+    for t in range(T - 1, 0, -1):
+        b = fac(t) @ (emis(t) * be[t])
+        be[t - 1] = b / b.sum()
+    g = np.array([al[t] * be[t] for t in range(T)])
+    return g / g.sum(axis=1, keepdims=True)

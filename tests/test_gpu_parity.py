@@ -124,3 +124,34 @@ def test_deterministic_emissions_recover_path(engine):
     path = out["zstar_t"][0]
     assert path[0] == K
     assert np.array_equal(path[1:], z[1:])
+
+
+FFBS_MODELS = ["hmm", "hmm-multinom", "hmm-multinom-semisup", "hhmm-tayal2009", "iohmm-reg", "iohmm-mix",
+               "iohmm-hmix"]
+
+
+@pytest.mark.parametrize("model", FFBS_MODELS)
+@pytest.mark.parametrize("T", [1, 2, 37, 130])
+def test_ffbs_parity(engine, oracle, model, T):
+    """FFBS draws bit-exact with the oracle's contract given the same uniforms,
+    requested alone and together with every other output."""
+    import hhmm_amd
+    data, draws = synth.GENERATORS[model](N=3, S=70, T=T)
+    uu = synth.ffbs_uniforms(210, T, seed=T)
+    for pars in (["z_ffbs"], synth.PARS[model] + ["z_ffbs"]):
+        got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, uniforms=uu, return_status=True)
+        ref = oracle.gqs(model, data, draws, pars=pars, uniforms=uu, return_status=True)
+        compare_all(got, ref, pars)
+
+
+@pytest.mark.parametrize("model", ["hmm-multinom", "hhmm-tayal2009", "iohmm-hmix"])
+def test_ffbs_parity_ragged(engine, oracle, model):
+    import hhmm_amd
+    N, S, T = 5, 64, 90
+    data, draws = synth.GENERATORS[model](N=N, S=S, T=T)
+    data["T"] = np.array([90, 1, 17, 64, 33], dtype=np.int32)
+    uu = synth.ffbs_uniforms(N * S, T, seed=4)
+    pars = ["z_ffbs", "gamma_tk", "loglik"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, uniforms=uu)
+    ref = oracle.gqs(model, data, draws, pars=pars, uniforms=uu)
+    compare_all(got, ref, pars)
