@@ -844,7 +844,7 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
     const int nchunk = (Tw_max + CV - 1) / CV;
 
     /* delta_tk[1, K] = emission of j for j = 1..K: only column K is written,
-     * the others keep stanc's NaN (Q3, e.g. hmm-multinom.stan:236-237). */
+     * the others keep stanc's NaN (Q3, e.g. hmm-multinom.stan:105-106). */
     double dl[K];
     Obs cur[CV];
     load_chunk<MODEL, CV, VAUX>(cur, sp, 0);
@@ -960,13 +960,13 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
     hhmm_status s = HHMM_OK;
     const uint32_t out = a.outputs;
     if (MODEL == HHMM_MODEL_TAYAL_LITE) {
-        /* in-sample forward: alpha_tk / unalpha_tk / loglik (hhmm-tayal2009-lite.stan:216-258) */
+        /* in-sample forward: alpha_tk / unalpha_tk / loglik (hhmm-tayal2009-lite.stan:50-92) */
         if (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) {
             s = launch_fb<MODEL, K>(a, true, st);
             if (s != HHMM_OK)
                 return s;
         }
-        /* out-of-sample forward and Viterbi on (x_oos, sign_oos) (:260-324) */
+        /* out-of-sample forward and Viterbi on (x_oos, sign_oos) (:94-158) */
         DevArgs o = a;
         o.Tmax = req->data.T_oos_max;
         o.Tout = req->data.T_oos_max;

@@ -166,7 +166,7 @@ static double stan_max_vec(const double *d, int n)
 
 /* row_vector * vector = Eigen dot on x86-64 SSE2: two 2-wide partial sums
  * over blocks of 4, one more packet, horizontal add, scalar tail.
- * (iohmm-reg/stan/iohmm-reg.stan:183,192). */
+ * (iohmm-reg/stan/iohmm-reg.stan:45,54). */
 static double stan_dot(const double *a, const double *b, int n)
 {
     if (n < 2) {
@@ -566,7 +566,7 @@ static void model_hmm_multinom_semisup(pair_ctx *c)
 /* ------------------------------------------------------------------ */
 
 /* Transition TP: unA[1] = A[1] = p_1k (filler); A[t] = softmax(u_t' w_j)
- * (iohmm-reg.stan:178-187; iohmm-mix.stan:42-51).  Arow[t*K + i]. */
+ * (iohmm-reg.stan:40-49; iohmm-mix.stan:42-51).  Arow[t*K + i]. */
 static void iohmm_transitions(pair_ctx *c)
 {
     const int K = c->K, T = c->T, M = c->M;
@@ -580,7 +580,7 @@ static void iohmm_transitions(pair_ctx *c)
 }
 
 /* hmix: logA[1] = log(p_1k); logA[t] = log(softmax(u_t' w_j))
- * (iohmm-hmix.stan:232-244; lite :422-434). */
+ * (iohmm-hmix.stan:36-48; iohmm-hmix-lite.stan:32-44). */
 static void iohmm_log_transitions(pair_ctx *c)
 {
     const int K = c->K, T = c->T, M = c->M;
@@ -597,7 +597,7 @@ static void iohmm_log_transitions(pair_ctx *c)
 
 /* Gaussian-mixture emission: loglambda = log(lambda_kl);
  * oblik[t][j] = LSE_l(loglambda[j][l] + normal_lpdf(x_t | mu_kl, s_kl))
- * (iohmm-mix.stan:53-65; iohmm-hmix.stan:246-258). */
+ * (iohmm-mix.stan:53-65; iohmm-hmix.stan:50-62; iohmm-hmix-lite.stan:46-58). */
 static void iohmm_mixture_oblik(pair_ctx *c)
 {
     const int K = c->K, T = c->T, L = c->L;
@@ -632,7 +632,7 @@ static void iohmm_forward(pair_ctx *c, int use_logA_table)
 }
 
 /* Backward: acc[i] = unbeta[t, i] + logA_t(i) + oblik[t][i], the same for
- * every j (iohmm-reg.stan:218-240; iohmm-hmix.stan:281-304). */
+ * every j (iohmm-reg.stan:80-102; iohmm-hmix.stan:85-108). */
 static void iohmm_backward(pair_ctx *c, int use_logA_table)
 {
     const int K = c->K, T = c->T;
@@ -652,7 +652,7 @@ static void iohmm_backward(pair_ctx *c, int use_logA_table)
 }
 
 /* Viterbi: (delta + logA_t(i)) + oblik[t][j]; buggy init unless fixed_init
- * (iohmm-reg.stan:288-319; iohmm-hmix.stan:356-389 has the fixed init). */
+ * (iohmm-reg.stan:150-181; iohmm-hmix.stan:160-193 has the fixed init, :166-167). */
 static void iohmm_viterbi(pair_ctx *c, int use_logA_table, int fixed_init)
 {
     const int K = c->K, T = c->T;
@@ -683,18 +683,18 @@ static void iohmm_viterbi(pair_ctx *c, int use_logA_table, int fixed_init)
 static void model_iohmm_reg(pair_ctx *c)
 {
     const int K = c->K, T = c->T, M = c->M;
-    iohmm_transitions(c); /* :178-187 */
-    for (int t = 0; t < T; ++t) /* emission, :189-195 */
+    iohmm_transitions(c); /* :40-49 */
+    for (int t = 0; t < T; ++t) /* emission, :51-57 */
         for (int j = 0; j < K; ++j)
             TK(c->oblik, t, j) = stan_normal_lpdf(
                 c->xr[t], stan_dot(&c->u[(size_t)t * M], &c->b[(size_t)j * M], M), c->sk[j]);
-    iohmm_forward(c, 0);                                        /* :197-212 */
-    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :214-215 */
-    iohmm_backward(c, 0);                                       /* :218-236 */
-    gq_softmax_rows(c->unbeta, c->beta, T, K);                  /* :238-239 */
-    gq_gamma(c);                                                /* :242-248 */
-    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :258 (priors excluded) */
-    iohmm_viterbi(c, 0, 0);                                     /* :288-319 */
+    iohmm_forward(c, 0);                                        /* :59-75 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :76-77 */
+    iohmm_backward(c, 0);                                       /* :80-98 */
+    gq_softmax_rows(c->unbeta, c->beta, T, K);                  /* :100-101 */
+    gq_gamma(c);                                                /* :104-110 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :120 (priors excluded) */
+    iohmm_viterbi(c, 0, 0);                                     /* :150-181 */
 }
 
 /* iohmm-mix/stan/iohmm-mix.stan */
@@ -716,8 +716,8 @@ static void model_iohmm_mix(pair_ctx *c)
     iohmm_viterbi(c, 0, 0);                                     /* :164-195, log(A_ij) */
 }
 
-/* oblik_t[t] = log_sum_exp(log(alpha_tk[t]) + oblik_tk[t]) (iohmm-hmix.stan:314-317);
- * lite recomputes log(softmax(unalpha)) (iohmm-hmix-lite.stan:468-471, Q10). */
+/* oblik_t[t] = log_sum_exp(log(alpha_tk[t]) + oblik_tk[t]) (iohmm-hmix.stan:118-121);
+ * lite recomputes log(softmax(unalpha)) (iohmm-hmix-lite.stan:78-81, Q10). */
 static void iohmm_oblik_t(pair_ctx *c)
 {
     const int K = c->K, T = c->T;
@@ -732,34 +732,34 @@ static void iohmm_oblik_t(pair_ctx *c)
 static void model_iohmm_hmix(pair_ctx *c)
 {
     const int K = c->K, T = c->T;
-    iohmm_log_transitions(c);                                   /* :232-244 */
-    iohmm_mixture_oblik(c);                                     /* :246-258 */
-    iohmm_forward(c, 1);                                        /* :260-275 */
-    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :277-278 */
-    iohmm_backward(c, 1);                                       /* :281-300 */
-    gq_softmax_rows(c->unbeta, c->beta, T, K);                  /* :302-303 */
-    for (int t = 0; t < T; ++t) {                               /* :306-312 */
+    iohmm_log_transitions(c);                                   /* :36-48 */
+    iohmm_mixture_oblik(c);                                     /* :50-62 */
+    iohmm_forward(c, 1);                                        /* :64-79 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :81-82 */
+    iohmm_backward(c, 1);                                       /* :85-104 */
+    gq_softmax_rows(c->unbeta, c->beta, T, K);                  /* :106-107 */
+    for (int t = 0; t < T; ++t) {                               /* :110-116 */
         for (int k = 0; k < K; ++k)
             TK(c->ungamma, t, k) = TK(c->alpha, t, k) * TK(c->beta, t, k);
         const double s = stan_sum_vec(&TK(c->ungamma, t, 0), K);
         for (int k = 0; k < K; ++k)
             TK(c->gamma, t, k) = TK(c->ungamma, t, k) / s;
     }
-    iohmm_oblik_t(c);                                           /* :314-317 */
-    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :330 */
-    iohmm_viterbi(c, 1, 1);                                     /* :356-389 */
+    iohmm_oblik_t(c);                                           /* :118-121 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :134 */
+    iohmm_viterbi(c, 1, 1);                                     /* :160-193 */
 }
 
 /* iohmm-mix/stan/iohmm-hmix-lite.stan */
 static void model_iohmm_hmix_lite(pair_ctx *c)
 {
     const int K = c->K, T = c->T;
-    iohmm_log_transitions(c);                                   /* :422-434 */
-    iohmm_mixture_oblik(c);                                     /* :436-448 */
-    iohmm_forward(c, 1);                                        /* :450-466 */
-    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* softmax in :470 */
-    iohmm_oblik_t(c);                                           /* :468-471 */
-    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :484 */
+    iohmm_log_transitions(c);                                   /* :32-44 */
+    iohmm_mixture_oblik(c);                                     /* :46-58 */
+    iohmm_forward(c, 1);                                        /* :60-76 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* softmax in :80 */
+    iohmm_oblik_t(c);                                           /* :78-81 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :94 */
 }
 
 /* ------------------------------------------------------------------ */
@@ -816,7 +816,7 @@ static void tayal_forward(pair_ctx *c, const int32_t *x, const int32_t *sg, int 
         }
 }
 
-/* Tayal Viterbi over (x, sign) (hhmm-tayal2009.stan:130-165; lite :289-324). */
+/* Tayal Viterbi over (x, sign) (hhmm-tayal2009.stan:130-165; lite :123-158). */
 static void tayal_viterbi(pair_ctx *c, const int32_t *x, const int32_t *sg, int T)
 {
     const int K = c->K;
@@ -868,12 +868,12 @@ static void model_tayal(pair_ctx *c)
 static void model_tayal_lite(pair_ctx *c)
 {
     const int K = c->K, T = c->T;
-    tayal_forward(c, c->x, c->sgn, T, c->unalpha);              /* lite :216-240 */
-    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :244 */
-    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :255-258 */
-    tayal_forward(c, c->x_oos, c->sgn_oos, c->T_oos, c->unalpha_oos); /* :260-283 */
-    gq_softmax_rows(c->unalpha_oos, c->alpha_oos, c->T_oos, K);       /* :285-286 */
-    tayal_viterbi(c, c->x_oos, c->sgn_oos, c->T_oos);                 /* :289-324 */
+    tayal_forward(c, c->x, c->sgn, T, c->unalpha);              /* lite :50-74 */
+    c->loglik = stan_log_sum_exp(&TK(c->unalpha, T - 1, 0), K); /* :78 */
+    gq_softmax_rows(c->unalpha, c->alpha, T, K);                /* :89-92 */
+    tayal_forward(c, c->x_oos, c->sgn_oos, c->T_oos, c->unalpha_oos); /* :94-117 */
+    gq_softmax_rows(c->unalpha_oos, c->alpha_oos, c->T_oos, K);       /* :119-120 */
+    tayal_viterbi(c, c->x_oos, c->sgn_oos, c->T_oos);                 /* :123-158 */
 }
 
 /* ------------------------------------------------------------------ */

@@ -228,7 +228,7 @@ def hmm_multinom(T, K, x, p_1k, A_ij, phi_k, g=None):
         for j in range(1, K + 1):
             acc = []
             for i in range(1, K + 1):
-                if G is None:   # hmm-multinom.stan:170
+                if G is None:   # hmm-multinom.stan:39
                     a = unalpha[t - 1][i - 1] + log(A_ij[i - 1][j - 1]) + log(phi(j, X[t]))
                 else:           # hmm-multinom-semisup.stan:39-44
                     a = unalpha[t - 1][i - 1] + log(phi(j, X[t]))

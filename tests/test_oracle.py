@@ -168,7 +168,7 @@ def test_kat_tayal_masks(oracle):
 
 def test_kat_iohmm_backward_is_state_independent(oracle):
     """Q5: the IOHMM backward accumulator does not depend on j, so beta_tk is
-    uniform at every t (iohmm-reg.stan:228-234)."""
+    uniform at every t (iohmm-reg.stan:90-97)."""
     data, draws = synth.iohmm_reg(N=1, S=2, T=25, K=3)
     out = oracle.gqs("iohmm-reg", data, draws, pars=["beta_tk", "unbeta_tk"])
     assert np.allclose(out["beta_tk"], 1 / 3, rtol=1e-14)
