@@ -256,10 +256,13 @@ __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const 
     }
 }
 
-/* out = e_t .* (in M_t), with the model's transition masks; in may alias out. */
+/* out = e_t .* (in M_t), with the model's FORWARD transition masks (semisup
+ * g_t on the current state, hmm-multinom-semisup.stan:42-44; Tayal sign_t on
+ * the current state, hhmm-tayal2009.stan:62-64); no renormalisation.  in may
+ * alias out. */
 template <int MODEL, int K>
-__device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
-                                            const double (&e)[K], const Obs &o, int &ex)
+__device__ __forceinline__ void fwd_step_raw(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
+                                             const double (&e)[K], const Obs &o)
 {
     double s[K];
 #pragma unroll
@@ -288,6 +291,13 @@ __device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)
 #pragma unroll
     for (int j = 0; j < K; ++j)
         out[j] = s[j] * e[j];
+}
+
+template <int MODEL, int K>
+__device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
+                                            const double (&e)[K], const Obs &o, int &ex)
+{
+    fwd_step_raw<MODEL, K>(al, out, pp, e, o);
     renorm<K>(out, ex);
 }
 
@@ -431,7 +441,22 @@ __device__ __forceinline__ void emit_posteriors(const DevArgs &a, int64_t p, int
 #pragma unroll
         for (int k = 0; k < K; ++k)
             ug[k] = al[k] * be[k];
-        const double r = fast_rcp(vsum<K>(ug));
+        double sg = vsum<K>(ug);
+        double r;
+        if (__builtin_expect(sg > 0x1p-960, 1)) {
+            r = fast_rcp(sg);
+        } else {
+            /* alpha and beta nearly disjoint (e.g. the Tayal masks of Q6 on a
+             * long series): form the product from the normalised vectors as
+             * the reference does, so that its underflow to 0 (and gamma = NaN)
+             * happens where Stan's does */
+            const double ra = 1.0 / vsum<K>(al), rb = 1.0 / vsum<K>(be);
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                ug[k] = (al[k] * ra) * (be[k] * rb);
+            sg = vsum<K>(ug);
+            r = 1.0 / sg;
+        }
 #pragma unroll
         for (int k = 0; k < K; ++k)
             ug[k] = ug[k] * r;
@@ -482,8 +507,12 @@ struct FbLane {
     PairParams<MODEL, K> pp;
     const double2 *slab;
     int L;
-    int64_t p;
-    int Tp;
+    int64_t p;   /* output pair */
+    int t0;      /* first step of this lane's sweep (0, or a scan chunk's start) */
+    int Tp;      /* one past its last step */
+    int cb;      /* t0 / C: first checkpoint row */
+    int64_t q;   /* checkpoint column (the pair, or the scan lane) */
+    int64_t Qs;  /* checkpoint row stride */
 };
 
 /* One forward chunk [t0, t0+C).  FULLC: every lane of the wave has all C
@@ -512,9 +541,9 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
             } else if (u == 0) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    at(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)ln.p * 8u) = al[k];
+                    at(a.ckpt + ln.Qs * ((int64_t)(c - ln.cb) * K + k), (uint32_t)ln.q * 8u) = al[k];
                 if constexpr (fb_base(MODE) == FB_FULL)
-                    at(a.ckpt_ls + a.P * (int64_t)c, (uint32_t)ln.p * 8u) = lsc + kLn2 * ex;
+                    at(a.ckpt_ls + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 8u) = lsc + kLn2 * ex;
             }
         }
         ecur = enx;
@@ -603,7 +632,7 @@ __device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, 
                                         z, uu[u]);
                 at(a.z_ffbs + a.P * (int64_t)t, (uint32_t)ln.p * 4u) = z + 1;
             }
-            if (t > 0) {
+            if (t > ln.t0) {
                 if constexpr (fb_base(MODE) == FB_FULL)
                     blsc += ecur.m;
                 bwd_step<MODEL, K>(be, ln.pp, ecur.e, cur[u], bex);
@@ -613,44 +642,31 @@ __device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, 
     }
 }
 
-template <int MODEL, int K, int MODE>
-__global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
+/* The forward-backward sweep of one lane over [ln.t0, ln.Tp): a whole series
+ * (fb_kernel) or one T-chunk of the parallel scan (fb_scan_kernel, SURVEY §8
+ * A16), which enters with the boundary vectors the scan computed: al = the
+ * forward state f_{t0-1} (ignored at t0 = 0, where the model's init runs),
+ * be = beta at the chunk's last step, with their log scales. */
+template <int MODEL, int K, int MODE, bool SCAN>
+__device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K> &ln, const SeriesPtrs &sp,
+                                         double (&al)[K], double lsc, double (&be)[K], double blsc)
 {
     constexpr int C = fb_chunk(K);
     constexpr bool AUX = ModelTraits<MODEL>::kAux;
-    HIP_DYNAMIC_SHARED(double2, lds)
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    /* lanes past the last pair redo pair P-1 (identical values, benign
-     * duplicate stores): every lane stays in the wave-wide reductions */
-    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
-    int64_t n, d;
-    pair_coords(a, p, n, d);
-    constexpr int KP = (K + 1) / 2;
-
-    FbLane<MODEL, K> ln;
-    ln.p = p;
-    ln.L = a.L;
-    ln.Tp = pair_len(a, n);
-    ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
-    load_params<MODEL, K, false>(ln.pp, a, d);
-    if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
-    const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
+    const int64_t p = ln.p;
     const int Tw_min = wave_min(ln.Tp);
     const int Tw_max = wave_max(ln.Tp);
     const int nfull = Tw_min / C;              /* chunks complete for every lane */
     const int nchunk = (Tw_max + C - 1) / C;   /* chunks any lane needs */
+    const int cb = ln.cb;
 
     /* ---- forward sweep ---- */
-    double al[K];
-    double lsc = 0.0; /* log scale excluding the binary exponent */
     int ex = 0;       /* sum of binary exponents removed */
     Obs cur[C];
-    load_chunk<MODEL, C, AUX>(cur, sp, 0);
+    load_chunk<MODEL, C, AUX>(cur, sp, cb * C);
     Em<K> ecur;
-    emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, cur[0], ecur);
-    for (int c = 0; c < nchunk; ++c) {
+    emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, cur[0], ecur);
+    for (int c = cb; c < nchunk; ++c) {
         Obs nxt[C];
         load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C);
         if (c < nfull)
@@ -661,17 +677,12 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
         for (int u = 0; u < C; ++u)
             cur[u] = nxt[u];
     }
-    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+    if (!SCAN && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
         a.loglik[p] = log(vsum<K>(al)) + (lsc + kLn2 * ex);
     if constexpr (fb_base(MODE) == FB_FWD)
         return;
 
     /* ---- backward sweep, chunk by chunk from the end ---- */
-    double be[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        be[k] = 1.0;
-    double blsc = 0.0;
     int bex = 0;
     const int clast = nchunk - 1;
     load_chunk<MODEL, C, AUX>(cur, sp, clast * C);
@@ -679,12 +690,12 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
      * (unused) slots past its own last chunk, never past the allocation */
     double ck[K], ck_ls = 0.0;
     {
-        const int cc = clast;
+        const int cc = clast - cb;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            ck[k] = at(a.ckpt + a.P * ((int64_t)cc * K + k), (uint32_t)p * 8u);
+            ck[k] = at(a.ckpt + ln.Qs * ((int64_t)cc * K + k), (uint32_t)ln.q * 8u);
         if constexpr (fb_base(MODE) == FB_FULL)
-            ck_ls = at(a.ckpt_ls + a.P * (int64_t)cc, (uint32_t)p * 8u);
+            ck_ls = at(a.ckpt_ls + ln.Qs * (int64_t)cc, (uint32_t)ln.q * 8u);
     }
     /* FFBS: the caller's uniforms, prefetched one chunk ahead like the observations */
     double uu[fb_ffbs(MODE) ? C : 1], un[fb_ffbs(MODE) ? C : 1];
@@ -695,7 +706,7 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
     }
     Obs onext = cur[0];
     int z = -1;
-    for (int c = clast; c >= 0; --c) {
+    for (int c = clast; c >= cb; --c) {
         Obs nxt[C];
         load_chunk<MODEL, C, AUX>(nxt, sp, (c - 1) * C);
         if constexpr (fb_ffbs(MODE)) {
@@ -705,12 +716,12 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
         }
         double cn[K], cn_ls = 0.0;
         {
-            const int cc = max(c - 1, 0);
+            const int cc = max(c - 1, cb) - cb;
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                cn[k] = at(a.ckpt + a.P * ((int64_t)cc * K + k), (uint32_t)p * 8u);
+                cn[k] = at(a.ckpt + ln.Qs * ((int64_t)cc * K + k), (uint32_t)ln.q * 8u);
             if constexpr (fb_base(MODE) == FB_FULL)
-                cn_ls = at(a.ckpt_ls + a.P * (int64_t)cc, (uint32_t)p * 8u);
+                cn_ls = at(a.ckpt_ls + ln.Qs * (int64_t)cc, (uint32_t)ln.q * 8u);
         }
         if (c < nfull)
             bwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, ck, ck_ls, be, blsc, bex, uu, onext, z);
@@ -730,6 +741,42 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
             ck[k] = cn[k];
         ck_ls = cn_ls;
     }
+}
+
+template <int MODEL, int K, int MODE>
+__global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
+{
+    constexpr bool AUX = ModelTraits<MODEL>::kAux;
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    /* lanes past the last pair redo pair P-1 (identical values, benign
+     * duplicate stores): every lane stays in the wave-wide reductions */
+    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    constexpr int KP = (K + 1) / 2;
+
+    FbLane<MODEL, K> ln;
+    ln.p = p;
+    ln.L = a.L;
+    ln.t0 = 0;
+    ln.Tp = pair_len(a, n);
+    ln.cb = 0;
+    ln.q = p;
+    ln.Qs = a.P;
+    ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+    load_params<MODEL, K, false>(ln.pp, a, d);
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
+    const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
+    double al[K], be[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        al[k] = 0.0;
+        be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
+    }
+    fb_sweep<MODEL, K, MODE, false>(a, ln, sp, al, 0.0, be, 0.0);
 }
 
 /* ------------------------------------------------------------------ */
@@ -870,6 +917,579 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
 }
 
 
+/* ------------------------------------------------------------------ */
+/* Log-space forward-backward (the unalpha_tk / unbeta_tk profile)       */
+/* ------------------------------------------------------------------ */
+/*
+ * The log-scale outputs unalpha_tk / unbeta_tk keep finite values for states
+ * whose probability is below the double range relative to the others (Stan
+ * works in log space: e.g. hhmm-tayal2009.stan:93-119 keeps unbeta ~ -2400
+ * where the linear recursion's component underflows).  When either is
+ * requested the recursion runs in log space like the reference -- log A and
+ * log phi tabulated once per pair, Stan's log_sum_exp per (t, j) -- with the
+ * same checkpoint / recompute structure as fb_kernel.  Posteriors follow the
+ * reference's formulas: alpha = softmax(unalpha), beta = softmax(unbeta),
+ * ungamma = alpha .* beta, gamma = ungamma / sum (hmm.stan:60-63, 85-96).
+ */
+template <int K>
+__device__ __forceinline__ double stan_lse(const double (&x)[K])
+{
+    double mx = dev_ninf();
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        if (x[i] > mx)
+            mx = x[i];
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        if (x[i] != dev_ninf())
+            sum += exp(x[i] - mx);
+    return mx + log(sum);
+}
+
+template <int K>
+__device__ __forceinline__ void stan_softmax_v(const double (&v)[K], double (&th)[K])
+{
+    double mx = v[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i)
+        if (v[i] > mx)
+            mx = v[i];
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        th[i] = exp(v[i] - mx);
+        sum += th[i];
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        th[i] = th[i] / sum;
+}
+
+/* unalpha_1 (hmm.stan:29-30 with the Q2 summed emission; multinom :30-31;
+ * Tayal :49-54).  pp.A holds log A. */
+template <int MODEL, int K>
+__device__ __forceinline__ void fwd_log_init(double (&u)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
+                                             const Obs &o)
+{
+    if constexpr (ModelTraits<MODEL>::kGauss) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double z = (o.xr - pp.mu[k]) * pp.isig[k];
+            const double z2 = z * z;
+            s += HHMM_NEG_LOG_SQRT_TWO_PI;
+            s -= pp.lsig[k];
+            s += -0.5 * z2;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            u[k] = log(pp.p[k]) + s;
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if constexpr (ModelTraits<MODEL>::kTayal)
+                u[k] = tayal_init_pred(o.aux, k) ? le[k] + log(pp.p[k]) : le[k];
+            else
+                u[k] = log(pp.p[k]) + le[k];
+        }
+    }
+}
+
+/* unalpha_t(j) = LSE_i(acc_i) with the reference's accumulator
+ * (hmm.stan:37; semisup :39-44 and Tayal :60-64: transition under the mask). */
+template <int MODEL, int K>
+__device__ __forceinline__ void fwd_log_step(const double (&u)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
+                                             const double (&le)[K], const Obs &o)
+{
+    double nu[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double acc[K];
+        if constexpr (ModelTraits<MODEL>::kAux) {
+            bool on;
+            if constexpr (ModelTraits<MODEL>::kSemisup)
+                on = semisup_mask(o.aux, j);
+            else
+                on = tayal_pred(o.aux, j);
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                acc[i] = u[i] + le[j];
+                acc[i] = on ? acc[i] + pp.A[i][j] : acc[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                acc[i] = (u[i] + pp.A[i][j]) + le[j];
+        }
+        nu[j] = stan_lse<K>(acc);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        out[j] = nu[j];
+}
+
+/* unbeta_{t-1}(j) = LSE_i(acc_i): (unbeta_t(i) + log A(j,i)) + le_t(i)
+ * (hmm.stan:79; semisup unmasked :84); Tayal: unbeta + log phi, + log A(j,i)
+ * under the predicate on the PREVIOUS state j (hhmm-tayal2009.stan:107-111). */
+template <int MODEL, int K>
+__device__ __forceinline__ void bwd_log_step(double (&ub)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
+                                             const Obs &o)
+{
+    double nb[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double acc[K];
+        if constexpr (ModelTraits<MODEL>::kTayal) {
+            const bool on = tayal_pred(o.aux, j);
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                acc[i] = ub[i] + le[i];
+                acc[i] = on ? acc[i] + pp.A[j][i] : acc[i];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                acc[i] = (ub[i] + pp.A[j][i]) + le[i];
+        }
+        nb[j] = stan_lse<K>(acc);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        ub[j] = nb[j];
+}
+
+template <int K>
+__device__ __forceinline__ void emit_log_posteriors(const DevArgs &a, int64_t p, int t, const double (&u)[K],
+                                                    const double (&ub)[K], bool fwd_only)
+{
+    const uint32_t o = a.outputs;
+    double al[K], be[K];
+    stan_softmax_v<K>(u, al);
+    if ((o & HHMM_OUT_UNALPHA) && a.unalpha)
+        store_tk<K>(a.unalpha, a, p, t, u);
+    if ((o & HHMM_OUT_ALPHA) && a.alpha)
+        store_tk<K>(a.alpha, a, p, t, al);
+    if (fwd_only)
+        return;
+    stan_softmax_v<K>(ub, be);
+    if ((o & HHMM_OUT_UNBETA) && a.unbeta)
+        store_tk<K>(a.unbeta, a, p, t, ub);
+    if ((o & HHMM_OUT_BETA) && a.beta)
+        store_tk<K>(a.beta, a, p, t, be);
+    if (o & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
+        double ug[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ug[k] = al[k] * be[k];
+        if ((o & HHMM_OUT_UNGAMMA) && a.ungamma)
+            store_tk<K>(a.ungamma, a, p, t, ug);
+        if ((o & HHMM_OUT_GAMMA) && a.gamma) {
+            const double r = 1.0 / vsum<K>(ug);
+            double v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                v[k] = ug[k] * r;
+            store_tk<K>(a.gamma, a, p, t, v);
+        }
+    }
+}
+
+template <int MODEL, int K, bool FWDONLY>
+__global__ void __launch_bounds__(kBlock) fb_log_kernel(const DevArgs a)
+{
+    constexpr int C = fb_chunk(K);
+    constexpr bool AUX = ModelTraits<MODEL>::kAux;
+    constexpr int KP = (K + 1) / 2;
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+    PairParams<MODEL, K> pp;
+    load_params<MODEL, K, true>(pp, a, d);
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        fill_table<K, true>(slab, a, d);
+    const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
+    const int nchunk = (wave_max(Tp) + C - 1) / C;
+
+    double u[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        u[k] = 0.0;
+    Obs cur[C];
+    load_chunk<MODEL, C, AUX>(cur, sp, 0);
+    for (int c = 0; c < nchunk; ++c) {
+        Obs nxt[C];
+        load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C);
+#pragma unroll
+        for (int v = 0; v < C; ++v) {
+            const int t = c * C + v;
+            if (t < Tp) {
+                double le[K];
+                emit_log<MODEL, K>(pp, slab, a.L, cur[v], le);
+                if (t == 0)
+                    fwd_log_init<MODEL, K>(u, pp, le, cur[v]);
+                else
+                    fwd_log_step<MODEL, K>(u, u, pp, le, cur[v]);
+                if constexpr (FWDONLY) {
+                    emit_log_posteriors<K>(a, p, t, u, u, true);
+                } else if (v == 0) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        at(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)p * 8u) = u[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < C; ++v)
+            cur[v] = nxt[v];
+    }
+    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik) /* target += log_sum_exp(unalpha_tk[T]) */
+        a.loglik[p] = stan_lse<K>(u);
+    if constexpr (FWDONLY)
+        return;
+
+    double ub[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        ub[k] = 1.0; /* unbeta_tk[T, j] = 1 (Q1) */
+    for (int c = nchunk - 1; c >= 0; --c) {
+        load_chunk<MODEL, C, AUX>(cur, sp, c * C);
+        double abuf[C][K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            abuf[0][k] = at(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)p * 8u);
+#pragma unroll
+        for (int v = 1; v < C; ++v) {
+            if (c * C + v < Tp) {
+                double le[K];
+                emit_log<MODEL, K>(pp, slab, a.L, cur[v], le);
+                fwd_log_step<MODEL, K>(abuf[v - 1], abuf[v], pp, le, cur[v]);
+            }
+        }
+#pragma unroll
+        for (int v = C - 1; v >= 0; --v) {
+            const int t = c * C + v;
+            if (t < Tp) {
+                emit_log_posteriors<K>(a, p, t, abuf[v], ub, false);
+                if (t > 0) {
+                    double le[K];
+                    emit_log<MODEL, K>(pp, slab, a.L, cur[v], le);
+                    bwd_log_step<MODEL, K>(ub, pp, le, cur[v]);
+                }
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Parallel scan over T                                  */
+/* ------------------------------------------------------------------ */
+/*
+ * For long series with few pairs (C5: Tayal, T = 1e6).  The forward filter is
+ * linear: f_t = f_{t-1} F_t with F_t(i,j) = Abar_t(i,j) e_t(j), Abar = A with
+ * the columns the forward mask switches off set to 1; the backward pass is
+ * beta_{t-1} = B_t beta_t with B_t(j,i) = Abar'_t(j,i) e_t(i), Abar' = A with
+ * the ROWS the backward mask switches off set to 1 (Tayal, Q6; the other
+ * programs' backward passes are unmasked, Q7).  All entries are
+ * non-negative, so chunk products keep every entry's relative precision (no
+ * cancellation), like the sequential recursion.
+ *   phase 1  lane = (pair, T-chunk c): Pf_c = prod_{t in c} F_t and
+ *            Qb_c = prod_{t in c} B_t (chunk 0 starts from the model's init f_0,
+ *            so its row 0 is f at the chunk's end)
+ *   phase 2  lane = pair: f entering every chunk (a left scan over Pf), beta
+ *            at every chunk's last step (a right scan over Qb), loglik
+ *   phase 3  lane = (pair, T-chunk): fb_sweep over the chunk from those vectors
+ * Each product is renormalised by an exact power of two after every step;
+ * the exponents and the Gaussian log-scale sum of the chunk travel with it.
+ */
+
+/* Whole-matrix power-of-two renormalisation (max entry into [0.5, 1)). */
+template <int K>
+__device__ __forceinline__ void renorm_mat(double (&M)[K][K], int &ex)
+{
+    double mx = M[0][0];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            mx = fmax(mx, M[i][j]);
+    const int e = __builtin_amdgcn_frexp_exp(mx);
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            M[i][j] = ldexp(M[i][j], -e);
+    ex += e;
+}
+
+/* q <- q B_t for a row vector q: q'(i) = e(i) sum_j q(j) Abar'(j,i), with the
+ * model's BACKWARD mask (hhmm-tayal2009.stan:109-111: the predicate on the
+ * previous state j; unmasked otherwise). */
+template <int MODEL, int K>
+__device__ __forceinline__ void bwd_row_raw(double (&q)[K], const PairParams<MODEL, K> &pp, const double (&e)[K],
+                                            const Obs &o)
+{
+    double qon[K];
+    double qoff = 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        bool on = true;
+        if constexpr (ModelTraits<MODEL>::kTayal)
+            on = tayal_pred(o.aux, j);
+        qon[j] = on ? q[j] : 0.0;
+        qoff += on ? 0.0 : q[j];
+    }
+    double s[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double acc = qon[0] * pp.A[0][i];
+#pragma unroll
+        for (int j = 1; j < K; ++j)
+            acc = fma(qon[j], pp.A[j][i], acc);
+        s[i] = acc + qoff;
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        q[i] = s[i] * e[i];
+}
+
+/* Observation of step t (clamped, unconditional). */
+template <int MODEL, bool AUX>
+__device__ __forceinline__ Obs load_obs(const SeriesPtrs &sp, int t)
+{
+    Obs o[1];
+    load_chunk<MODEL, 1, AUX>(o, sp, t);
+    return o[0];
+}
+
+template <int MODEL, int K, bool BWD>
+__global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
+{
+    constexpr bool AUX = ModelTraits<MODEL>::kAux;
+    constexpr int KP = (K + 1) / 2;
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t G = a.P * (int64_t)a.scan_nc;
+    const int64_t g = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, G - 1);
+    const int64_t p = g % a.P;
+    const int c = (int)(g / a.P);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int t0 = c * a.scan_cl;
+    const int t1 = min(t0 + a.scan_cl, Tp);
+    PairParams<MODEL, K> pp;
+    load_params<MODEL, K, false>(pp, a, d);
+    const double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
+    const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
+
+    double F[K][K], Q[K][K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            F[i][j] = (i == j) ? 1.0 : 0.0;
+            Q[i][j] = F[i][j];
+        }
+    int fex = 0, qex = 0;
+    double lsc = 0.0;
+    int tb = t0;
+    if (c == 0) { /* chunk 0 enters from the model's init vector f_0 (every row) */
+        const Obs o0 = load_obs<MODEL, AUX>(sp, 0);
+        Em<K> em;
+        emit_prob<MODEL, K>(pp, slab, a.L, o0, em);
+        double f0[K];
+        fwd_init<MODEL, K>(f0, pp, em, o0, lsc, fex);
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                F[i][j] = f0[j];
+        tb = 1;
+    }
+    Obs onx = load_obs<MODEL, AUX>(sp, tb);
+    for (int t = tb; t < t1; ++t) {
+        const Obs o = onx;
+        onx = load_obs<MODEL, AUX>(sp, t + 1);
+        Em<K> em;
+        emit_prob<MODEL, K>(pp, slab, a.L, o, em);
+        lsc += em.m;
+#pragma unroll
+        for (int r = 0; r < K; ++r)
+            fwd_step_raw<MODEL, K>(F[r], F[r], pp, em.e, o);
+        renorm_mat<K>(F, fex);
+        if constexpr (BWD) {
+#pragma unroll
+            for (int r = 0; r < K; ++r)
+                bwd_row_raw<MODEL, K>(Q[r], pp, em.e, o);
+            renorm_mat<K>(Q, qex);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            at(a.sc_mf + a.P * ((int64_t)(c * K + i) * K + j), (uint32_t)p * 8u) = F[i][j];
+            if constexpr (BWD)
+                at(a.sc_qb + a.P * ((int64_t)(c * K + i) * K + j), (uint32_t)p * 8u) = Q[i][j];
+        }
+    at(a.sc_mx + a.P * (int64_t)(c * 3 + 0), (uint32_t)p * 8u) = (double)fex;
+    at(a.sc_mx + a.P * (int64_t)(c * 3 + 1), (uint32_t)p * 8u) = lsc;
+    at(a.sc_mx + a.P * (int64_t)(c * 3 + 2), (uint32_t)p * 8u) = (double)qex;
+}
+
+template <int K>
+__device__ __forceinline__ void load_mat(const double *base, const DevArgs &a, int c, int64_t p, double (&M)[K][K])
+{
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            M[i][j] = base[p + a.P * ((int64_t)(c * K + i) * K + j)];
+}
+
+/* Phase 2: one lane per pair scans its chunk products (matrices of the next
+ * chunk prefetched while the current one is applied). */
+template <int MODEL, int K, bool BWD>
+__global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
+{
+    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int ncp = (Tp + a.scan_cl - 1) / a.scan_cl;
+    auto mx = [&](int c, int f) { return a.sc_mx[p + a.P * (int64_t)(c * 3 + f)]; };
+
+    double f[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        f[j] = a.sc_mf[p + a.P * (int64_t)j];
+    double sc = mx(0, 1) + kLn2 * mx(0, 0);
+    double M[K][K], Mn[K][K];
+    load_mat<K>(a.sc_mf, a, min(1, ncp - 1), p, M);
+    for (int c = 1; c < ncp; ++c) {
+        load_mat<K>(a.sc_mf, a, min(c + 1, ncp - 1), p, Mn);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            a.sc_st[p + a.P * (int64_t)(c * K + k)] = f[k];
+        a.sc_sl[p + a.P * (int64_t)c] = sc;
+        double nf[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            double acc = f[0] * M[0][j];
+#pragma unroll
+            for (int i = 1; i < K; ++i)
+                acc = fma(f[i], M[i][j], acc);
+            nf[j] = acc;
+        }
+        int e2 = 0;
+        renorm<K>(nf, e2);
+        sc += mx(c, 1) + kLn2 * (mx(c, 0) + e2);
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            f[j] = nf[j];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                M[i][j] = Mn[i][j];
+    }
+    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+        a.loglik[p] = log(vsum<K>(f)) + sc;
+    if constexpr (BWD) {
+        double b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            b[k] = 1.0; /* unbeta_tk[T] = 1 (Q1) */
+            a.sc_be[p + a.P * (int64_t)((ncp - 1) * K + k)] = b[k];
+        }
+        a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = 0.0;
+        double bsc = 0.0;
+        load_mat<K>(a.sc_qb, a, ncp - 1, p, M);
+        for (int c = ncp - 1; c >= 1; --c) {
+            load_mat<K>(a.sc_qb, a, max(c - 1, 1), p, Mn);
+            double nb[K];
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                double acc = M[r][0] * b[0];
+#pragma unroll
+                for (int i = 1; i < K; ++i)
+                    acc = fma(M[r][i], b[i], acc);
+                nb[r] = acc;
+            }
+            int e2 = 0;
+            renorm<K>(nb, e2);
+            bsc += mx(c, 1) + kLn2 * (mx(c, 2) + e2);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                b[k] = nb[k];
+                a.sc_be[p + a.P * (int64_t)((c - 1) * K + k)] = b[k];
+            }
+            a.sc_bl[p + a.P * (int64_t)(c - 1)] = bsc;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    M[i][j] = Mn[i][j];
+        }
+    }
+}
+
+/* Phase 3: the forward-backward sweep of one (pair, T-chunk). */
+template <int MODEL, int K, int MODE>
+__global__ void __launch_bounds__(kBlock) fb_scan_kernel(const DevArgs a)
+{
+    constexpr bool AUX = ModelTraits<MODEL>::kAux;
+    constexpr int KP = (K + 1) / 2;
+    constexpr int C = fb_chunk(K);
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t G = a.P * (int64_t)a.scan_nc;
+    const int64_t g = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, G - 1);
+    const int64_t p = g % a.P;
+    const int c = (int)(g / a.P);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tpair = pair_len(a, n);
+    FbLane<MODEL, K> ln;
+    ln.p = p;
+    ln.L = a.L;
+    ln.t0 = c * a.scan_cl;
+    ln.Tp = max(min(ln.t0 + a.scan_cl, Tpair), ln.t0); /* chunks past the pair's end do nothing */
+    ln.cb = ln.t0 / C;
+    ln.q = g;
+    ln.Qs = G;
+    ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+    load_params<MODEL, K, false>(ln.pp, a, d);
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
+    const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
+    const bool live = ln.t0 < Tpair;
+    double al[K], be[K];
+    double lsa = 0.0, lsb = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        al[k] = (c > 0 && live) ? a.sc_st[p + a.P * (int64_t)(c * K + k)] : 0.0;
+        be[k] = 1.0;
+        if (fb_base(MODE) != FB_FWD && live)
+            be[k] = a.sc_be[p + a.P * (int64_t)(c * K + k)];
+    }
+    if (c > 0 && live)
+        lsa = a.sc_sl[p + a.P * (int64_t)c];
+    if (fb_base(MODE) != FB_FWD && live)
+        lsb = a.sc_bl[p + a.P * (int64_t)c];
+    fb_sweep<MODEL, K, MODE, true>(a, ln, sp, al, lsa, be, lsb);
+}
+
 static inline bool model_has_backward(int model)
 {
     return model == HHMM_MODEL_HMM_GAUSS || model == HHMM_MODEL_HMM_MULTINOM ||
@@ -918,7 +1538,23 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
     }
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     const bool ffbs = (a.outputs & HHMM_OUT_FFBS) != 0;
-    if (fwd_only)
+    if (a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) {
+        /* log-scale outputs: the log-space recursion; FFBS draws (if any)
+         * from the linear filter of the contract in a second launch */
+        DevArgs b = a;
+        b.outputs &= ~HHMM_OUT_FFBS;
+        if (fwd_only)
+            hipLaunchKernelGGL((fb_log_kernel<MODEL, K, true>), s.grid, s.block, s.lds, st, b);
+        else
+            hipLaunchKernelGGL((fb_log_kernel<MODEL, K, false>), s.grid, s.block, s.lds, st, b);
+        if (ffbs) {
+            DevArgs f = a;
+            f.outputs = HHMM_OUT_FFBS;
+            f.gamma = nullptr;
+            f.loglik = nullptr;
+            hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA | FB_FFBS>), s.grid, s.block, s.lds, st, f);
+        }
+    } else if (fwd_only)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FWD>), s.grid, s.block, s.lds, st, a);
     else if ((a.outputs & extra) && ffbs)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FULL | FB_FFBS>), s.grid, s.block, s.lds, st, a);
@@ -931,6 +1567,39 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("fb_kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+/* The forward-backward as a parallel scan over T (phases 1-3 above). */
+template <int MODEL, int K>
+static hhmm_status launch_fb_scan(const DevArgs &a, bool fwd_only, hipStream_t st)
+{
+    LaunchShape s;
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
+        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const int64_t G = a.P * (int64_t)a.scan_nc;
+    const dim3 gridG((unsigned)((G + s.block.x - 1) / s.block.x));
+    const dim3 gridP((unsigned)((a.P + 63) / 64));
+    const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
+    if (fwd_only) {
+        hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, false>), gridG, s.block, s.lds, st, a);
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), gridP, dim3(64), 0, st, a);
+        hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG, s.block, s.lds, st, a);
+    } else {
+        hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, true>), gridG, s.block, s.lds, st, a);
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), gridP, dim3(64), 0, st, a);
+        if (a.outputs & extra)
+            hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG, s.block, s.lds, st, a);
+        else
+            hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_GAMMA>), gridG, s.block, s.lds, st, a);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("scan launch: %s", hipGetErrorString(e));
         return HHMM_ERR_HIP;
     }
     return HHMM_OK;
@@ -993,7 +1662,10 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
     const bool any_fwd = (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA |
                                  HHMM_OUT_UNBETA | HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA | HHMM_OUT_FFBS)) != 0;
     if (any_fwd) {
-        s = launch_fb<MODEL, K>(a, !needs_backward(MODEL, out), st);
+        if (a.scan_cl > 0 && !(out & HHMM_OUT_FFBS))
+            s = launch_fb_scan<MODEL, K>(a, !needs_backward(MODEL, out), st);
+        else
+            s = launch_fb<MODEL, K>(a, !needs_backward(MODEL, out), st);
         if (s != HHMM_OK)
             return s;
     }

@@ -50,7 +50,24 @@ struct DevArgs {
     double *ckpt_ls;    /* [nchunk][P]    log scale at each checkpoint */
     uint32_t *bp;       /* [nword][P]     packed Viterbi back-pointers */
     double *lam;        /* [Tmax][P]      IOHMM: running sum of log c_t (unbeta pass) */
+    /* parallel scan over T; scan_cl = 0: sequential sweeps */
+    int32_t scan_cl;    /* steps per T-chunk (multiple of fb_chunk(K)) */
+    int32_t scan_nc;    /* T-chunks per pair (of T_max) */
+    double *sc_mf;      /* [nc][K][K][P] forward chunk products (chunk 0: row 0 = f at its end) */
+    double *sc_qb;      /* [nc][K][K][P] backward chunk products */
+    double *sc_mx;      /* [nc][3][P]    per chunk: forward exponent, log scale, backward exponent */
+    double *sc_st;      /* [nc][K][P]    forward state entering each chunk */
+    double *sc_sl;      /* [nc][P]       its log scale */
+    double *sc_be;      /* [nc][K][P]    beta at each chunk's last step */
+    double *sc_bl;      /* [nc][P]       its log scale */
 };
+
+/* Parallel-scan plan of one request: T-chunk length and count (cl = 0: off). */
+struct ScanPlan {
+    int cl;
+    int nc;
+};
+ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint32_t flags);
 
 /* Time steps between forward checkpoints kept for the backward sweep. */
 constexpr int fb_chunk(int K) { return K <= 4 ? 8 : 4; }
@@ -64,10 +81,10 @@ constexpr int kBlock = 256;
 constexpr size_t kLdsLimit = 160 * 1024;
 
 /* Bytes of workspace the kernels need for this launch shape. */
-size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs);
+size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags);
 
 /* Carves the workspace into DevArgs pointers. */
-void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos);
+void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags);
 
 /* Launches every kernel the request needs on `stream` (device pointers). */
 hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws,

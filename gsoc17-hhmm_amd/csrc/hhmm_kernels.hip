@@ -82,42 +82,111 @@ static int nword_of(int K, int T) { return T / bp_steps_per_word(K) + 1; }
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs)
+/* Parallel scan over T for the HMM-family forward-backward:
+ * used when a batch has too few pairs to fill the chip with one lane per
+ * pair.  The T-chunk length targets ~512k (pair, chunk) lanes. */
+ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint32_t flags)
 {
-    size_t bytes = 0;
-    if (needs_ckpt(model, outputs)) {
-        bytes += align256((size_t)nchunk_of(K, Tmax) * K * P * sizeof(double));
-        bytes += align256((size_t)nchunk_of(K, Tmax) * P * sizeof(double));
+    ScanPlan sp{0, 0};
+    const bool family = model == HHMM_MODEL_HMM_GAUSS || model == HHMM_MODEL_HMM_MULTINOM ||
+                        model == HHMM_MODEL_HMM_MULTINOM_SEMISUP || model == HHMM_MODEL_TAYAL;
+    const uint32_t fb_out = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
+                            HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
+    /* the log-scale outputs run the sequential log-space recursion (hhmm_hmm.h) */
+    if (!family || (flags & HHMM_FLAG_SCAN_OFF) || (outputs & (HHMM_OUT_FFBS | HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) ||
+        !(outputs & fb_out))
+        return sp;
+    const int C = fb_chunk(K);
+    const int log2cl = (int)((flags >> 8) & 0xffu);
+    int cl;
+    if (log2cl > 0) {
+        cl = 1 << log2cl;
+    } else {
+        const int64_t want = (int64_t)Tmax * P / 524288;
+        cl = 8 * C;
+        while (cl < want && cl < 65536)
+            cl *= 2;
+    }
+    if (cl < C)
+        cl = C;
+    cl -= cl % C;
+    const int nc = (Tmax + cl - 1) / cl;
+    if (!(flags & HHMM_FLAG_SCAN_FORCE) && (P >= 131072 || Tmax < 16384 || nc < 4))
+        return sp;
+    if ((int64_t)P * nc >= (int64_t(1) << 29)) /* checkpoint columns are 32-bit byte offsets */
+        return sp;
+    sp.cl = cl;
+    sp.nc = nc;
+    return sp;
+}
+
+/* Offsets of every workspace region (SIZE_MAX = unused) and the total. */
+struct WsLayout {
+    size_t ckpt, ckpt_ls, bp, lam, mf, qb, mx, st, sl, be, bl, total;
+    ScanPlan sp;
+};
+
+static WsLayout ws_layout(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
+{
+    WsLayout w;
+    const size_t NONE = SIZE_MAX;
+    w.ckpt = w.ckpt_ls = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align256(bytes);
+        return o;
+    };
+    const size_t d = sizeof(double);
+    w.sp = scan_plan(model, K, Tmax, P, outputs, flags);
+    if (w.sp.cl > 0) {
+        const size_t nc = (size_t)w.sp.nc, G = (size_t)P * nc, rows = (size_t)(w.sp.cl / fb_chunk(K));
+        w.ckpt = take(rows * K * G * d);
+        w.ckpt_ls = take(rows * G * d);
+        w.mf = take(nc * K * K * P * d);
+        w.qb = take(nc * K * K * P * d);
+        w.mx = take(nc * 3 * P * d);
+        w.st = take(nc * K * P * d);
+        w.sl = take(nc * P * d);
+        w.be = take(nc * K * P * d);
+        w.bl = take(nc * P * d);
+    } else if (needs_ckpt(model, outputs)) {
+        w.ckpt = take((size_t)nchunk_of(K, Tmax) * K * P * d);
+        w.ckpt_ls = take((size_t)nchunk_of(K, Tmax) * P * d);
     }
     if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
         const int Tv = (model == HHMM_MODEL_TAYAL_LITE) ? Toos : Tmax;
-        bytes += align256((size_t)nword_of(K, Tv) * P * sizeof(uint32_t));
+        w.bp = take((size_t)nword_of(K, Tv) * P * sizeof(uint32_t));
     }
     if (is_iohmm_model(model) && (outputs & HHMM_OUT_UNBETA))
-        bytes += align256((size_t)Tmax * P * sizeof(double));
-    return bytes + 256;
+        w.lam = take((size_t)Tmax * P * d);
+    w.total = off + 256;
+    return w;
 }
 
-void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos)
+size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
+{
+    return ws_layout(model, K, Tmax, Toos, P, outputs, flags).total;
+}
+
+void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
 {
     char *b = (char *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
-    a.ckpt = nullptr;
-    a.ckpt_ls = nullptr;
-    a.bp = nullptr;
-    if (needs_ckpt(a.model, a.outputs)) {
-        a.ckpt = (double *)b;
-        b += align256((size_t)nchunk_of(a.K, Tmax) * a.K * a.P * sizeof(double));
-        a.ckpt_ls = (double *)b;
-        b += align256((size_t)nchunk_of(a.K, Tmax) * a.P * sizeof(double));
-    }
-    a.lam = nullptr;
-    if (a.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
-        a.bp = (uint32_t *)b;
-        b += align256((size_t)nword_of(a.K, a.model == HHMM_MODEL_TAYAL_LITE ? Toos : Tmax) * a.P *
-                      sizeof(uint32_t));
-    }
-    if (is_iohmm_model(a.model) && (a.outputs & HHMM_OUT_UNBETA))
-        a.lam = (double *)b;
+    const WsLayout w = ws_layout(a.model, a.K, Tmax, Toos, a.P, a.outputs, flags);
+    auto at_off = [&](size_t o) -> void * { return o == SIZE_MAX ? nullptr : (void *)(b + o); };
+    a.ckpt = (double *)at_off(w.ckpt);
+    a.ckpt_ls = (double *)at_off(w.ckpt_ls);
+    a.bp = (uint32_t *)at_off(w.bp);
+    a.lam = (double *)at_off(w.lam);
+    a.scan_cl = w.sp.cl;
+    a.scan_nc = w.sp.nc;
+    a.sc_mf = (double *)at_off(w.mf);
+    a.sc_qb = (double *)at_off(w.qb);
+    a.sc_mx = (double *)at_off(w.mx);
+    a.sc_st = (double *)at_off(w.st);
+    a.sc_sl = (double *)at_off(w.sl);
+    a.sc_be = (double *)at_off(w.be);
+    a.sc_bl = (double *)at_off(w.bl);
 }
 
 DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
@@ -178,11 +247,7 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
                        hipStream_t st)
 {
     DevArgs a = make_args(req, res, P);
-    bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max);
-    if (req->model == HHMM_MODEL_TAYAL_LITE && (req->outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))) {
-        /* the OOS Viterbi is the only workspace user of tayal-lite */
-        a.bp = (uint32_t *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
-    }
+    bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max, (uint32_t)req->flags);
     const bool lo = a.K <= 4;
     switch (req->model) {
     case HHMM_MODEL_HMM_GAUSS: return lo ? run_gauss_lo(a, req, res, st) : run_gauss_hi(a, req, res, st);

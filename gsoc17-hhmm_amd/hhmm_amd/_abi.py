@@ -34,6 +34,16 @@ MODELS = {
 PAIR_GRID = 0
 PAIR_ZIP = 1
 
+# hhmm_request.flags
+FLAG_SCAN_AUTO = 0
+FLAG_SCAN_FORCE = 1 << 0
+FLAG_SCAN_OFF = 1 << 1
+
+
+def flag_scan_chunk_log2(n):
+    """T-chunk length 2^n for the parallel scan (HHMM_FLAG_SCAN_CHUNK_LOG2)."""
+    return int(n) << 8
+
 OUT = {
     "loglik": 1 << 0,
     "unalpha_tk": 1 << 1,
@@ -107,7 +117,7 @@ class Request(C.Structure):
         ("draws", Draws),
         ("ffbs_u", C.c_void_p),
         ("device", C.c_int32),
-        ("reserved", C.c_int32),
+        ("flags", C.c_int32),
     ]
 
 

@@ -73,7 +73,7 @@ def _series_array(a, N, kind):
 class PreparedRequest:
     """A request plus the numpy buffers it points at (kept alive together)."""
 
-    def __init__(self, model, data, draws, pars, pairing="grid", device=-1, uniforms=None):
+    def __init__(self, model, data, draws, pars, pairing="grid", device=-1, uniforms=None, flags=0):
         if model not in _abi.MODELS:
             raise ValueError(f"unknown model {model!r}; one of {sorted(_abi.MODELS)}")
         self.model = model
@@ -83,6 +83,7 @@ class PreparedRequest:
         req.model = _abi.MODELS[model]
         req.pairing = {"grid": _abi.PAIR_GRID, "zip": _abi.PAIR_ZIP}[pairing]
         req.device = device
+        req.flags = int(flags)
 
         xkey = "x_t" if model.startswith("iohmm") else "x"
         x = np.asarray(data[xkey])
@@ -176,15 +177,17 @@ class PreparedRequest:
         return np.zeros(shape, dtype=np.int32, order="F")
 
 
-def gqs(model, data, draws, pars=None, pairing="grid", device=-1, lib=None, return_status=False, uniforms=None):
+def gqs(model, data, draws, pars=None, pairing="grid", device=-1, lib=None, return_status=False, uniforms=None,
+        flags=0):
     """Evaluates the model's TP/GQ outputs for every (series, draw) pair on the GPU.
 
     Returns {name: array} with pair-major shapes (P, T, K) / (P, T) / (P,);
     pair p = s + S*n under "grid" pairing (see reshape_pairs).  "z_ffbs" (a
     forward-filtering backward-sampling draw) consumes the
-    caller's uniforms, shape (P, T_max), values in (0, 1)."""
+    caller's uniforms, shape (P, T_max), values in (0, 1).  `flags`: HHMM_FLAG_*
+    (e.g. force / forbid the parallel scan over T, _abi.FLAG_SCAN_*)."""
     lib = lib or load_library()
-    pr = PreparedRequest(model, data, draws, pars, pairing, device, uniforms)
+    pr = PreparedRequest(model, data, draws, pars, pairing, device, uniforms, flags)
     st = lib.hhmm_run(C.byref(pr.req), C.byref(pr.res))
     if st < 0:
         raise HHMMError(st, lib.hhmm_last_error().decode())

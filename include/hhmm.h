@@ -149,6 +149,16 @@ typedef struct hhmm_draws {
     const double *A_row;       /* [S, 2, 2] tayal A_row[r][c] at s + S*(r + 2*c) */
 } hhmm_draws;
 
+/* Request flags (hhmm_request.flags).  Forward/backward over long series with
+ * few pairs runs as a parallel scan over T (T-chunks per pair: chunk transfer
+ * products, a scan over chunk boundaries, then per-chunk sweeps).  AUTO picks
+ * it when the batch has too few pairs to fill the GPU; FFBS always runs
+ * sequentially (the draws chain across the whole series). */
+#define HHMM_FLAG_SCAN_AUTO 0u
+#define HHMM_FLAG_SCAN_FORCE (1u << 0)
+#define HHMM_FLAG_SCAN_OFF (1u << 1)
+#define HHMM_FLAG_SCAN_CHUNK_LOG2(n) ((uint32_t)(n) << 8) /* T-chunk length 2^n (0 = automatic) */
+
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */
     int32_t model;             /* hhmm_model */
@@ -158,7 +168,7 @@ typedef struct hhmm_request {
     hhmm_draws draws;
     const double *ffbs_u;      /* [P, T_max] uniforms in (0,1) for HHMM_OUT_FFBS */
     int32_t device;            /* HIP device ordinal for hhmm_run; -1 = current */
-    int32_t reserved;
+    int32_t flags;             /* HHMM_FLAG_* (0 = defaults) */
 } hhmm_request;
 
 /* Caller-allocated outputs; a pointer may be NULL when its bit is not requested. */

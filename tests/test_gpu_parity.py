@@ -155,3 +155,12 @@ def test_ffbs_parity_ragged(engine, oracle, model):
     got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, uniforms=uu)
     ref = oracle.gqs(model, data, draws, pars=pars, uniforms=uu)
     compare_all(got, ref, pars)
+
+
+@pytest.mark.parametrize("model", DEVICE_MODELS)
+def test_parity_long_full_profile(engine, oracle, model):
+    """Every declared output at T = 1000: log-scale outputs (unalpha / unbeta)
+    of states far below the others stay finite, as in Stan's log space."""
+    data, draws = synth.GENERATORS[model](N=2, S=40, T=1000)
+    got, ref = run_both(engine, oracle, model, data, draws, synth.PARS[model])
+    compare_all(got, ref, synth.PARS[model] + ["pair_status"])
