@@ -442,7 +442,7 @@ hhmm_status hhmm_workspace_size(const hhmm_request *req, size_t *bytes)
         set_error("request describes no pairs");
         return HHMM_ERR_INVALID_ARGUMENT;
     }
-    *bytes = workspace_bytes(req->model, req->data.K, req->data.T_max, req->data.T_oos_max, P, req->outputs,
+    *bytes = workspace_bytes(req->model, req->data.K, req->data.L, req->data.T_max, req->data.T_oos_max, P, req->outputs,
                             (uint32_t)req->flags);
     return HHMM_OK;
 }
@@ -533,7 +533,7 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
     (void)hipMemset(dstatus, 0, (size_t)P * sizeof(int32_t));
     dres.pair_status = (int32_t *)dstatus;
 
-    size_t wsb = workspace_bytes(req->model, req->data.K, req->data.T_max, req->data.T_oos_max, P, req->outputs,
+    size_t wsb = workspace_bytes(req->model, req->data.K, req->data.L, req->data.T_max, req->data.T_oos_max, P, req->outputs,
                                  (uint32_t)req->flags);
     void *ws = pool_get(dev, wsb);
     if (!ws) {

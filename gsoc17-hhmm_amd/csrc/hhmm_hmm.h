@@ -400,10 +400,14 @@ enum FbMode {
     FB_GAMMA = 0, /* loglik + gamma_tk: the hot path, no per-output branches */
     FB_FULL = 1,  /* any mix of alpha/beta/unalpha/unbeta/ungamma/gamma (+ per-step log scale) */
     FB_FWD = 2,   /* forward only: loglik / alpha / unalpha (tayal-lite, no backward output) */
-    FB_FFBS = 4   /* flag: FFBS draws in the backward sweep */
+    FB_FFBS = 4,  /* flag: FFBS draws in the backward sweep */
+    FB_PACK = 8   /* flag: the forward sweep packs each chunk's symbols (4 bits, L <= 16)
+                   * into the checkpoint record; the backward sweep reads those
+                   * instead of re-reading x (hmm-multinom: 4 B -> 1 B per step) */
 };
 constexpr int fb_base(int mode) { return mode & 3; }
 constexpr bool fb_ffbs(int mode) { return (mode & FB_FFBS) != 0; }
+constexpr bool fb_pack(int mode) { return (mode & FB_PACK) != 0; }
 
 
 /* Writes the forward-side outputs of step t (alpha, unalpha). */
@@ -544,6 +548,13 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
                     at(a.ckpt + ln.Qs * ((int64_t)(c - ln.cb) * K + k), (uint32_t)ln.q * 8u) = al[k];
                 if constexpr (fb_base(MODE) == FB_FULL)
                     at(a.ckpt_ls + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 8u) = lsc + kLn2 * ex;
+                if constexpr (fb_pack(MODE)) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int v = 0; v < C; ++v)
+                        w |= ((uint32_t)(cur[v].x - 1) & 15u) << (4 * v);
+                    at(a.xpk + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 4u) = w;
+                }
             }
         }
         ecur = enx;
@@ -685,7 +696,21 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     /* ---- backward sweep, chunk by chunk from the end ---- */
     int bex = 0;
     const int clast = nchunk - 1;
-    load_chunk<MODEL, C, AUX>(cur, sp, clast * C);
+    /* observations of chunk cc: x itself, or the packed record of the forward sweep */
+    auto obs_chunk = [&](Obs (&dst)[C], int cc) {
+        if constexpr (fb_pack(MODE)) {
+            const uint32_t w = at(a.xpk + ln.Qs * (int64_t)(max(cc, cb) - cb), (uint32_t)ln.q * 4u);
+#pragma unroll
+            for (int v = 0; v < C; ++v) {
+                dst[v].x = (int)((w >> (4 * v)) & 15u) + 1;
+                dst[v].aux = 0;
+                dst[v].xr = 0.0;
+            }
+        } else {
+            load_chunk<MODEL, C, AUX>(dst, sp, cc * C);
+        }
+    };
+    obs_chunk(cur, clast);
     /* checkpoint rows are wave-uniform: a lane shorter than the wave reads
      * (unused) slots past its own last chunk, never past the allocation */
     double ck[K], ck_ls = 0.0;
@@ -708,7 +733,7 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     int z = -1;
     for (int c = clast; c >= cb; --c) {
         Obs nxt[C];
-        load_chunk<MODEL, C, AUX>(nxt, sp, (c - 1) * C);
+        obs_chunk(nxt, c - 1);
         if constexpr (fb_ffbs(MODE)) {
 #pragma unroll
             for (int u = 0; u < C; ++u)
@@ -800,7 +825,14 @@ __device__ __forceinline__ void emit_log(const PairParams<MODEL, K> &pp, const d
 
 /* One max-plus step t >= 1: delta_t(j) = max_i cand(i, j) with the
  * reference's strict '>' from -inf (first maximising i wins, NaN never
- * wins); back-pointer i packed into `word` at `slot`. */
+ * wins); back-pointer i packed into `word` at `slot`.
+ * VALU form: the running max is one v_max_f64 (maxNum: a NaN candidate
+ * leaves it unchanged, and an equal one leaves its value unchanged) and the
+ * back-pointer one select on the strict compare, so each candidate costs
+ * 2 adds + cmp + max + select.  Value-identical to the reference loop; the
+ * back-pointer differs only where every candidate is -inf / NaN (the
+ * reference leaves it unset, here 0), which the epilogue flags through
+ * delta_T = -inf exactly as before. */
 template <int MODEL, int K>
 __device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
                                          const Obs &o, uint32_t &word, int slot)
@@ -810,11 +842,12 @@ __device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL
     double nd[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        double best = dev_ninf();
-        uint32_t arg = 0;
         bool on = true;
         if constexpr (ModelTraits<MODEL>::kTayal)
             on = tayal_pred(o.aux, j);
+        const int sh = slot * STEPB + j * BITS;
+        double best = dev_ninf();
+        uint32_t argsh = 0;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             double cand;
@@ -826,13 +859,16 @@ __device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL
                 /* (delta + log A) + emission (hmm.stan:111) */
                 cand = (dl[i] + pp.A[i][j]) + le[j];
             }
-            if (cand > best) {
-                best = cand;
-                arg = (uint32_t)i;
+            if (i == 0) {
+                best = fmax(best, cand);
+            } else {
+                const bool gt = cand > best;
+                best = fmax(best, cand);
+                argsh = gt ? ((uint32_t)i << sh) : argsh;
             }
         }
         nd[j] = best;
-        word |= arg << (slot * STEPB + j * BITS);
+        word |= argsh;
     }
 #pragma unroll
     for (int j = 0; j < K; ++j)
@@ -1556,6 +1592,10 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
         }
     } else if (fwd_only)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FWD>), s.grid, s.block, s.lds, st, a);
+    else if (MODEL == HHMM_MODEL_HMM_MULTINOM && a.xpk && !(a.outputs & extra) && ffbs)
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA | FB_FFBS | FB_PACK>), s.grid, s.block, s.lds, st, a);
+    else if (MODEL == HHMM_MODEL_HMM_MULTINOM && a.xpk && !(a.outputs & extra))
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA | FB_PACK>), s.grid, s.block, s.lds, st, a);
     else if ((a.outputs & extra) && ffbs)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FULL | FB_FFBS>), s.grid, s.block, s.lds, st, a);
     else if (a.outputs & extra)

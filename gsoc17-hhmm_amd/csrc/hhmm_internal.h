@@ -50,6 +50,7 @@ struct DevArgs {
     double *ckpt_ls;    /* [nchunk][P]    log scale at each checkpoint */
     uint32_t *bp;       /* [nword][P]     packed Viterbi back-pointers */
     double *lam;        /* [Tmax][P]      IOHMM: running sum of log c_t (unbeta pass) */
+    uint32_t *xpk;      /* [nchunk][P]    packed symbols of each checkpoint chunk (multinom, L <= 16) */
     /* parallel scan over T; scan_cl = 0: sequential sweeps */
     int32_t scan_cl;    /* steps per T-chunk (multiple of fb_chunk(K)) */
     int32_t scan_nc;    /* T-chunks per pair (of T_max) */
@@ -81,7 +82,7 @@ constexpr int kBlock = 256;
 constexpr size_t kLdsLimit = 160 * 1024;
 
 /* Bytes of workspace the kernels need for this launch shape. */
-size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags);
+size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags);
 
 /* Carves the workspace into DevArgs pointers. */
 void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags);

@@ -122,15 +122,15 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
 
 /* Offsets of every workspace region (SIZE_MAX = unused) and the total. */
 struct WsLayout {
-    size_t ckpt, ckpt_ls, bp, lam, mf, qb, mx, st, sl, be, bl, total;
+    size_t ckpt, ckpt_ls, xpk, bp, lam, mf, qb, mx, st, sl, be, bl, total;
     ScanPlan sp;
 };
 
-static WsLayout ws_layout(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
+static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
 {
     WsLayout w;
     const size_t NONE = SIZE_MAX;
-    w.ckpt = w.ckpt_ls = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
+    w.ckpt = w.ckpt_ls = w.xpk = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -153,6 +153,10 @@ static WsLayout ws_layout(int model, int K, int Tmax, int Toos, int64_t P, uint3
     } else if (needs_ckpt(model, outputs)) {
         w.ckpt = take((size_t)nchunk_of(K, Tmax) * K * P * d);
         w.ckpt_ls = take((size_t)nchunk_of(K, Tmax) * P * d);
+        /* hot profile of hmm-multinom: symbols repacked 4 bits each for the backward sweep */
+        const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
+        if (model == HHMM_MODEL_HMM_MULTINOM && L <= 16 && !(outputs & extra))
+            w.xpk = take((size_t)nchunk_of(K, Tmax) * P * sizeof(uint32_t));
     }
     if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
         const int Tv = (model == HHMM_MODEL_TAYAL_LITE) ? Toos : Tmax;
@@ -164,18 +168,19 @@ static WsLayout ws_layout(int model, int K, int Tmax, int Toos, int64_t P, uint3
     return w;
 }
 
-size_t workspace_bytes(int model, int K, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
+size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
 {
-    return ws_layout(model, K, Tmax, Toos, P, outputs, flags).total;
+    return ws_layout(model, K, L, Tmax, Toos, P, outputs, flags).total;
 }
 
 void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
 {
     char *b = (char *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
-    const WsLayout w = ws_layout(a.model, a.K, Tmax, Toos, a.P, a.outputs, flags);
+    const WsLayout w = ws_layout(a.model, a.K, a.L, Tmax, Toos, a.P, a.outputs, flags);
     auto at_off = [&](size_t o) -> void * { return o == SIZE_MAX ? nullptr : (void *)(b + o); };
     a.ckpt = (double *)at_off(w.ckpt);
     a.ckpt_ls = (double *)at_off(w.ckpt_ls);
+    a.xpk = (uint32_t *)at_off(w.xpk);
     a.bp = (uint32_t *)at_off(w.bp);
     a.lam = (double *)at_off(w.lam);
     a.scan_cl = w.sp.cl;

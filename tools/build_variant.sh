@@ -12,6 +12,6 @@ else
   (cd "$ROOT" && git archive "$REV" include gsoc17-hhmm_amd/csrc) | tar -x -C "$TMP"
 fi
 mkdir -p "$ROOT/gsoc17-hhmm_amd/lib/variants"
-make -s -C "$TMP/gsoc17-hhmm_amd/csrc" OUT="$ROOT/gsoc17-hhmm_amd/lib/variants/libhhmm_$NAME.so" "$@"
+make -s -j8 -C "$TMP/gsoc17-hhmm_amd/csrc" OUT="$ROOT/gsoc17-hhmm_amd/lib/variants/libhhmm_$NAME.so" "$@"
 rm -rf "$TMP"
 echo "built libhhmm_$NAME.so from $REV"
