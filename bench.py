@@ -4,11 +4,13 @@
 Workload (BASELINE.json configs[1], the metric's single-GPU config C2):
 hmm/stan/hmm-multinom.stan, K=4, L=9, 1,000,000 (series, draw) pairs
 (one posterior draw per series, HHMM_PAIR_ZIP) x T=1000, fp64.  One step =
-one pass of the hot path over the whole batch with inputs resident in HBM:
-libhhmm's fb_kernel (alpha/beta/gamma + loglik) and viterbi_kernel
-(zstar + logp_zstar), launched through the C ABI (hhmm_run_device) on
-torch's current stream.  Outputs: gamma_tk [P,T,K], zstar_t [P,T],
-loglik [P], logp_zstar [P].
+one pass of the hot path over the whole batch with inputs resident in HBM,
+through the C ABI (hhmm_run_device): the forward-backward request (gamma_tk
+[P,T,K], loglik [P]; fb_kernel) on torch's current stream and the Viterbi
+request (zstar_t [P,T], logp_zstar [P]; viterbi_kernel) on a second stream
+forked from it and joined back, so the VALU-bound decoder runs beside the
+HBM-bound forward-backward (what the library itself does for a single
+request asking for both).  --split runs them one after the other.
 
 Multi-GPU (torch.distributed.run, one process per GPU): every rank evaluates
 its own 1M pairs (weak scaling, no data-path collective); the per-step
@@ -50,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="also check a slice against the oracle")
+    ap.add_argument("--split", action="store_true",
+                    help="run the forward-backward and Viterbi one after the other on one stream")
     return ap.parse_args()
 
 
@@ -175,16 +179,20 @@ def cpu_baseline(T, target_s, seed):
                       f"{dt:.1f} s on {threads} threads, oracle libm-log build"}
 
 
-def load_traffic(tag):
-    """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (profiles/<tag>_pmc.json, written by tools/pmc_summary.py) or None."""
-    p = ROOT / "profiles" / f"{tag}_pmc.json"
-    if not p.exists():
-        return None
+def load_traffic(kernel, P, T):
+    """HBM bytes per launch of `kernel` from the committed PMC passes
+    (profiles/bench_traffic.json, written by tools/prof_summary.py from
+    rocprofv3 FETCH_SIZE / WRITE_SIZE, gfx950 correction applied), when they
+    were taken on this batch shape; else None."""
+    p = ROOT / "profiles" / "bench_traffic.json"
     try:
-        return json.loads(p.read_text())
+        bt = json.loads(p.read_text())
     except Exception:
         return None
+    if bt.get("pairs") != P or bt.get("T") != T:
+        return None
+    k = bt.get("kernels", {}).get(kernel)
+    return k.get("hbm_bytes_per_launch") if k else None
 
 
 def main():
@@ -206,15 +214,42 @@ def main():
     run = DeviceRun(lib, x, draws, P, T, dev)
     torch.cuda.synchronize()
 
+    s0 = torch.cuda.current_stream()
+    s1 = torch.cuda.Stream()
+
     def step(ev=None):
+        """One pass of the hot path.  ev = 5 events: step start, fb start/end
+        (recorded on fb's stream), viterbi start/end (on viterbi's stream)."""
         if ev:
-            ev[0].record()
+            ev[0].record(s0)
+        if a.split:
+            if ev:
+                ev[1].record(s0)
+            run.launch("fb")
+            if ev:
+                ev[2].record(s0)
+                ev[3].record(s0)
+            run.launch("viterbi")
+            if ev:
+                ev[4].record(s0)
+            return
+        fork = torch.cuda.Event()
+        fork.record(s0)
+        s1.wait_event(fork)
+        with torch.cuda.stream(s1):
+            if ev:
+                ev[3].record(s1)
+            run.launch("viterbi")
+            if ev:
+                ev[4].record(s1)
+        if ev:
+            ev[1].record(s0)
         run.launch("fb")
         if ev:
-            ev[1].record()
-        run.launch("viterbi")
-        if ev:
-            ev[2].record()
+            ev[2].record(s0)
+        join = torch.cuda.Event()
+        join.record(s1)
+        s0.wait_event(join)
         if world > 1:
             import torch.distributed as dist
             s = run.out["loglik"].sum().reshape(1)
@@ -226,7 +261,7 @@ def main():
     if a.check:
         check_slice(run, x, draws, P, T)
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(a.steps)]
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -238,8 +273,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    fb_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    vit_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    fb_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    vit_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
+    pair_ms = float(np.mean([e[0].elapsed_time(e[4]) if a.split else e[0].elapsed_time(e[2]) for e in evs]))
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -249,15 +285,22 @@ def main():
     if rank == 0:
         fb_b, vit_b, whole_b = bytes_per_step(T)
         units = P * T
-        if fb_ms >= vit_ms:
-            dom, dom_ms, dom_b = "fb_kernel", fb_ms, fb_b
+        kernels_ms = {"fb_kernel": fb_ms, "viterbi_kernel": vit_ms}
+        if a.split:  # sequential: the dominant kernel alone
+            if fb_ms >= vit_ms:
+                dom, dom_ms, dom_b = "fb_kernel", fb_ms, fb_b
+            else:
+                dom, dom_ms, dom_b = "viterbi_kernel", vit_ms, vit_b
+            traffic = load_traffic(dom, P, T)
         else:
-            dom, dom_ms, dom_b = "viterbi_kernel", vit_ms, vit_b
+            # concurrent: the two launches overlap for the whole step, so the
+            # unit is the launch pair -- the step's algorithmic bytes over the
+            # fork-to-join time (HIP events on the launch streams); traffic =
+            # both kernels' PMC bytes
+            dom, dom_ms, dom_b = "fb_kernel+viterbi_kernel", pair_ms, whole_b
+            t1, t2 = load_traffic("fb_kernel", P, T), load_traffic("viterbi_kernel", P, T)
+            traffic = (t1 + t2) if (t1 is not None and t2 is not None) else None
         achieved = dom_b * units / (dom_ms * 1e-3)
-        pmc = load_traffic("r01")
-        traffic = None
-        if pmc and pmc.get("kernel") == dom and pmc.get("pairs") == P and pmc.get("T") == T:
-            traffic = pmc.get("hbm_bytes_per_launch")
         value = world * units * a.steps / elapsed
         line = {
             "metric": "series-timesteps/sec forward-backward+Viterbi (K=4) at 1/2/4/8 GPU; % HBM roofline",
@@ -274,12 +317,14 @@ def main():
             "data": "synthetic (seeded HMM of hmm/main-multinom-semisup.R, Dirichlet-jittered draws)",
             "config": {"workload": "C2 hmm-multinom K=4 L=9, 1M pairs x T=1000 per GPU (zip pairing)",
                        "pairs_per_gpu": P, "T": T, "outputs": "gamma_tk zstar_t loglik logp_zstar",
-                       "parallelism": f"pairs sharded over {world} GPU(s)"},
+                       "parallelism": f"pairs sharded over {world} GPU(s)",
+                       "schedule": "fb and viterbi sequential" if a.split else "fb || viterbi (two streams)"},
             "whole_step_roofline_frac": whole_b * world * units * a.steps / elapsed / (HBM_PEAK * world),
-            "kernels_ms": {"fb_kernel": fb_ms, "viterbi_kernel": vit_ms},
+            "kernels_ms": kernels_ms,
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": traffic, "algorithmic_bytes_per_series_timestep": dom_b},
+                         "traffic": traffic, "algorithmic_bytes_per_series_timestep": dom_b,
+                         "duration_ms": dom_ms},
             "pair_failures": bad,
         }
         if not a.no_cpu_baseline and world == 1:

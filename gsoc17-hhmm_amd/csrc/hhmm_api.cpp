@@ -100,6 +100,66 @@ static void pool_put(void *ptr)
     p.live.erase(it);
 }
 
+/* ---------------- side streams (one per device) ---------------- */
+struct SideStreams {
+    std::mutex mu;
+    std::map<int, std::pair<hipStream_t, hipEvent_t>> by_dev; /* stream, fork event */
+    std::map<int, hipEvent_t> join_ev;
+};
+static SideStreams &side_streams()
+{
+    static SideStreams s;
+    return s;
+}
+
+hhmm_status fork_stream(hipStream_t st, hipStream_t *side)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_error("hipGetDevice failed");
+        return HHMM_ERR_HIP;
+    }
+    SideStreams &ss = side_streams();
+    std::lock_guard<std::mutex> g(ss.mu);
+    auto it = ss.by_dev.find(dev);
+    if (it == ss.by_dev.end()) {
+        hipStream_t s2 = nullptr;
+        hipEvent_t ev = nullptr, ej = nullptr;
+        if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ej, hipEventDisableTiming) != hipSuccess) {
+            set_error("side stream creation failed");
+            return HHMM_ERR_HIP;
+        }
+        it = ss.by_dev.emplace(dev, std::make_pair(s2, ev)).first;
+        ss.join_ev[dev] = ej;
+    }
+    if (hipEventRecord(it->second.second, st) != hipSuccess ||
+        hipStreamWaitEvent(it->second.first, it->second.second, 0) != hipSuccess) {
+        set_error("stream fork failed");
+        return HHMM_ERR_HIP;
+    }
+    *side = it->second.first;
+    return HHMM_OK;
+}
+
+hhmm_status join_stream(hipStream_t st, hipStream_t side)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_error("hipGetDevice failed");
+        return HHMM_ERR_HIP;
+    }
+    SideStreams &ss = side_streams();
+    std::lock_guard<std::mutex> g(ss.mu);
+    hipEvent_t ej = ss.join_ev[dev];
+    if (!ej || hipEventRecord(ej, side) != hipSuccess || hipStreamWaitEvent(st, ej, 0) != hipSuccess) {
+        set_error("stream join failed");
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
 static void pool_release_all()
 {
     Pool &p = pool();

@@ -768,8 +768,9 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     }
 }
 
+/* One workgroup of the forward-backward: pairs [block * blockDim, +blockDim). */
 template <int MODEL, int K, int MODE>
-__global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
+__device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
 {
     constexpr bool AUX = ModelTraits<MODEL>::kAux;
     HIP_DYNAMIC_SHARED(double2, lds)
@@ -777,7 +778,7 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
     const int wave = threadIdx.x >> 6;
     /* lanes past the last pair redo pair P-1 (identical values, benign
      * duplicate stores): every lane stays in the wave-wide reductions */
-    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    const int64_t p = min((int64_t)block * blockDim.x + threadIdx.x, a.P - 1);
     int64_t n, d;
     pair_coords(a, p, n, d);
     constexpr int KP = (K + 1) / 2;
@@ -802,6 +803,12 @@ __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
         be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
     }
     fb_sweep<MODEL, K, MODE, false>(a, ln, sp, al, 0.0, be, 0.0);
+}
+
+template <int MODEL, int K, int MODE>
+__global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
+{
+    fb_block<MODEL, K, MODE>(a, blockIdx.x);
 }
 
 /* ------------------------------------------------------------------ */
@@ -901,15 +908,16 @@ __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const
     }
 }
 
+/* One workgroup of the Viterbi decoder: pairs [block * blockDim, +blockDim). */
 template <int MODEL, int K>
-__global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
+__device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
 {
     constexpr int CV = vit_chunk(K);
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal; /* semisup Viterbi is unmasked (Q7) */
     HIP_DYNAMIC_SHARED(double2, lds)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    const int64_t p = min((int64_t)block * blockDim.x + threadIdx.x, a.P - 1);
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
@@ -951,6 +959,13 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
     }
     viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dl, word);
 }
+
+template <int MODEL, int K>
+__global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
+{
+    viterbi_block<MODEL, K>(a, blockIdx.x);
+}
+
 
 
 /* ------------------------------------------------------------------ */
@@ -1701,6 +1716,20 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
     }
     const bool any_fwd = (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA |
                                  HHMM_OUT_UNBETA | HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA | HHMM_OUT_FFBS)) != 0;
+    /* The Viterbi pass is independent of the forward-backward: it runs on a
+     * side stream forked from (and joined back into) the caller's stream, so
+     * the VALU-bound decoder's workgroups fill in beside the HBM-bound
+     * forward-backward's instead of strictly after them. */
+    const bool vit = (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) != 0;
+    hipStream_t vs = st;
+    if (vit && any_fwd && !(a.flags & HHMM_FLAG_NO_FUSE)) {
+        s = fork_stream(st, &vs);
+        if (s != HHMM_OK)
+            return s;
+        s = launch_viterbi<MODEL, K>(a, vs);
+        if (s != HHMM_OK)
+            return s;
+    }
     if (any_fwd) {
         if (a.scan_cl > 0 && !(out & HHMM_OUT_FFBS))
             s = launch_fb_scan<MODEL, K>(a, !needs_backward(MODEL, out), st);
@@ -1709,7 +1738,9 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
         if (s != HHMM_OK)
             return s;
     }
-    if (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
+    if (vs != st)
+        return join_stream(st, vs);
+    if (vit)
         s = launch_viterbi<MODEL, K>(a, st);
     return s;
 }

@@ -52,6 +52,7 @@ struct DevArgs {
     double *lam;        /* [Tmax][P]      IOHMM: running sum of log c_t (unbeta pass) */
     uint32_t *xpk;      /* [nchunk][P]    packed symbols of each checkpoint chunk (multinom, L <= 16) */
     /* parallel scan over T; scan_cl = 0: sequential sweeps */
+    uint32_t flags;     /* hhmm_request.flags */
     int32_t scan_cl;    /* steps per T-chunk (multiple of fb_chunk(K)) */
     int32_t scan_nc;    /* T-chunks per pair (of T_max) */
     double *sc_mf;      /* [nc][K][K][P] forward chunk products (chunk 0: row 0 = f at its end) */
@@ -108,6 +109,12 @@ hhmm_status run_io_reg_hi(const DevArgs &a, hipStream_t st);
 hhmm_status run_io_mix_lo(const DevArgs &a, hipStream_t st);
 hhmm_status run_io_mix_hi(const DevArgs &a, hipStream_t st);
 bool iohmm_supported(int K, int M, int L, char *why, size_t why_len);
+
+/* Side stream of the calling thread's current device for an independent
+ * pass: fork_stream makes *side wait for everything enqueued on `st` so far;
+ * join_stream makes `st` wait for everything enqueued on `side`. */
+hhmm_status fork_stream(hipStream_t st, hipStream_t *side);
+hhmm_status join_stream(hipStream_t st, hipStream_t side);
 
 /* Device self-test of the correctly rounded log (host arrays). */
 hhmm_status selftest_cr_log(const double *in, double *out, int64_t n);

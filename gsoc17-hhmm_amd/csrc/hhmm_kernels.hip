@@ -211,6 +211,7 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
     a.Tmax = d.T_max;
     a.Tout = d.T_max;
     a.outputs = req->outputs;
+    a.flags = (uint32_t)req->flags;
     a.T = d.T;
     a.x = d.x_int;
     a.xr = d.x_real;

@@ -38,6 +38,7 @@ PAIR_ZIP = 1
 FLAG_SCAN_AUTO = 0
 FLAG_SCAN_FORCE = 1 << 0
 FLAG_SCAN_OFF = 1 << 1
+FLAG_NO_FUSE = 1 << 2
 
 
 def flag_scan_chunk_log2(n):

@@ -158,6 +158,11 @@ typedef struct hhmm_draws {
 #define HHMM_FLAG_SCAN_FORCE (1u << 0)
 #define HHMM_FLAG_SCAN_OFF (1u << 1)
 #define HHMM_FLAG_SCAN_CHUNK_LOG2(n) ((uint32_t)(n) << 8) /* T-chunk length 2^n (0 = automatic) */
+/* With the forward-backward and Viterbi outputs both requested, the Viterbi
+ * pass runs on a library side stream forked from the caller's stream and
+ * joined back into it (the call's semantics are unchanged); this flag runs
+ * both passes on the caller's stream, one after the other. */
+#define HHMM_FLAG_NO_FUSE (1u << 2)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */

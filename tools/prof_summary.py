@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output into profiles/ (committed evidence).
 
-  python tools/prof_summary.py TAG gpurun_out/prof_TAG [--bench gpurun_out/bench_TAG.json]
+  python tools/prof_summary.py TAG gpurun_out/prof_TAG ['{"pairs": 1000000, "T": 1000}']
 
 Writes profiles/TAG_kernel_stats.csv (per-kernel calls / total / avg / min / max
 duration from the --kernel-trace --stats pass; SQLite .db or CSV input),
@@ -111,6 +111,17 @@ def main():
         if summ:
             (out / f"{tag}_pmc_traffic.json").write_text(json.dumps(summ, indent=1))
             print("wrote", out / f"{tag}_pmc_traffic.json")
+            # the bench's roofline.traffic: HBM bytes per launch of each bench kernel,
+            # keyed by its short name, for the batch shape the PMC passes ran
+            shape = {}
+            if len(sys.argv) > 3:
+                shape = json.loads(sys.argv[3])
+            bt = {"source": f"profiles/{tag}_pmc_traffic.json", **shape, "kernels": {}}
+            for k, v in summ.items():
+                base = k.split("::")[-1].split("<")[0]
+                bt["kernels"][base] = {"template": k, "hbm_bytes_per_launch": v["hbm_bytes_per_launch"]}
+            (out / "bench_traffic.json").write_text(json.dumps(bt, indent=1))
+            print("wrote", out / "bench_traffic.json")
 
 
 if __name__ == "__main__":
