@@ -401,13 +401,22 @@ enum FbMode {
     FB_FULL = 1,  /* any mix of alpha/beta/unalpha/unbeta/ungamma/gamma (+ per-step log scale) */
     FB_FWD = 2,   /* forward only: loglik / alpha / unalpha (tayal-lite, no backward output) */
     FB_FFBS = 4,  /* flag: FFBS draws in the backward sweep */
-    FB_PACK = 8   /* flag: the forward sweep packs each chunk's symbols (4 bits, L <= 16)
+    FB_PACK = 8,  /* flag: the forward sweep packs each chunk's symbols (4 bits, L <= 16)
                    * into the checkpoint record; the backward sweep reads those
                    * instead of re-reading x (hmm-multinom: 4 B -> 1 B per step) */
+    FB_BIG = 16   /* flag (gamma profile): checkpoints every kBigChunk steps, and a
+                   * two-level recompute in the backward sweep (every kGroup-th
+                   * state kept, each group recomputed before it is consumed):
+                   * checkpoint traffic 8 -> 4 B per step for ~1.44 forward
+                   * recomputes per step instead of 1 */
 };
 constexpr int fb_base(int mode) { return mode & 3; }
 constexpr bool fb_ffbs(int mode) { return (mode & FB_FFBS) != 0; }
 constexpr bool fb_pack(int mode) { return (mode & FB_PACK) != 0; }
+constexpr bool fb_big(int mode) { return (mode & FB_BIG) != 0; }
+constexpr int kBigChunk = 16; /* checkpoint interval of FB_BIG (a multiple of fb_chunk(K) = 8) */
+constexpr int kGroup = 2;     /* pass 1 keeps every kGroup-th state (32 steps / groups of 4 need
+                               * ~300 VGPRs: occupancy 1) */
 
 
 /* Writes the forward-side outputs of step t (alpha, unalpha). */
@@ -542,19 +551,22 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
             }
             if constexpr (fb_base(MODE) == FB_FWD) {
                 emit_alpha<K>(a, ln.p, t, al, lsc + kLn2 * ex);
-            } else if (u == 0) {
+            } else if (u == 0 && (!fb_big(MODE) || (c - ln.cb) % (kBigChunk / C) == 0)) {
+                /* checkpoint row: one per C-chunk, or one per kBigChunk steps (FB_BIG) */
+                const int64_t row = fb_big(MODE) ? (c - ln.cb) / (kBigChunk / C) : (c - ln.cb);
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    at(a.ckpt + ln.Qs * ((int64_t)(c - ln.cb) * K + k), (uint32_t)ln.q * 8u) = al[k];
+                    at(a.ckpt + ln.Qs * (row * K + k), (uint32_t)ln.q * 8u) = al[k];
                 if constexpr (fb_base(MODE) == FB_FULL)
                     at(a.ckpt_ls + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 8u) = lsc + kLn2 * ex;
-                if constexpr (fb_pack(MODE)) {
-                    uint32_t w = 0;
+            }
+            if (fb_pack(MODE) && u == 0) {
+                /* the chunk's C <= 8 symbols, 4 bits each, for the backward sweep */
+                uint32_t w = 0;
 #pragma unroll
-                    for (int v = 0; v < C; ++v)
-                        w |= ((uint32_t)(cur[v].x - 1) & 15u) << (4 * v);
-                    at(a.xpk + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 4u) = w;
-                }
+                for (int v = 0; v < C; ++v)
+                    w |= ((uint32_t)(cur[v].x - 1) & 15u) << (4 * v);
+                at(a.xpk + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 4u) = w;
             }
         }
         ecur = enx;
@@ -653,6 +665,134 @@ __device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, 
     }
 }
 
+/* FB_BIG applies to hmm-multinom's packed gamma profile with 8-step chunks. */
+template <int MODEL, int K>
+constexpr bool fb_big_ok()
+{
+    return MODEL == HHMM_MODEL_HMM_MULTINOM && fb_chunk(K) == 8;
+}
+
+/* Observation u of a kBigChunk-step block from its packed words (FB_PACK). */
+__device__ __forceinline__ Obs unpack_obs(const uint32_t (&w)[kBigChunk / 8], int u)
+{
+    Obs o;
+    o.x = (int)((w[u >> 3] >> (4 * (u & 7))) & 15u) + 1;
+    o.aux = 0;
+    o.xr = 0.0;
+    return o;
+}
+
+/* One kBigChunk-step block of the FB_BIG backward sweep: pass 1 recomputes
+ * the block's forward states from its checkpoint keeping every kGroup-th;
+ * pass 2 takes the groups from the end, recomputes each group's states and
+ * walks it backwards (posteriors, beta step). */
+template <int MODEL, int K, int MODE, bool FULLB>
+__device__ __forceinline__ void bwd_block_big(const DevArgs &a, const FbLane<MODEL, K> &ln, int t0,
+                                              const uint32_t (&w)[kBigChunk / 8], const double (&ck)[K],
+                                              double (&be)[K], int &bex)
+{
+    constexpr int B = kBigChunk, G = kGroup, NG = B / G;
+    double ga[NG][K];
+    double al[K];
+    int exb = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        al[k] = ga[0][k] = ck[k];
+    /* pass 1; each step's emission row is fetched one step ahead, and a
+     * scheduling barrier per step keeps the compiler from hoisting every
+     * LDS read of the unrolled block into registers at once */
+    Em<K> ecur, enx;
+    emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, 1), ecur);
+#pragma unroll
+    for (int u = 1; u < B; ++u) {
+        if (u + 1 < B)
+            emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, u + 1 < B ? u + 1 : u), enx);
+        if (FULLB || t0 + u < ln.Tp)
+            fwd_step<MODEL, K>(al, ln.pp, ecur.e, unpack_obs(w, u), exb);
+        if (u % G == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                ga[u / G][k] = al[k];
+        }
+        ecur = enx;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    /* pass 2: emission rows re-read from LDS one step ahead (keeping a
+     * group's rows in registers would cost 40 VGPRs) */
+#pragma unroll
+    for (int g = NG - 1; g >= 0; --g) {
+        double gb[G][K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            gb[0][k] = ga[g][k];
+        Em<K> e1, e2;
+        emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, g * G + 1), e1);
+#pragma unroll
+        for (int r = 1; r < G; ++r) {
+            const int u = g * G + r;
+            /* next: the following recompute step, or (after the last) the group's last step again */
+            emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, r + 1 < G ? u + 1 : g * G + G - 1), e2);
+            if (FULLB || t0 + u < ln.Tp)
+                fwd_step_to<MODEL, K>(gb[r - 1], gb[r], ln.pp, e1.e, unpack_obs(w, u), exb);
+            e1 = e2;
+        }
+        /* e1 = emission of step g*G + G-1 */
+#pragma unroll
+        for (int r = G - 1; r >= 0; --r) {
+            const int u = g * G + r;
+            const int t = t0 + u;
+            if (r > 0)
+                emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, r > 0 ? u - 1 : u), e2);
+            if (FULLB || t < ln.Tp) {
+                emit_posteriors<K, MODE>(a, ln.p, t, gb[r], be, 0.0, 0.0);
+                if (t > ln.t0)
+                    bwd_step<MODEL, K>(be, ln.pp, e1.e, unpack_obs(w, u), bex);
+            }
+            e1 = e2;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+/* FB_BIG backward sweep (gamma profile, packed symbols): kBigChunk-step
+ * blocks from the end, each block's checkpoint and packed words prefetched
+ * one block ahead. */
+template <int MODEL, int K, int MODE>
+__device__ __forceinline__ void fb_backward_big(const DevArgs &a, const FbLane<MODEL, K> &ln, int Tw_min, int Tw_max,
+                                                double (&be)[K], int &bex)
+{
+    static_assert(fb_pack(MODE) && fb_base(MODE) == FB_GAMMA && !fb_ffbs(MODE), "FB_BIG: packed gamma profile");
+    constexpr int B = kBigChunk, C = fb_chunk(K), NW = B / 8;
+    static_assert(C == 8, "FB_BIG packs 8-step chunks");
+    const int nblk = (Tw_max + B - 1) / B;
+    const int nfullb = Tw_min / B;
+    auto load_blk = [&](int blk, double (&ck)[K], uint32_t (&w)[NW]) {
+        const int bb = max(blk, 0);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ck[k] = at(a.ckpt + ln.Qs * ((int64_t)bb * K + k), (uint32_t)ln.q * 8u);
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = at(a.xpk + ln.Qs * (int64_t)(bb * NW + i), (uint32_t)ln.q * 4u);
+    };
+    double ck[K], ckn[K];
+    uint32_t w[NW], wn[NW];
+    load_blk(nblk - 1, ck, w);
+    for (int blk = nblk - 1; blk >= 0; --blk) {
+        load_blk(blk - 1, ckn, wn);
+        if (blk < nfullb)
+            bwd_block_big<MODEL, K, MODE, true>(a, ln, blk * B, w, ck, be, bex);
+        else
+            bwd_block_big<MODEL, K, MODE, false>(a, ln, blk * B, w, ck, be, bex);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ck[k] = ckn[k];
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = wn[i];
+    }
+}
+
 /* The forward-backward sweep of one lane over [ln.t0, ln.Tp): a whole series
  * (fb_kernel) or one T-chunk of the parallel scan (fb_scan_kernel, SURVEY §8
  * A16), which enters with the boundary vectors the scan computed: al = the
@@ -695,6 +835,10 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
 
     /* ---- backward sweep, chunk by chunk from the end ---- */
     int bex = 0;
+    if constexpr (fb_big(MODE)) {
+        fb_backward_big<MODEL, K, MODE>(a, ln, Tw_min, Tw_max, be, bex);
+        return;
+    }
     const int clast = nchunk - 1;
     /* observations of chunk cc: x itself, or the packed record of the forward sweep */
     auto obs_chunk = [&](Obs (&dst)[C], int cc) {
@@ -1609,6 +1753,9 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FWD>), s.grid, s.block, s.lds, st, a);
     else if (MODEL == HHMM_MODEL_HMM_MULTINOM && a.xpk && !(a.outputs & extra) && ffbs)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA | FB_FFBS | FB_PACK>), s.grid, s.block, s.lds, st, a);
+    else if (fb_big_ok<MODEL, K>() && a.xpk && !(a.outputs & extra))
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, fb_big_ok<MODEL, K>() ? FB_GAMMA | FB_PACK | FB_BIG : FB_GAMMA>),
+                           s.grid, s.block, s.lds, st, a);
     else if (MODEL == HHMM_MODEL_HMM_MULTINOM && a.xpk && !(a.outputs & extra))
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA | FB_PACK>), s.grid, s.block, s.lds, st, a);
     else if ((a.outputs & extra) && ffbs)

@@ -156,7 +156,9 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
         /* hot profile of hmm-multinom: symbols repacked 4 bits each for the backward sweep */
         const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
         if (model == HHMM_MODEL_HMM_MULTINOM && L <= 16 && !(outputs & extra))
-            w.xpk = take((size_t)nchunk_of(K, Tmax) * P * sizeof(uint32_t));
+            /* ceil(T/8) words (8-step chunks, 1 word each) or ceil(T/32) * 4
+             * (32-step chunks of the two-level recompute): at most T/8 + 4 */
+            w.xpk = take(((size_t)nchunk_of(K, Tmax) + 4) * P * sizeof(uint32_t));
     }
     if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
         const int Tv = (model == HHMM_MODEL_TAYAL_LITE) ? Toos : Tmax;

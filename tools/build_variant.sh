@@ -7,7 +7,10 @@ NAME=$1; REV=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TMP=$(mktemp -d)
 if [ "$REV" = "WT" ]; then
-  cp -r "$ROOT/include" "$ROOT/gsoc17-hhmm_amd" "$TMP/"
+  # sources only: copying lib/obj would give stale objects fresh mtimes
+  mkdir -p "$TMP/gsoc17-hhmm_amd"
+  cp -r "$ROOT/include" "$TMP/"
+  cp -r "$ROOT/gsoc17-hhmm_amd/csrc" "$TMP/gsoc17-hhmm_amd/"
 else
   (cd "$ROOT" && git archive "$REV" include gsoc17-hhmm_amd/csrc) | tar -x -C "$TMP"
 fi
