@@ -1648,10 +1648,15 @@ __global__ void __launch_bounds__(kBlock) fb_scan_kernel(const DevArgs a)
     HIP_DYNAMIC_SHARED(double2, lds)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int64_t G = a.P * (int64_t)a.scan_nc;
+    /* lane g = pp + Pp * c with Pp = P rounded up to whole waves: every wave
+     * lies in ONE T-chunk, so the sweep's wave-uniform chunk bounds (and its
+     * unconditional checkpoint prefetches) stay inside that chunk's rows.
+     * Lanes pp >= P redo pair P-1 (identical values, benign duplicate stores). */
+    const int64_t Pp = scan_lanes_per_chunk(a.P);
+    const int64_t G = Pp * (int64_t)a.scan_nc;
     const int64_t g = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, G - 1);
-    const int64_t p = g % a.P;
-    const int c = (int)(g / a.P);
+    const int64_t p = min(g % Pp, a.P - 1);
+    const int c = (int)(g / Pp);
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tpair = pair_len(a, n);
@@ -1783,21 +1788,23 @@ static hhmm_status launch_fb_scan(const DevArgs &a, bool fwd_only, hipStream_t s
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
-    const int64_t G = a.P * (int64_t)a.scan_nc;
+    const int64_t G = a.P * (int64_t)a.scan_nc;                        /* phase 1 lanes */
+    const int64_t G3 = scan_lanes_per_chunk(a.P) * (int64_t)a.scan_nc; /* phase 3 lanes */
     const dim3 gridG((unsigned)((G + s.block.x - 1) / s.block.x));
+    const dim3 gridG3((unsigned)((G3 + s.block.x - 1) / s.block.x));
     const dim3 gridP((unsigned)((a.P + 63) / 64));
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     if (fwd_only) {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, false>), gridG, s.block, s.lds, st, a);
         hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), gridP, dim3(64), 0, st, a);
-        hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG, s.block, s.lds, st, a);
+        hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
     } else {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, true>), gridG, s.block, s.lds, st, a);
         hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), gridP, dim3(64), 0, st, a);
         if (a.outputs & extra)
-            hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG, s.block, s.lds, st, a);
+            hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
         else
-            hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_GAMMA>), gridG, s.block, s.lds, st, a);
+            hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_GAMMA>), gridG3, s.block, s.lds, st, a);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

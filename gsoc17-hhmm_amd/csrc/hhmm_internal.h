@@ -64,6 +64,9 @@ struct DevArgs {
     double *sc_bl;      /* [nc][P]       its log scale */
 };
 
+/* Phase-3 lanes of the T-scan per T-chunk: P rounded up to whole waves. */
+constexpr int64_t scan_lanes_per_chunk(int64_t P) { return (P + 63) & ~(int64_t)63; }
+
 /* Parallel-scan plan of one request: T-chunk length and count (cl = 0: off). */
 struct ScanPlan {
     int cl;

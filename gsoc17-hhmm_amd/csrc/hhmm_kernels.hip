@@ -113,7 +113,7 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
     const int nc = (Tmax + cl - 1) / cl;
     if (!(flags & HHMM_FLAG_SCAN_FORCE) && (P >= 131072 || Tmax < 16384 || nc < 4))
         return sp;
-    if ((int64_t)P * nc >= (int64_t(1) << 29)) /* checkpoint columns are 32-bit byte offsets */
+    if (scan_lanes_per_chunk(P) * nc >= (int64_t(1) << 29)) /* checkpoint columns are 32-bit byte offsets */
         return sp;
     sp.cl = cl;
     sp.nc = nc;
@@ -140,7 +140,9 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     const size_t d = sizeof(double);
     w.sp = scan_plan(model, K, Tmax, P, outputs, flags);
     if (w.sp.cl > 0) {
-        const size_t nc = (size_t)w.sp.nc, G = (size_t)P * nc, rows = (size_t)(w.sp.cl / fb_chunk(K));
+        /* phase-3 checkpoint columns: one per (pair rounded up to whole waves, chunk) */
+        const size_t nc = (size_t)w.sp.nc, G = (size_t)scan_lanes_per_chunk(P) * nc,
+                     rows = (size_t)(w.sp.cl / fb_chunk(K));
         w.ckpt = take(rows * K * G * d);
         w.ckpt_ls = take(rows * G * d);
         w.mf = take(nc * K * K * P * d);

@@ -88,3 +88,28 @@ def test_scan_auto_long_tayal_matches_sequential(engine):
     ok = ~(n1 | n2)
     from tolerances import compare
     compare("gamma_tk", g1[ok], g2[ok])
+
+
+@pytest.mark.parametrize("model", SCAN_MODELS)
+@pytest.mark.parametrize("S", [250, 65, 1])
+def test_scan_pairs_not_whole_waves(engine, oracle, model, S):
+    """Pair counts that are not a multiple of the 64-lane wave: the per-chunk
+    sweep pads each T-chunk's lanes to whole waves, so no wave spans two
+    chunks (a wave that did once read checkpoint rows past its chunk's)."""
+    import hhmm_amd
+    data, draws = synth.GENERATORS[model](N=1, S=S, T=600)
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=force(4))
+    ref = oracle.gqs(model, data, draws, pars=pars)
+    compare_all(got, ref, pars)
+
+
+def test_scan_c5_shape_many_chunks(engine):
+    """C5's lane shape (250 pairs) across hundreds of T-chunks: the scan agrees
+    with the sequential sweep."""
+    import hhmm_amd
+    data, draws = synth.hmm_multinom(N=1, S=250, T=30_000)
+    pars = ["loglik", "gamma_tk"]
+    scan = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=force(6))
+    seq = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=_abi.FLAG_SCAN_OFF)
+    compare_all(scan, seq, pars)
