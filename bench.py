@@ -36,6 +36,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import hhmm_amd  # noqa: E402
+import hhmm_amd.api  # noqa: E402
 from hhmm_amd import _abi, synth  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md chip table)
@@ -52,6 +53,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="also check a slice against the oracle")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
+                         "printed as its own line: c3 iohmm-reg grid, c4 iohmm-hmix + FFBS, c5 Tayal T=1e6 "
+                         "(parallel scan over T)")
     ap.add_argument("--split", action="store_true",
                     help="run the forward-backward and Viterbi one after the other on one stream")
     return ap.parse_args()
@@ -209,6 +214,8 @@ def main():
     lib = hhmm_amd.load_library()
     assert lib.hhmm_init(1) == 0, lib.hhmm_last_error().decode()
 
+    if a.workload != "c2":
+        return other_workload(a, lib, dev, world, rank)
     P, T = a.pairs, a.T
     x, draws = make_batch(P, T, a.seed + 7919 * rank, dev)
     run = DeviceRun(lib, x, draws, P, T, dev)
@@ -329,6 +336,116 @@ def main():
         }
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(T, a.cpu_seconds, a.seed)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# The other BASELINE configs (evidence lines; C2 above is the metric)
+# ---------------------------------------------------------------------------
+
+WORKLOADS = {
+    # name: (model, generator kwargs per GPU, pairing, outputs, algorithmic bytes per series-timestep
+    #        (SURVEY.md §8d), description)
+    "c3": ("iohmm-reg", dict(N=1250, S=4000, T=300, K=4, M=4), "grid",
+           ["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
+           lambda T, S: 32 + 4 + (8 + 32) / S + 320 / T,
+           "C3 iohmm-reg K=4 M=4 T=300, 1250 series x 4000 draws per GPU (10k series / 8 GPUs), grid"),
+    "c4": ("iohmm-hmix", dict(N=16, S=4096, T=10_000, K=4, L=3, M=4), "grid",
+           ["loglik", "gamma_tk", "z_ffbs"],
+           lambda T, S: 32 + 4 + 8 + (8 + 32) / S + 8 * (4 + 4 * 4 + 3 * 4 * 3) / T,
+           "C4 iohmm-hmix K=4 L=3 M=4 T=10k, 16 series x 4096 draws, batched FFBS"),
+    "c5": ("hhmm-tayal2009", dict(N=1, S=250, T=1_000_000, L=9), "grid",
+           ["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
+           lambda T, S: 32 + 4 + 8 / S + (8 * (1 + 4 + 36) + 16) / T,
+           "C5 tayal K=4 L=9 T=1e6, 1 series x 250 draws per GPU (8 series / 8 GPUs), "
+           "parallel scan over T for the forward-backward"),
+}
+
+
+def other_workload(a, lib, dev, world, rank):
+    """C3 / C4 / C5: one request per step through hhmm_run_device on resident
+    device buffers (synthetic inputs from hhmm_amd.synth, copied once)."""
+    model, kw, pairing, pars, bps, desc = WORKLOADS[a.workload]
+    kw = dict(kw)
+    if model.startswith("iohmm"):
+        data, draws = synth.GENERATORS[model](seed=a.seed + 7919 * rank, **kw)
+    else:
+        data, draws = synth.tayal(seed=a.seed + 7919 * rank, **kw)
+    T = kw["T"]
+    # the request's input pointers from the host mirror (outputs are device-only)
+    host = hhmm_amd.api.PreparedRequest(model, data, draws, ["loglik"], pairing)
+    req, res = host.req, host.res
+    dmap = {}
+    for arr in host.keep:
+        dmap[arr.ctypes.data] = torch.from_numpy(np.asarray(arr).reshape(-1, order="F").copy()).to(dev)
+    for struct in (req.data, req.draws):
+        for name, ctype in struct._fields_:
+            v = getattr(struct, name)
+            if ctype is C.c_void_p and v and v in dmap:
+                setattr(struct, name, dmap[v].data_ptr())
+    P = host.P
+    if "z_ffbs" in pars:
+        dmap["u"] = torch.from_numpy(synth.ffbs_uniforms(P, T, seed=a.seed + rank).reshape(-1, order="F")).to(dev)
+        req.ffbs_u = dmap["u"].data_ptr()
+    req.outputs = 0
+    outs = {}
+    shape = {"P": P, "PTK": P * T * int(data["K"] if "K" in data else 4), "PT": P * T, "PTz": P * T}
+    for name in pars:
+        dt, code = _abi.RESULT_ARRAYS[name]
+        outs[name] = torch.empty(shape[code], dtype=torch.float64 if dt == "f64" else torch.int32, device=dev)
+        req.outputs |= _abi.OUT[name]
+        setattr(res, name, outs[name].data_ptr())
+    status = torch.zeros(P, dtype=torch.int32, device=dev)
+    res.pair_status = status.data_ptr()
+    ws = C.c_size_t(0)
+    assert lib.hhmm_workspace_size(C.byref(req), C.byref(ws)) == 0
+    wsbuf = torch.empty(max(int(ws.value), 256), dtype=torch.uint8, device=dev)
+
+    def step():
+        st = lib.hhmm_run_device(C.byref(req), C.byref(res), wsbuf.data_ptr(), wsbuf.numel(),
+                                 torch.cuda.current_stream().cuda_stream)
+        if st < 0:
+            raise RuntimeError(lib.hhmm_last_error().decode())
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(a.steps):
+        step()
+    ev[1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    dev_ms = ev[0].elapsed_time(ev[1]) / a.steps
+    units = P * T
+    B = bps(T, kw["S"])
+    if rank == 0:
+        line = {
+            "metric": "series-timesteps/sec (SURVEY §8d config) -- evidence line, not the headline",
+            "value": world * units * a.steps / elapsed, "unit": "series-timesteps/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (hhmm_amd.synth generators, seeded)",
+            "config": {"workload": desc, "model": model, "pairs_per_gpu": P, "T": T, "outputs": pars},
+            "roofline": {"kernel": "whole request", "bound": "hbm", "achieved": B * units / (dev_ms * 1e-3) / 1e9,
+                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": B * units / (dev_ms * 1e-3) / HBM_PEAK,
+                         "traffic": None, "algorithmic_bytes_per_series_timestep": B, "duration_ms": dev_ms},
+            "pair_failures": int((status != 0).sum().item()),
+        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
