@@ -644,7 +644,15 @@ hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n)
     hhmm_status s = check_device();
     if (s != HHMM_OK)
         return s;
-    return selftest_cr_log(in, out, n);
+    return selftest_cr_math(in, out, n, 0);
+}
+
+hhmm_status hhmm_selftest_cr_exp(const double *in, double *out, int64_t n)
+{
+    hhmm_status s = check_device();
+    if (s != HHMM_OK)
+        return s;
+    return selftest_cr_math(in, out, n, 1);
 }
 
 } /* extern "C" */

@@ -1111,6 +1111,205 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
 }
 
 
+/* ---- state-parallel Viterbi (few pairs, long T; C5) ------------------- *
+ * One lane per (pair, state j): a pair's K <= 4 states sit in one lane quad.
+ * Each step a lane fetches delta_{t-1} of the quad by DPP quad broadcasts,
+ * forms its own K candidates in the reference's order and reduces them with
+ * the same fmax / strict-compare rules as vit_step, so delta, the
+ * back-pointers and the paths are bit-identical to the lane-per-pair decoder.
+ * The per-step dependency chain is K candidates instead of K^2, which is what
+ * bounds a batch too small to hide latency with other waves (250 pairs x
+ * T = 1e6: 4 waves on the whole chip).  The back-pointer bits of the quad are
+ * OR-reduced into the same packed word layout, so the epilogue (run by all
+ * four lanes on the gathered delta_T; identical duplicate stores) and the
+ * backtrack are shared. */
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+/* d[i] = v of lane i of this lane's quad. */
+template <int K>
+__device__ __forceinline__ void quad_gather(double v, double (&d)[K])
+{
+    d[0] = dpp_f64<0x00>(v);
+    if constexpr (K > 1)
+        d[1] = dpp_f64<0x55>(v);
+    if constexpr (K > 2)
+        d[2] = dpp_f64<0xAA>(v);
+    if constexpr (K > 3)
+        d[3] = dpp_f64<0xFF>(v);
+}
+
+/* OR of w over this lane's quad. */
+__device__ __forceinline__ uint32_t quad_or(uint32_t w)
+{
+    w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false); /* quad_perm(1,0,3,2) */
+    w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false); /* quad_perm(2,3,0,1) */
+    return w;
+}
+
+/* Steps per prefetched observation chunk: a multiple of the word length, two
+ * Viterbi chunks deep so the (latency-bound) loads run far ahead. */
+constexpr int vit_sp_chunk(int K) { return 2 * vit_chunk(K); }
+
+template <int MODEL, int K>
+struct SpLane {
+    double colA[K]; /* log A[i][js] */
+    double mu, isig, c0; /* gauss: state js */
+    const double *slab;  /* discrete: log phi[js][.] column, stride 64 */
+    int js;              /* state of this lane */
+    int j;               /* quad position (bits only from j < K) */
+};
+
+template <int MODEL, int K>
+__device__ __forceinline__ double sp_emit(const SpLane<MODEL, K> &ln, const Obs &o, int L)
+{
+    if constexpr (ModelTraits<MODEL>::kGauss) {
+        const double z = (o.xr - ln.mu) * ln.isig;
+        const double z2 = z * z;
+        return ln.c0 + (-0.5 * z2);
+    } else {
+        return ln.slab[(min(max(o.x, 1), L) - 1) * 64];
+    }
+}
+
+template <int MODEL, int K, int CS, bool FULLC>
+__device__ __forceinline__ void vit_sp_chunk_run(const DevArgs &a, int64_t p, const SpLane<MODEL, K> &ln, int Tp,
+                                                 int c, const Obs (&cur)[CS], const Obs &nxt0, double &le,
+                                                 double &dl, uint32_t &bits)
+{
+    constexpr int BITS = bp_bits(K);
+    constexpr int STEPB = K * BITS;
+    constexpr int SPW = bp_steps_per_word(K);
+    const int t0 = c * CS;
+    const uint32_t jbit = (uint32_t)(ln.j * BITS);
+    const bool owns = ln.j < K;
+#pragma unroll
+    for (int u = 0; u < CS; ++u) {
+        const int t = t0 + u;
+        const double lnx = sp_emit<MODEL, K>(ln, (u + 1 < CS) ? cur[u + 1 < CS ? u + 1 : 0] : nxt0, a.L);
+        if (FULLC || t < Tp) {
+            if (!(u == 0 && c == 0)) {
+                double d[K];
+                quad_gather<K>(dl, d);
+                bool on = true;
+                if constexpr (ModelTraits<MODEL>::kTayal)
+                    on = tayal_pred(cur[u].aux, ln.js);
+                double best = dev_ninf();
+                uint32_t arg = 0;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    double cand;
+                    if constexpr (ModelTraits<MODEL>::kTayal) {
+                        cand = d[i] + le; /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
+                        cand = on ? cand + ln.colA[i] : cand;
+                    } else {
+                        cand = (d[i] + ln.colA[i]) + le; /* (delta + log A) + emission (hmm.stan:111) */
+                    }
+                    if (i == 0) {
+                        best = fmax(best, cand);
+                    } else {
+                        const bool gt = cand > best;
+                        best = fmax(best, cand);
+                        arg = gt ? (uint32_t)i : arg;
+                    }
+                }
+                dl = best;
+                if (owns)
+                    bits |= arg << ((uint32_t)((u % SPW) * STEPB) + jbit);
+            }
+            if (u % SPW == SPW - 1) {
+                const uint32_t w = quad_or(bits);
+                at(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u) = w;
+                bits = 0;
+            }
+        }
+        le = lnx;
+    }
+}
+
+template <int MODEL, int K>
+__global__ void __launch_bounds__(64) viterbi_sp_kernel(const DevArgs a)
+{
+    static_assert(K >= 2 && K <= 4, "state-parallel Viterbi: one lane quad per pair");
+    constexpr int CS = vit_sp_chunk(K);
+    constexpr bool VAUX = ModelTraits<MODEL>::kTayal; /* semisup Viterbi is unmasked (Q7) */
+    HIP_DYNAMIC_SHARED(double, ldsd)
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t p = min(g >> 2, a.P - 1);
+    SpLane<MODEL, K> ln;
+    ln.j = (int)(g & 3);
+    ln.js = min(ln.j, K - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+
+    {
+        PairParams<MODEL, K> pp;
+        load_params<MODEL, K, true>(pp, a, d);
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            double v = pp.A[i][0];
+#pragma unroll
+            for (int jj = 1; jj < K; ++jj)
+                v = (ln.js == jj) ? pp.A[i][jj] : v;
+            ln.colA[i] = v;
+        }
+        ln.mu = ln.isig = ln.c0 = 0.0;
+        if constexpr (ModelTraits<MODEL>::kGauss) {
+            ln.mu = pp.mu[0];
+            ln.isig = pp.isig[0];
+            ln.c0 = pp.c0[0];
+#pragma unroll
+            for (int jj = 1; jj < K; ++jj) {
+                ln.mu = (ln.js == jj) ? pp.mu[jj] : ln.mu;
+                ln.isig = (ln.js == jj) ? pp.isig[jj] : ln.isig;
+                ln.c0 = (ln.js == jj) ? pp.c0[jj] : ln.c0;
+            }
+        }
+    }
+    ln.slab = ldsd + lane;
+    if constexpr (ModelTraits<MODEL>::kDiscrete) {
+        double *col = ldsd + lane;
+        for (int l = 0; l < a.L; ++l)
+            col[l * 64] = hhmm_cr_log(draw2<K>(a.phi_k, a, d, ln.js, l, K));
+    }
+    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, n);
+    const int Tw_min = wave_min(Tp);
+    const int Tw_max = wave_max(Tp);
+    const int nfull = Tw_min / CS;
+    const int nchunk = (Tw_max + CS - 1) / CS;
+
+    Obs cur[CS];
+    load_chunk<MODEL, CS, VAUX>(cur, sp, 0);
+    double le = sp_emit<MODEL, K>(ln, cur[0], a.L);
+    /* Q3: only column K of delta_tk[1] is written, the others stay NaN */
+    double dl = (ln.js == K - 1) ? le : dev_nan();
+    uint32_t bits = 0;
+    for (int c = 0; c < nchunk; ++c) {
+        Obs nxt[CS];
+        load_chunk<MODEL, CS, VAUX>(nxt, sp, (c + 1) * CS);
+        if (c < nfull)
+            vit_sp_chunk_run<MODEL, K, CS, true>(a, p, ln, Tp, c, cur, nxt[0], le, dl, bits);
+        else
+            vit_sp_chunk_run<MODEL, K, CS, false>(a, p, ln, Tp, c, cur, nxt[0], le, dl, bits);
+#pragma unroll
+        for (int u = 0; u < CS; ++u)
+            cur[u] = nxt[u];
+    }
+    double dv[K];
+    quad_gather<K>(dl, dv);
+    viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dv, quad_or(bits));
+}
+
+
 
 /* ------------------------------------------------------------------ */
 /* Log-space forward-backward (the unalpha_tk / unbeta_tk profile)       */
@@ -1814,9 +2013,37 @@ static hhmm_status launch_fb_scan(const DevArgs &a, bool fwd_only, hipStream_t s
     return HHMM_OK;
 }
 
+/* State-parallel decoding for batches too small to hide the per-step
+ * latency with other waves (lane-per-pair below ~2 waves per SIMD), or when
+ * the caller forces it; K = 2..4 (one lane quad per pair). */
+static bool use_vit_states(const DevArgs &a)
+{
+    if (a.K < 2 || a.K > 4 || (a.flags & HHMM_FLAG_VIT_LANES))
+        return false;
+    return (a.flags & HHMM_FLAG_VIT_STATES) || a.P < 131072;
+}
+
 template <int MODEL, int K>
 static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
 {
+    if constexpr (K >= 2 && K <= 4) {
+        if (use_vit_states(a)) {
+            const size_t lds = ModelTraits<MODEL>::kDiscrete ? (size_t)a.L * 64 * sizeof(double) : 0;
+            if (lds > kLdsLimit) {
+                set_error("emission column L = %d does not fit in LDS", a.L);
+                return HHMM_ERR_UNSUPPORTED;
+            }
+            const int64_t lanes = 4 * a.P;
+            hipLaunchKernelGGL((viterbi_sp_kernel<MODEL, K>), dim3((unsigned)((lanes + 63) / 64)), dim3(64), lds,
+                               st, a);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) {
+                set_error("viterbi_sp_kernel launch: %s", hipGetErrorString(e));
+                return HHMM_ERR_HIP;
+            }
+            return HHMM_OK;
+        }
+    }
     LaunchShape s;
     if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);

@@ -119,8 +119,8 @@ bool iohmm_supported(int K, int M, int L, char *why, size_t why_len);
 hhmm_status fork_stream(hipStream_t st, hipStream_t *side);
 hhmm_status join_stream(hipStream_t st, hipStream_t side);
 
-/* Device self-test of the correctly rounded log (host arrays). */
-hhmm_status selftest_cr_log(const double *in, double *out, int64_t n);
+/* Device self-test of the correctly rounded log (which = 0) / exp (1), host arrays. */
+hhmm_status selftest_cr_math(const double *in, double *out, int64_t n, int which);
 
 void set_error(const char *fmt, ...);
 

@@ -50,11 +50,11 @@ hhmm_status launch_iohmm(const DevArgs &a, hipStream_t st)
 /* ------------------------------------------------------------------ */
 /* Self-test kernel                                                       */
 /* ------------------------------------------------------------------ */
-__global__ void cr_log_kernel(const double *in, double *out, int64_t n)
+__global__ void cr_math_kernel(const double *in, double *out, int64_t n, int which)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n)
-        out[i] = hhmm_cr_log(in[i]);
+        out[i] = which ? hhmm_cr_exp(in[i]) : hhmm_cr_log(in[i]);
 }
 
 
@@ -276,7 +276,7 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
     }
 }
 
-hhmm_status selftest_cr_log(const double *in, double *out, int64_t n)
+hhmm_status selftest_cr_math(const double *in, double *out, int64_t n, int which)
 {
     double *din = nullptr, *dout = nullptr;
     const size_t bytes = (size_t)(n > 0 ? n : 1) * sizeof(double);
@@ -287,7 +287,7 @@ hhmm_status selftest_cr_log(const double *in, double *out, int64_t n)
     }
     hipError_t e = hipMemcpy(din, in, (size_t)n * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess && n > 0) {
-        hipLaunchKernelGGL(cr_log_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, din, dout, n);
+        hipLaunchKernelGGL(cr_math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, din, dout, n, which);
         e = hipGetLastError();
     }
     if (e == hipSuccess)

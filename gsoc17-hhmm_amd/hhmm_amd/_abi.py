@@ -39,6 +39,8 @@ FLAG_SCAN_AUTO = 0
 FLAG_SCAN_FORCE = 1 << 0
 FLAG_SCAN_OFF = 1 << 1
 FLAG_NO_FUSE = 1 << 2
+FLAG_VIT_LANES = 1 << 3
+FLAG_VIT_STATES = 1 << 4
 
 
 def flag_scan_chunk_log2(n):
@@ -215,4 +217,6 @@ def declare(lib):
     lib.hhmm_run_device.restype = C.c_int
     lib.hhmm_selftest_cr_log.argtypes = [F64P, F64P, C.c_int64]
     lib.hhmm_selftest_cr_log.restype = C.c_int
+    lib.hhmm_selftest_cr_exp.argtypes = [F64P, F64P, C.c_int64]
+    lib.hhmm_selftest_cr_exp.restype = C.c_int
     return lib

@@ -163,6 +163,11 @@ typedef struct hhmm_draws {
  * joined back into it (the call's semantics are unchanged); this flag runs
  * both passes on the caller's stream, one after the other. */
 #define HHMM_FLAG_NO_FUSE (1u << 2)
+/* Viterbi decoding layout (HMM family, K = 2..4): by default batches below
+ * 131072 pairs decode one lane per (pair, state), larger ones one lane per
+ * pair; results are bit-identical either way.  These force one or the other. */
+#define HHMM_FLAG_VIT_LANES (1u << 3)
+#define HHMM_FLAG_VIT_STATES (1u << 4)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */
@@ -227,8 +232,10 @@ hhmm_status hhmm_workspace_size(const hhmm_request *req, size_t *bytes);
 hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res,
                             void *workspace, size_t workspace_bytes, void *stream);
 
-/* Self-test hook: the device's correctly rounded log over n host doubles. */
+/* Self-test hooks: the device's correctly rounded log / exp over n host
+ * doubles (the transcendentals every exact Viterbi / FFBS input goes through). */
 hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n);
+hhmm_status hhmm_selftest_cr_exp(const double *in, double *out, int64_t n);
 
 #ifdef __cplusplus
 }

@@ -1223,6 +1223,59 @@ void hhmm_oracle_log_array(const double *in, double *out, int64_t n)
         out[i] = OR_LOG(in[i]);
 }
 
+void hhmm_oracle_exp_array(const double *in, double *out, int64_t n)
+{
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = OR_EXP(in[i]);
+}
+
+/* Self-check of hhmm_crmath.h's quick phases against its accurate phases
+ * (which = 0: log, 1: exp) over in[0..n): stats[0] = max relative distance
+ * between the two double-double values where the quick phase applies,
+ * stats[1] = arguments whose rounding test failed (accurate fallback),
+ * stats[2] = arguments where hhmm_cr_* differs from the accurate value rounded
+ * once (must be 0), stats[3] = arguments the quick phase covered. */
+void hhmm_oracle_crmath_quick_check(int which, const double *in, int64_t n, double *stats)
+{
+    double maxrel = 0.0, fails = 0.0, bad = 0.0, covered = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double x = in[i];
+        hhmm_dd q, a;
+        double acc, bound;
+        int eq = 0, ea = 0;
+        if (which == 0) {
+            if (!(x >= 0x1p-1022) || x == __builtin_inf() || x == 1.0)
+                continue;
+            q = hhmm_cr_log_quick_dd(x);
+            a = hhmm_cr_log_acc_dd(x);
+            acc = a.hi + a.lo;
+            bound = fabs(q.hi) * 0x1p-68;
+            bad += (hhmm_cr_log(x) != acc);
+        } else {
+            if (!(x > -707.0 && x < 693.0))
+                continue;
+            q = hhmm_cr_exp_quick_dd(x, &eq);
+            a = hhmm_cr_exp_acc_dd(x, &ea);
+            if (eq != ea) {
+                bad += 1.0;
+                continue;
+            }
+            acc = a.hi + a.lo;
+            bound = q.hi * 0x1p-72;
+            bad += (hhmm_cr_exp(x) != acc * ldexp(1.0, ea));
+        }
+        covered += 1.0;
+        const double rel = fabs((q.hi - a.hi) + (q.lo - a.lo)) / fabs(a.hi);
+        if (rel > maxrel)
+            maxrel = rel;
+        fails += !hhmm_round_safe(q.hi, q.lo, bound);
+    }
+    stats[0] = maxrel;
+    stats[1] = fails;
+    stats[2] = bad;
+    stats[3] = covered;
+}
+
 const char *hhmm_oracle_variant(void)
 {
 #ifdef HHMM_ORACLE_LIBM_LOG

@@ -64,6 +64,30 @@ def gqs(model, data, draws, pars=None, pairing="grid", nthreads=1, variant="cr",
     return out
 
 
+def exp_array(x, variant="cr"):
+    import numpy as np
+    lib = load(variant)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib.hhmm_oracle_exp_array(x.ctypes.data_as(C.POINTER(C.c_double)),
+                              y.ctypes.data_as(C.POINTER(C.c_double)), x.size)
+    return y
+
+
+def crmath_quick_check(which, x):
+    """(max relative quick-vs-accurate distance, rounding-test fallbacks,
+    mismatches, arguments covered) of hhmm_crmath.h's quick phase; which is
+    "log" or "exp"."""
+    import numpy as np
+    lib = load("cr")
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    st = np.zeros(4)
+    lib.hhmm_oracle_crmath_quick_check(C.c_int({"log": 0, "exp": 1}[which]),
+                                       x.ctypes.data_as(C.POINTER(C.c_double)), C.c_int64(x.size),
+                                       st.ctypes.data_as(C.POINTER(C.c_double)))
+    return float(st[0]), int(st[1]), int(st[2]), int(st[3])
+
+
 def log_array(x, variant="cr"):
     import numpy as np
     lib = load(variant)

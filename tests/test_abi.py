@@ -25,7 +25,8 @@ def declared_functions():
 def test_header_declares_entry_points():
     names = declared_functions()
     for n in ("hhmm_run", "hhmm_run_device", "hhmm_workspace_size", "hhmm_validate", "hhmm_version",
-              "hhmm_last_error", "hhmm_init", "hhmm_shutdown", "hhmm_num_pairs", "hhmm_selftest_cr_log"):
+              "hhmm_last_error", "hhmm_init", "hhmm_shutdown", "hhmm_num_pairs", "hhmm_selftest_cr_log",
+              "hhmm_selftest_cr_exp"):
         assert n in names
 
 

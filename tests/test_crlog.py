@@ -75,3 +75,64 @@ def test_neg_log_sqrt_two_pi_constant(oracle, variant):
            "hhmm_crlog_table.h").read_text()
     m = re.search(r"#define HHMM_NEG_LOG_SQRT_TWO_PI (\S+)", hdr)
     assert float.fromhex(m.group(1)) == -math.log(math.sqrt(2.0 * math.pi))
+
+
+def _cr_exp_reference(x):
+    with decimal.localcontext() as ctx:
+        ctx.prec = 60
+        ctx.Emin = -9999
+        return float(D(x).exp())
+
+
+def test_crexp_is_correctly_rounded(oracle):
+    g = np.random.Generator(np.random.Philox(12))
+    x = np.concatenate([(g.random(800) - 0.5) * 1490.0, (g.random(400) - 0.5) * 40.0,
+                        -708.0 - g.random(200) * 37.0,  # subnormal results
+                        (g.random(100) - 0.5) * 1e-8,
+                        np.array([0.0, 1.0, -1.0, 709.78, -745.13, 1e-300, -1e-300])])
+    y = oracle.exp_array(x, "cr")
+    ref = np.array([_cr_exp_reference(v) for v in x])
+    bad = np.flatnonzero(y != ref)
+    assert bad.size == 0, [(x[i].hex(), y[i].hex(), ref[i].hex()) for i in bad[:5]]
+
+
+def test_crexp_special_values(oracle):
+    x = np.array([np.nan, np.inf, -np.inf, 710.0, -746.0, 0.0, -0.0])
+    y = oracle.exp_array(x, "cr")
+    assert np.isnan(y[0]) and y[1] == np.inf and y[2] == 0.0 and y[3] == np.inf and y[4] == 0.0
+    assert y[5] == 1.0 and y[6] == 1.0
+
+
+def _quick_sets(n, seed):
+    g = np.random.Generator(np.random.Philox(seed))
+    logs = {
+        "bits": g.integers(0x0010000000000000, 0x7FF0000000000000, size=n, dtype=np.int64).view(np.float64),
+        "near1": 1.0 + (g.random(n) - 0.5) * 2.0 ** -6,
+        "unit": g.random(n),
+        "probs": g.dirichlet(np.ones(4), size=n // 4).ravel(),
+    }
+    exps = {
+        "wide": (g.random(n) - 0.5) * 1400.0,
+        "small": (g.random(n) - 0.5) * 40.0,
+        "tiny": (g.random(n) - 0.5) * 1e-6,
+    }
+    return logs, exps
+
+
+def test_crmath_quick_phase_matches_accurate_phase(oracle):
+    """The quick phases (double arithmetic + a rounding test) return the
+    accurate phase's rounding on every argument they accept: their measured
+    error stays well inside the bound the rounding test assumes (2^-68 log,
+    2^-72 exp), and only a sliver of arguments falls back."""
+    import pyoracle
+    logs, exps = _quick_sets(1_000_000, seed=21)
+    for name, x in logs.items():
+        maxrel, fails, bad, cov = pyoracle.crmath_quick_check("log", x)
+        assert bad == 0, name
+        assert maxrel < 2.0 ** -71, (name, np.log2(maxrel))
+        assert fails < 1e-3 * cov, (name, fails)
+    for name, x in exps.items():
+        maxrel, fails, bad, cov = pyoracle.crmath_quick_check("exp", x)
+        assert bad == 0, name
+        assert maxrel < 2.0 ** -75, (name, np.log2(maxrel))
+        assert fails < 1e-3 * cov, (name, fails)

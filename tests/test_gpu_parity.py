@@ -7,7 +7,7 @@ device share the correctly rounded log and the reference's operation order).
 import numpy as np
 import pytest
 
-from hhmm_amd import synth
+from hhmm_amd import _abi, synth
 from tolerances import compare, compare_all
 
 pytestmark = pytest.mark.gpu
@@ -45,6 +45,27 @@ def test_cr_log_device_matches_oracle(engine, oracle):
     ref = oracle.log_array(x, "cr")
     same = (y.view(np.int64) == ref.view(np.int64)) | (np.isnan(y) & np.isnan(ref))
     assert same.all(), f"{(~same).sum()} device logs differ from the oracle's"
+
+
+def test_cr_exp_device_matches_oracle(engine, oracle):
+    """Device exp (quick phase + accurate fallback) bit-identical to the
+    oracle's, across the normal, subnormal-result and overflow ranges."""
+    import ctypes as C
+    g = np.random.Generator(np.random.Philox(8))
+    wide = (g.random(200_000) - 0.5) * 1500.0
+    small = (g.random(100_000) - 0.5) * 40.0
+    neg = -g.random(100_000) * 30.0
+    tiny = (g.random(50_000) - 0.5) * 1e-9
+    special = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 709.78, 709.79, -708.39, -708.4,
+                        -745.13, -745.14, -707.0, 693.0, 5e-324, -5e-324])
+    x = np.concatenate([wide, small, neg, tiny, special])
+    y = np.empty_like(x)
+    st = engine.hhmm_selftest_cr_exp(x.ctypes.data_as(C.POINTER(C.c_double)),
+                                     y.ctypes.data_as(C.POINTER(C.c_double)), x.size)
+    assert st == 0, engine.hhmm_last_error()
+    ref = oracle.exp_array(x, "cr")
+    same = (y.view(np.int64) == ref.view(np.int64)) | (np.isnan(y) & np.isnan(ref))
+    assert same.all(), f"{(~same).sum()} device exps differ from the oracle's"
 
 
 CASES = [
@@ -164,3 +185,67 @@ def test_parity_long_full_profile(engine, oracle, model):
     data, draws = synth.GENERATORS[model](N=2, S=40, T=1000)
     got, ref = run_both(engine, oracle, model, data, draws, synth.PARS[model])
     compare_all(got, ref, synth.PARS[model] + ["pair_status"])
+
+
+VIT_CASES = [("hmm", dict(K=2)), ("hmm", dict(K=3)), ("hmm", dict(K=4)), ("hmm-multinom", dict(K=2, L=5)),
+             ("hmm-multinom", dict(K=3, L=5)), ("hmm-multinom", dict(K=4, L=9)),
+             ("hmm-multinom-semisup", dict(K=4, L=9)), ("hhmm-tayal2009", dict()),
+             ("hhmm-tayal2009-lite", dict())]
+
+
+@pytest.mark.parametrize("layout", ["lanes", "states"])
+@pytest.mark.parametrize("model,kw", VIT_CASES, ids=[f"{m}-{'-'.join(f'{k}{v}' for k, v in kw.items())}"
+                                                     for m, kw in VIT_CASES])
+@pytest.mark.parametrize("T", [1, 2, 37, 1000])
+def test_viterbi_layouts_match_oracle(engine, oracle, model, kw, T, layout):
+    """Both Viterbi decoders -- one lane per pair and one lane per (pair,
+    state) -- are bit-exact with the oracle (paths, logp_zstar, status)."""
+    import hhmm_amd
+    flags = _abi.FLAG_VIT_LANES if layout == "lanes" else _abi.FLAG_VIT_STATES
+    data, draws = synth.GENERATORS[model](N=3, S=30, T=T, **kw)
+    pars = ["zstar_t", "logp_zstar"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=flags, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+@pytest.mark.parametrize("layout", ["lanes", "states"])
+@pytest.mark.parametrize("model", ["hmm", "hmm-multinom", "hhmm-tayal2009"])
+def test_viterbi_layouts_ragged(engine, oracle, model, layout):
+    import hhmm_amd
+    flags = _abi.FLAG_VIT_LANES if layout == "lanes" else _abi.FLAG_VIT_STATES
+    N, S, T = 5, 13, 90
+    data, draws = synth.GENERATORS[model](N=N, S=S, T=T)
+    data["T"] = np.array([90, 1, 17, 64, 33], dtype=np.int32)
+    pars = ["zstar_t", "logp_zstar", "loglik"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=flags, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+@pytest.mark.parametrize("layout", ["lanes", "states"])
+def test_viterbi_layouts_invalid_backpointer(engine, oracle, layout):
+    import hhmm_amd
+    flags = _abi.FLAG_VIT_LANES if layout == "lanes" else _abi.FLAG_VIT_STATES
+    data, draws = synth.hmm_multinom(N=1, S=4, T=12, K=3, L=4)
+    draws["phi_k"][:, :, 3] = 0.0
+    draws["phi_k"] /= draws["phi_k"].sum(axis=2, keepdims=True)
+    data["x"][0, 7] = 4
+    pars = ["zstar_t", "logp_zstar"]
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=flags, return_status=True)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, return_status=True)
+    assert (ref["pair_status"] == 1).all()
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+@pytest.mark.parametrize("model", ["hmm", "hhmm-tayal2009"])
+def test_viterbi_layouts_agree_long(engine, model):
+    """C5-like shape (few pairs, long T): the two decoders return identical
+    paths and logp_zstar."""
+    import hhmm_amd
+    data, draws = synth.GENERATORS[model](N=2, S=150, T=50_000)
+    pars = ["zstar_t", "logp_zstar"]
+    a = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=_abi.FLAG_VIT_LANES)
+    b = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=_abi.FLAG_VIT_STATES)
+    assert np.array_equal(a["zstar_t"], b["zstar_t"])
+    assert np.array_equal(a["logp_zstar"].view(np.int64), b["logp_zstar"].view(np.int64))
