@@ -57,6 +57,9 @@ def parse():
                     help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
                          "printed as its own line: c3 iohmm-reg grid, c4 iohmm-hmix + FFBS, c5 Tayal T=1e6 "
                          "(parallel scan over T)")
+    ap.add_argument("--pars", default=None,
+                    help="c3-c5 probes: comma-separated outputs instead of the workload's")
+    ap.add_argument("--flags", type=int, default=0, help="c3-c5 probes: hhmm_request.flags")
     ap.add_argument("--split", action="store_true",
                     help="run the forward-backward and Viterbi one after the other on one stream")
     return ap.parse_args()
@@ -369,6 +372,9 @@ def other_workload(a, lib, dev, world, rank):
     device buffers (synthetic inputs from hhmm_amd.synth, copied once)."""
     model, kw, pairing, pars, bps, desc = WORKLOADS[a.workload]
     kw = dict(kw)
+    if a.pars:
+        pars = a.pars.split(",")
+        desc += f" [probe: outputs {a.pars}, flags {a.flags}]"
     if model.startswith("iohmm"):
         data, draws = synth.GENERATORS[model](seed=a.seed + 7919 * rank, **kw)
     else:
@@ -390,6 +396,7 @@ def other_workload(a, lib, dev, world, rank):
         dmap["u"] = torch.from_numpy(synth.ffbs_uniforms(P, T, seed=a.seed + rank).reshape(-1, order="F")).to(dev)
         req.ffbs_u = dmap["u"].data_ptr()
     req.outputs = 0
+    req.flags = a.flags
     outs = {}
     shape = {"P": P, "PTK": P * T * int(data["K"] if "K" in data else 4), "PT": P * T, "PTz": P * T}
     for name in pars:

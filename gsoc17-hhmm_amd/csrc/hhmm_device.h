@@ -195,10 +195,13 @@ constexpr int vit_chunk(int K)
                                       : (8 % bp_steps_per_word(K) == 0 ? 8 : 2 * bp_steps_per_word(K));
 }
 
-/* Backtrack over chunk c (descending): writes zstar[t] and steps z. */
+/* Backtrack over chunk c (descending): zb[u] = zstar[t0 + u] (1-based) for
+ * the chunk's steps inside the series, stepping z; the stores are issued
+ * later (vit_back_flush), after the next chunk's word loads, so that waiting
+ * for those loads never waits for stores as well (vmcnt counts both on gfx9). */
 template <int K, int CV, bool FULLC>
-__device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int64_t p, int Tp, int c,
-                                               const uint32_t (&w)[CV / bp_steps_per_word(K)], int &z)
+__device__ __forceinline__ void vit_back_chunk(int Tp, int c, const uint32_t (&w)[CV / bp_steps_per_word(K)],
+                                               int &z, int (&zb)[CV])
 {
     constexpr int BITS = bp_bits(K);
     constexpr int SPW = bp_steps_per_word(K);
@@ -209,9 +212,39 @@ __device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int64_t p, int 
     for (int u = CV - 1; u >= 0; --u) {
         const int t = t0 + u;
         if (FULLC || t < Tp) {
-            at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = z + 1;
+            zb[u] = z + 1;
             if (t > 0)
                 z = (int)((w[u / SPW] >> ((u % SPW) * STEPB + z * BITS)) & MASK);
+        }
+    }
+}
+
+/* Stores chunk c's zstar values.  QUAD (one lane quad per pair, all four
+ * holding the same zb): lane j of the quad stores steps u = j, j+4, ... so a
+ * chunk takes CV/4 store instructions instead of CV. */
+template <int CV, bool QUAD>
+__device__ __forceinline__ void vit_back_flush(const DevArgs &a, int64_t p, int Tp, int c, const int (&zb)[CV])
+{
+    const int t0 = c * CV;
+    if constexpr (QUAD) {
+        static_assert(CV % 4 == 0, "quad flush needs whole quads of steps");
+        const int j = (int)(threadIdx.x & 3);
+#pragma unroll
+        for (int m = 0; m < CV / 4; ++m) {
+            /* masked OR, not a select chain: LLVM folds selects of array
+             * elements into a dynamically indexed load, i.e. scratch */
+            const int v = (zb[4 * m] & -(int)(j == 0)) | (zb[4 * m + 1] & -(int)(j == 1)) |
+                          (zb[4 * m + 2] & -(int)(j == 2)) | (zb[4 * m + 3] & -(int)(j == 3));
+            const int t = t0 + 4 * m + j;
+            if (t < Tp)
+                at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = v;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < CV; ++u) {
+            const int t = t0 + u;
+            if (t < Tp)
+                at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = zb[u];
         }
     }
 }
@@ -220,13 +253,14 @@ __device__ __forceinline__ void vit_back_chunk(const DevArgs &a, int64_t p, int 
  * back-pointer word, logp_zstar = max(delta_T) with Eigen's SSE2 maxCoeff NaN
  * rule, zstar_T = the LAST j attaining it (e.g. hmm/stan/hmm.stan:120-124),
  * pair_status, then the backtrack chunk by chunk with the words prefetched one
- * chunk ahead (hmm.stan:126-128). */
-template <int K>
+ * chunk ahead (hmm.stan:126-128).  QUAD: the state-parallel decoder's lane
+ * quads (every lane of a quad holds the same delta_T and word). */
+template <int K, bool QUAD = false>
 __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, int Tp, int Tw_min, int Tw_max,
                                                  const double (&dl)[K], uint32_t word)
 {
     constexpr int SPW = bp_steps_per_word(K);
-    constexpr int CV = vit_chunk(K);
+    constexpr int CV = QUAD ? 2 * vit_chunk(K) : vit_chunk(K);
     constexpr int WPC = CV / SPW; /* words per chunk */
     const int nfull = Tw_min / CV;
     const int nchunk = (Tw_max + CV - 1) / CV;
@@ -259,22 +293,27 @@ __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, in
      * are never consumed) */
     const int wmax = a.Tmax / SPW;
     uint32_t w[WPC], wn[WPC];
+    int zb[CV];
     const int clast = nchunk - 1;
 #pragma unroll
     for (int i = 0; i < WPC; ++i)
-        w[i] = at(a.bp + a.P * (int64_t)min(clast * WPC + i, wmax), (uint32_t)p * 4u);
+        w[i] = at(a.bp + a.P * (int64_t)min(max(clast * WPC + i, 0), wmax), (uint32_t)p * 4u);
     for (int c = clast; c >= 0; --c) {
 #pragma unroll
         for (int i = 0; i < WPC; ++i)
             wn[i] = at(a.bp + a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax), (uint32_t)p * 4u);
+        if (c < clast)
+            vit_back_flush<CV, QUAD>(a, p, Tp, c + 1, zb);
         if (c < nfull)
-            vit_back_chunk<K, CV, true>(a, p, Tp, c, w, z);
+            vit_back_chunk<K, CV, true>(Tp, c, w, z, zb);
         else
-            vit_back_chunk<K, CV, false>(a, p, Tp, c, w, z);
+            vit_back_chunk<K, CV, false>(Tp, c, w, z, zb);
 #pragma unroll
         for (int i = 0; i < WPC; ++i)
             w[i] = wn[i];
     }
+    if (clast >= 0)
+        vit_back_flush<CV, QUAD>(a, p, Tp, 0, zb);
 }
 
 } // namespace hhmm

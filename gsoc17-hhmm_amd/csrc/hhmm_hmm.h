@@ -1128,8 +1128,8 @@ template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v)
 {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
@@ -1149,8 +1149,8 @@ __device__ __forceinline__ void quad_gather(double v, double (&d)[K])
 /* OR of w over this lane's quad. */
 __device__ __forceinline__ uint32_t quad_or(uint32_t w)
 {
-    w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false); /* quad_perm(1,0,3,2) */
-    w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false); /* quad_perm(2,3,0,1) */
+    w |= (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false); /* quad_perm(1,0,3,2) */
+    w |= (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0x4E, 0xF, 0xF, false); /* quad_perm(2,3,0,1) */
     return w;
 }
 
@@ -1163,6 +1163,7 @@ struct SpLane {
     double colA[K]; /* log A[i][js] */
     double mu, isig, c0; /* gauss: state js */
     const double *slab;  /* discrete: log phi[js][.] column, stride 64 */
+    const double *arow;  /* tayal: rows [sign 1 | sign 2 | other][i] of the masked column, stride 64 */
     int js;              /* state of this lane */
     int j;               /* quad position (bits only from j < K) */
 };
@@ -1179,10 +1180,37 @@ __device__ __forceinline__ double sp_emit(const SpLane<MODEL, K> &ln, const Obs 
     }
 }
 
+/* Tayal: the masked transition column of this lane for a step's sign:
+ * log A[i][js] where the mask is on, -0.0 where it is off (x + -0.0 == x for
+ * every double x, so the off candidate keeps its value bit for bit). */
+template <int MODEL, int K>
+__device__ __forceinline__ void sp_arow(const SpLane<MODEL, K> &ln, int sign, double (&ar)[K])
+{
+    const int r = (sign == 1) ? 0 : (sign == 2 ? 1 : 2);
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        ar[i] = ln.arow[(r * K + i) * 64];
+}
+
+/* Stores chunk c's back-pointer words (issued after the next chunk's loads). */
+template <int K, int CS>
+__device__ __forceinline__ void sp_flush_words(const DevArgs &a, int64_t p, int Tp, int c,
+                                               const uint32_t (&wb)[CS / bp_steps_per_word(K)])
+{
+    constexpr int SPW = bp_steps_per_word(K);
+#pragma unroll
+    for (int i = 0; i < CS / SPW; ++i) {
+        const int t = c * CS + i * SPW + SPW - 1;
+        if (t < Tp)
+            at(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u) = wb[i];
+    }
+}
+
 template <int MODEL, int K, int CS, bool FULLC>
-__device__ __forceinline__ void vit_sp_chunk_run(const DevArgs &a, int64_t p, const SpLane<MODEL, K> &ln, int Tp,
-                                                 int c, const Obs (&cur)[CS], const Obs &nxt0, double &le,
-                                                 double &dl, uint32_t &bits)
+__device__ __forceinline__ void vit_sp_chunk_run(const DevArgs &a, const SpLane<MODEL, K> &ln, int Tp, int c,
+                                                 const Obs (&cur)[CS], const Obs &nxt0, double &le, double (&ar)[K],
+                                                 double &dl, uint32_t &bits,
+                                                 uint32_t (&wb)[CS / bp_steps_per_word(K)])
 {
     constexpr int BITS = bp_bits(K);
     constexpr int STEPB = K * BITS;
@@ -1193,22 +1221,23 @@ __device__ __forceinline__ void vit_sp_chunk_run(const DevArgs &a, int64_t p, co
 #pragma unroll
     for (int u = 0; u < CS; ++u) {
         const int t = t0 + u;
-        const double lnx = sp_emit<MODEL, K>(ln, (u + 1 < CS) ? cur[u + 1 < CS ? u + 1 : 0] : nxt0, a.L);
+        const Obs &on1 = (u + 1 < CS) ? cur[u + 1 < CS ? u + 1 : 0] : nxt0;
+        const double lnx = sp_emit<MODEL, K>(ln, on1, a.L);
+        double arx[K];
+        if constexpr (ModelTraits<MODEL>::kTayal)
+            sp_arow<MODEL, K>(ln, on1.aux, arx);
         if (FULLC || t < Tp) {
             if (!(u == 0 && c == 0)) {
                 double d[K];
                 quad_gather<K>(dl, d);
-                bool on = true;
-                if constexpr (ModelTraits<MODEL>::kTayal)
-                    on = tayal_pred(cur[u].aux, ln.js);
                 double best = dev_ninf();
                 uint32_t arg = 0;
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     double cand;
                     if constexpr (ModelTraits<MODEL>::kTayal) {
-                        cand = d[i] + le; /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
-                        cand = on ? cand + ln.colA[i] : cand;
+                        /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
+                        cand = (d[i] + le) + ar[i];
                     } else {
                         cand = (d[i] + ln.colA[i]) + le; /* (delta + log A) + emission (hmm.stan:111) */
                     }
@@ -1225,12 +1254,16 @@ __device__ __forceinline__ void vit_sp_chunk_run(const DevArgs &a, int64_t p, co
                     bits |= arg << ((uint32_t)((u % SPW) * STEPB) + jbit);
             }
             if (u % SPW == SPW - 1) {
-                const uint32_t w = quad_or(bits);
-                at(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u) = w;
+                wb[u / SPW] = quad_or(bits);
                 bits = 0;
             }
         }
         le = lnx;
+        if constexpr (ModelTraits<MODEL>::kTayal) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                ar[i] = arx[i];
+        }
     }
 }
 
@@ -1276,10 +1309,19 @@ __global__ void __launch_bounds__(64) viterbi_sp_kernel(const DevArgs a)
         }
     }
     ln.slab = ldsd + lane;
+    ln.arow = ldsd + (size_t)a.L * 64 + lane;
     if constexpr (ModelTraits<MODEL>::kDiscrete) {
         double *col = ldsd + lane;
         for (int l = 0; l < a.L; ++l)
             col[l * 64] = hhmm_cr_log(draw2<K>(a.phi_k, a, d, ln.js, l, K));
+    }
+    if constexpr (ModelTraits<MODEL>::kTayal) {
+        double *rows = ldsd + (size_t)a.L * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                rows[(r * K + i) * 64] = tayal_pred(r + 1, ln.js) ? ln.colA[i] : -0.0;
     }
     const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, n);
     const int Tw_min = wave_min(Tp);
@@ -1287,26 +1329,38 @@ __global__ void __launch_bounds__(64) viterbi_sp_kernel(const DevArgs a)
     const int nfull = Tw_min / CS;
     const int nchunk = (Tw_max + CS - 1) / CS;
 
+    __syncthreads(); /* LDS tables written (one wave per block; orders LDS) */
+
     Obs cur[CS];
     load_chunk<MODEL, CS, VAUX>(cur, sp, 0);
     double le = sp_emit<MODEL, K>(ln, cur[0], a.L);
+    double ar[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        ar[i] = 0.0;
     /* Q3: only column K of delta_tk[1] is written, the others stay NaN */
     double dl = (ln.js == K - 1) ? le : dev_nan();
     uint32_t bits = 0;
+    constexpr int WPC = CS / bp_steps_per_word(K);
+    uint32_t wb[WPC];
     for (int c = 0; c < nchunk; ++c) {
         Obs nxt[CS];
         load_chunk<MODEL, CS, VAUX>(nxt, sp, (c + 1) * CS);
+        if (c > 0)
+            sp_flush_words<K, CS>(a, p, Tp, c - 1, wb);
         if (c < nfull)
-            vit_sp_chunk_run<MODEL, K, CS, true>(a, p, ln, Tp, c, cur, nxt[0], le, dl, bits);
+            vit_sp_chunk_run<MODEL, K, CS, true>(a, ln, Tp, c, cur, nxt[0], le, ar, dl, bits, wb);
         else
-            vit_sp_chunk_run<MODEL, K, CS, false>(a, p, ln, Tp, c, cur, nxt[0], le, dl, bits);
+            vit_sp_chunk_run<MODEL, K, CS, false>(a, ln, Tp, c, cur, nxt[0], le, ar, dl, bits, wb);
 #pragma unroll
         for (int u = 0; u < CS; ++u)
             cur[u] = nxt[u];
     }
+    if (nchunk > 0)
+        sp_flush_words<K, CS>(a, p, Tp, nchunk - 1, wb);
     double dv[K];
     quad_gather<K>(dl, dv);
-    viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dv, quad_or(bits));
+    viterbi_epilogue<K, true>(a, p, Tp, Tw_min, Tw_max, dv, quad_or(bits));
 }
 
 
@@ -2028,7 +2082,8 @@ static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
 {
     if constexpr (K >= 2 && K <= 4) {
         if (use_vit_states(a)) {
-            const size_t lds = ModelTraits<MODEL>::kDiscrete ? (size_t)a.L * 64 * sizeof(double) : 0;
+            const size_t lds = ((ModelTraits<MODEL>::kDiscrete ? (size_t)a.L : 0) +
+                                (ModelTraits<MODEL>::kTayal ? (size_t)3 * K : 0)) * 64 * sizeof(double);
             if (lds > kLdsLimit) {
                 set_error("emission column L = %d does not fit in LDS", a.L);
                 return HHMM_ERR_UNSUPPORTED;
