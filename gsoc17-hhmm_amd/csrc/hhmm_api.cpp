@@ -200,11 +200,13 @@ static uint32_t available_outputs(int m)
         return fb | HHMM_OUT_FFBS;
     case HHMM_MODEL_IOHMM_REG:
     case HHMM_MODEL_IOHMM_MIX:
-        return fb | HHMM_OUT_OBLIK_TK | HHMM_OUT_LOGA | HHMM_OUT_FFBS;
-    case HHMM_MODEL_IOHMM_HMIX:
+        /* + the fitted-output GQ draws (iohmm-reg.stan:124-148; iohmm-mix.stan:133-161) */
+        return fb | HHMM_OUT_OBLIK_TK | HHMM_OUT_LOGA | HHMM_OUT_FFBS | HHMM_OUT_HATPI | HHMM_OUT_HATZ |
+               HHMM_OUT_HATX | (m == HHMM_MODEL_IOHMM_MIX ? HHMM_OUT_HATL : 0u);
+    case HHMM_MODEL_IOHMM_HMIX: /* hatpi_tk is a local there (iohmm-hmix.stan:147) */
         return HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_GAMMA |
                HHMM_OUT_OBLIK_TK | HHMM_OUT_OBLIK_T | HHMM_OUT_LOGA | HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR |
-               HHMM_OUT_FFBS;
+               HHMM_OUT_FFBS | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
     case HHMM_MODEL_IOHMM_HMIX_LITE:
         return HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_OBLIK_TK | HHMM_OUT_OBLIK_T | HHMM_OUT_LOGA;
     case HHMM_MODEL_TAYAL_LITE:
@@ -315,11 +317,17 @@ static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool ho
                 {HHMM_OUT_FFBS, o->z_ffbs, "z_ffbs"},
                 {HHMM_OUT_ALPHA_OOS, o->alpha_tk_oos, "alpha_tk_oos"},
                 {HHMM_OUT_UNALPHA_OOS, o->unalpha_tk_oos, "unalpha_tk_oos"},
-                {HHMM_OUT_LOGA, o->logA_ij, "logA_ij"}};
+                {HHMM_OUT_LOGA, o->logA_ij, "logA_ij"},
+                {HHMM_OUT_HATPI, o->hatpi_tk, "hatpi_tk"},
+                {HHMM_OUT_HATZ, o->hatz_t, "hatz_t"},
+                {HHMM_OUT_HATL, o->hatl_t, "hatl_t"},
+                {HHMM_OUT_HATX, o->hatx_t, "hatx_t"}};
     for (auto &e : outs)
         REQUIRE(!(r->outputs & e.bit) || e.ptr, "output %s requested but its pointer is NULL", e.name);
     if (r->outputs & HHMM_OUT_FFBS)
         REQUIRE(r->ffbs_u, "FFBS needs ffbs_u");
+    if (r->outputs & (HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX))
+        REQUIRE(r->hat_rand, "hatz_t / hatl_t / hatx_t need hat_rand");
 
     if (host) {
         const int64_t N = d.n_series;
@@ -410,6 +418,7 @@ static void describe(const hhmm_request *r, const hhmm_result *o, hhmm_request *
     in(w.p_11, (const void **)&dr->draws.p_11, S, 8);
     in(w.A_row, (const void **)&dr->draws.A_row, S * 4, 8);
     in(r->ffbs_u, (const void **)&dr->ffbs_u, P * Tm, 8);
+    in(r->hat_rand, (const void **)&dr->hat_rand, P * Tm * 3, 8);
     const size_t Tz = (r->model == HHMM_MODEL_TAYAL_LITE) ? To : Tm;
     ou(HHMM_OUT_LOGLIK, o->loglik, (void **)&dq->loglik, P, 8);
     ou(HHMM_OUT_UNALPHA, o->unalpha_tk, (void **)&dq->unalpha_tk, P * Tm * K, 8);
@@ -426,6 +435,10 @@ static void describe(const hhmm_request *r, const hhmm_result *o, hhmm_request *
     ou(HHMM_OUT_ALPHA_OOS, o->alpha_tk_oos, (void **)&dq->alpha_tk_oos, P * To * K, 8);
     ou(HHMM_OUT_UNALPHA_OOS, o->unalpha_tk_oos, (void **)&dq->unalpha_tk_oos, P * To * K, 8);
     ou(HHMM_OUT_LOGA, o->logA_ij, (void **)&dq->logA_ij, P * Tm * K, 8);
+    ou(HHMM_OUT_HATPI, o->hatpi_tk, (void **)&dq->hatpi_tk, P * Tm * K, 8);
+    ou(HHMM_OUT_HATZ, o->hatz_t, (void **)&dq->hatz_t, P * Tm, 4);
+    ou(HHMM_OUT_HATL, o->hatl_t, (void **)&dq->hatl_t, P * Tm, 4);
+    ou(HHMM_OUT_HATX, o->hatx_t, (void **)&dq->hatx_t, P * Tm, 8);
 }
 
 static hhmm_status hip_fail(hipError_t e, const char *what)
@@ -451,7 +464,7 @@ using namespace hhmm;
 
 extern "C" {
 
-const char *hhmm_version(void) { return "hhmm-mi355x 0.1.0 gfx950 abi 1"; }
+const char *hhmm_version(void) { return "hhmm-mi355x 0.2.0 gfx950 abi 2"; }
 
 const char *hhmm_last_error(void) { return g_last_error.c_str(); }
 

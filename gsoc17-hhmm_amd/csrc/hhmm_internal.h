@@ -45,6 +45,11 @@ struct DevArgs {
     double *logA;       /* [P, Tout, K] A_ij (reg / mix) or logA_ij (hmix / lite) */
     int32_t *z_ffbs;    /* [P, Tout]    FFBS draw */
     const double *ffbs_u; /* [P, Tmax]  caller uniforms */
+    /* fitted-output GQ draws */
+    double *hatpi;        /* [P, Tout, K] */
+    int32_t *hatz, *hatl; /* [P, Tout] 1-based */
+    double *hatx;         /* [P, Tout] */
+    const double *hat_rand; /* [P, Tmax, 3] caller uniforms / normal deviates */
     /* workspace */
     double *ckpt;       /* [nchunk][K][P] forward checkpoints */
     double *ckpt_ls;    /* [nchunk][P]    log scale at each checkpoint */
@@ -107,6 +112,8 @@ hhmm_status run_tayal_lite(const DevArgs &a, const hhmm_request *req, const hhmm
 
 /* IOHMM family (iohmm-reg / -mix / -hmix / -hmix-lite), hhmm_iohmm.hip. */
 hhmm_status launch_iohmm(const DevArgs &a, hipStream_t stream);
+/* Fitted-output draws hatpi / hatz / hatl / hatx (hhmm_fitted.hip). */
+hhmm_status launch_fitted(const DevArgs &a, hipStream_t stream);
 hhmm_status run_io_reg_lo(const DevArgs &a, hipStream_t st);
 hhmm_status run_io_reg_hi(const DevArgs &a, hipStream_t st);
 hhmm_status run_io_mix_lo(const DevArgs &a, hipStream_t st);

@@ -250,6 +250,11 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
     a.logA = res->logA_ij;
     a.z_ffbs = res->z_ffbs;
     a.ffbs_u = req->ffbs_u;
+    a.hatpi = res->hatpi_tk;
+    a.hatz = res->hatz_t;
+    a.hatl = res->hatl_t;
+    a.hatx = res->hatx_t;
+    a.hat_rand = req->hat_rand;
     return a;
 }
 
@@ -269,7 +274,15 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
     case HHMM_MODEL_IOHMM_REG:
     case HHMM_MODEL_IOHMM_MIX:
     case HHMM_MODEL_IOHMM_HMIX:
-    case HHMM_MODEL_IOHMM_HMIX_LITE: return launch_iohmm(a, st);
+    case HHMM_MODEL_IOHMM_HMIX_LITE: {
+        constexpr uint32_t kHat = HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
+        hhmm_status s = HHMM_OK;
+        if (a.outputs & ~kHat)
+            s = launch_iohmm(a, st);
+        if (s == HHMM_OK && (a.outputs & kHat))
+            s = launch_fitted(a, st);
+        return s;
+    }
     default:
         set_error("model %d has no device path in this build", req->model);
         return HHMM_ERR_UNSUPPORTED;

@@ -1,11 +1,11 @@
-"""ctypes mirror of include/hhmm.h (ABI version 1).
+"""ctypes mirror of include/hhmm.h (ABI version 2).
 
 Field order and types must match the C structs exactly; tests/test_abi.py
 checks the sizes against offsets parsed from the header.
 """
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # hhmm_status
 OK = 0
@@ -63,6 +63,10 @@ OUT = {
     "alpha_tk_oos": 1 << 12,
     "unalpha_tk_oos": 1 << 13,
     "logA_ij": 1 << 14,
+    "hatpi_tk": 1 << 15,
+    "hatz_t": 1 << 16,
+    "hatl_t": 1 << 17,
+    "hatx_t": 1 << 18,
 }
 
 I32P = C.POINTER(C.c_int32)
@@ -121,6 +125,7 @@ class Request(C.Structure):
         ("ffbs_u", C.c_void_p),
         ("device", C.c_int32),
         ("flags", C.c_int32),
+        ("hat_rand", C.c_void_p),
     ]
 
 
@@ -142,6 +147,10 @@ class Result(C.Structure):
         ("unalpha_tk_oos", C.c_void_p),
         ("logA_ij", C.c_void_p),
         ("pair_status", C.c_void_p),
+        ("hatpi_tk", C.c_void_p),
+        ("hatz_t", C.c_void_p),
+        ("hatl_t", C.c_void_p),
+        ("hatx_t", C.c_void_p),
     ]
 
 
@@ -193,6 +202,10 @@ RESULT_ARRAYS = {
     "alpha_tk_oos": ("f64", "PToK"),
     "unalpha_tk_oos": ("f64", "PToK"),
     "logA_ij": ("f64", "PTK"),
+    "hatpi_tk": ("f64", "PTK"),
+    "hatz_t": ("i32", "PT"),
+    "hatl_t": ("i32", "PT"),
+    "hatx_t": ("f64", "PT"),
 }
 
 

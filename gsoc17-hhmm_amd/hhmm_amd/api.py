@@ -73,7 +73,8 @@ def _series_array(a, N, kind):
 class PreparedRequest:
     """A request plus the numpy buffers it points at (kept alive together)."""
 
-    def __init__(self, model, data, draws, pars, pairing="grid", device=-1, uniforms=None, flags=0):
+    def __init__(self, model, data, draws, pars, pairing="grid", device=-1, uniforms=None, flags=0,
+                 hat_rand=None):
         if model not in _abi.MODELS:
             raise ValueError(f"unknown model {model!r}; one of {sorted(_abi.MODELS)}")
         self.model = model
@@ -160,6 +161,13 @@ class PreparedRequest:
             if uu.shape != (self.P, Tmax):
                 raise ValueError(f"uniforms must have shape {(self.P, Tmax)}, got {uu.shape}")
             req.ffbs_u = self._ptr(uu)
+        if {"hatz_t", "hatl_t", "hatx_t"} & set(self.pars):
+            if hat_rand is None:
+                raise ValueError("hatz_t / hatl_t / hatx_t need hat_rand of shape (P, T_max, 3)")
+            hr = _f64(hat_rand)
+            if hr.shape != (self.P, Tmax, 3):
+                raise ValueError(f"hat_rand must have shape {(self.P, Tmax, 3)}, got {hr.shape}")
+            req.hat_rand = self._ptr(hr)
         self.status = np.zeros(self.P, dtype=np.int32)
         res.pair_status = self.status.ctypes.data
         self.req, self.res = req, res
@@ -178,16 +186,19 @@ class PreparedRequest:
 
 
 def gqs(model, data, draws, pars=None, pairing="grid", device=-1, lib=None, return_status=False, uniforms=None,
-        flags=0):
+        flags=0, hat_rand=None):
     """Evaluates the model's TP/GQ outputs for every (series, draw) pair on the GPU.
 
     Returns {name: array} with pair-major shapes (P, T, K) / (P, T) / (P,);
     pair p = s + S*n under "grid" pairing (see reshape_pairs).  "z_ffbs" (a
     forward-filtering backward-sampling draw) consumes the
     caller's uniforms, shape (P, T_max), values in (0, 1).  `flags`: HHMM_FLAG_*
-    (e.g. force / forbid the parallel scan over T, _abi.FLAG_SCAN_*)."""
+    (e.g. force / forbid the parallel scan over T, _abi.FLAG_SCAN_*).  The IOHMM
+    fitted-output draws hatz_t / hatl_t / hatx_t (Stan's categorical_rng /
+    normal_rng) consume `hat_rand`, shape (P, T_max, 3): a uniform for hatz, a
+    uniform for hatl and a standard normal deviate for hatx per (pair, t)."""
     lib = lib or load_library()
-    pr = PreparedRequest(model, data, draws, pars, pairing, device, uniforms, flags)
+    pr = PreparedRequest(model, data, draws, pars, pairing, device, uniforms, flags, hat_rand)
     st = lib.hhmm_run(C.byref(pr.req), C.byref(pr.res))
     if st < 0:
         raise HHMMError(st, lib.hhmm_last_error().decode())

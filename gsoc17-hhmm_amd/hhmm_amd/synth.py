@@ -265,6 +265,18 @@ def ffbs_uniforms(P, T, seed=SEED):
     return np.where(u > 0.0, u, 0.5)
 
 
+def hat_rand(P, T, seed=SEED):
+    """Caller randomness of the IOHMM fitted-output draws, shape (P, T, 3):
+    [..., 0] uniform for hatz_t, [..., 1] uniform for hatl_t (both in (0, 1)),
+    [..., 2] standard normal deviate for hatx_t (Philox stream 8)."""
+    g = rng(seed, 8)
+    r = np.empty((P, T, 3))
+    u = g.random((P, T, 2))
+    r[..., :2] = np.where(u > 0.0, u, 0.5)
+    r[..., 2] = g.standard_normal((P, T))
+    return r
+
+
 GENERATORS = {
     "hmm": hmm_gauss,
     "hmm-multinom": hmm_multinom,
@@ -294,3 +306,10 @@ PARS["hmm-multinom"] = PARS["hmm"]
 PARS["hmm-multinom-semisup"] = PARS["hmm"]
 PARS["hhmm-tayal2009"] = PARS["hmm"]
 PARS["iohmm-mix"] = PARS["iohmm-reg"]
+
+# Fitted-output GQ draws each IOHMM program declares.
+HAT_PARS = {
+    "iohmm-reg": ["hatpi_tk", "hatz_t", "hatx_t"],
+    "iohmm-mix": ["hatpi_tk", "hatz_t", "hatl_t", "hatx_t"],
+    "iohmm-hmix": ["hatz_t", "hatl_t", "hatx_t"],
+}

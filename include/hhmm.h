@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define HHMM_ABI_VERSION 1u
+#define HHMM_ABI_VERSION 2u
 
 typedef enum hhmm_status {
     HHMM_OK = 0,
@@ -109,6 +109,23 @@ typedef enum hhmm_pairing {
 #define HHMM_OUT_ALPHA_OOS     (1u << 12) /* tayal-lite alpha_tk_oos                [P,T_oos,K] */
 #define HHMM_OUT_UNALPHA_OOS   (1u << 13) /* tayal-lite unalpha_tk_oos              [P,T_oos,K] */
 #define HHMM_OUT_LOGA          (1u << 14) /* IOHMM A_ij / logA_ij per t             [P,T,K] */
+/* Fitted-output draws of the IOHMM generated quantities:
+ * iohmm-reg.stan:124-148, iohmm-mix.stan:133-161, iohmm-hmix.stan:137-157.
+ * Stan draws them with its own RNG; here the caller supplies the randomness
+ * (hhmm_request.hat_rand), so draws are reproducible bit for bit:
+ *   hatpi_tk[t] = softmax(u_t' w_j)                         (reg, mix)
+ *   hatz_t[t]   = categorical_rng(hatpi_tk[t])  with uniform hat_rand[p,t,0]
+ *   hatl_t[t]   = categorical_rng(lambda_kl[hatz]) with uniform hat_rand[p,t,1] (mix, hmix)
+ *   hatx_t[t]   = normal_rng(mu, sigma) = z * sigma + mu with the standard
+ *                 normal deviate z = hat_rand[p,t,2] (boost's normal_distribution
+ *                 form); mu, sigma = u_t' b_km[hatz], s_k[hatz] (reg) or
+ *                 mu_kl, s_kl[hatz][hatl] (mix, hmix)
+ * categorical_rng(theta, u) = Stan's inverse CDF: c = theta[1], b = 1;
+ * while (b < K && u > c) c += theta[++b]; returns b. */
+#define HHMM_OUT_HATPI         (1u << 15) /* hatpi_tk                               [P,T,K] */
+#define HHMM_OUT_HATZ          (1u << 16) /* hatz_t (1-based)                       [P,T] */
+#define HHMM_OUT_HATL          (1u << 17) /* hatl_t (1-based)                       [P,T] */
+#define HHMM_OUT_HATX          (1u << 18) /* hatx_t                                 [P,T] */
 
 /* The Stan `data` block, batched over N series (series fastest). */
 typedef struct hhmm_data {
@@ -179,6 +196,8 @@ typedef struct hhmm_request {
     const double *ffbs_u;      /* [P, T_max] uniforms in (0,1) for HHMM_OUT_FFBS */
     int32_t device;            /* HIP device ordinal for hhmm_run; -1 = current */
     int32_t flags;             /* HHMM_FLAG_* (0 = defaults) */
+    const double *hat_rand;    /* [P, T_max, 3] for HHMM_OUT_HATZ/HATL/HATX: uniform (hatz),
+                                * uniform (hatl), standard normal (hatx) at p + P*(t + T_max*c) */
 } hhmm_request;
 
 /* Caller-allocated outputs; a pointer may be NULL when its bit is not requested. */
@@ -199,6 +218,10 @@ typedef struct hhmm_result {
     double  *unalpha_tk_oos;   /* [P, T_oos_max, K] */
     double  *logA_ij;          /* [P, T_max, K] */
     int32_t *pair_status;      /* [P] optional */
+    double  *hatpi_tk;         /* [P, T_max, K] */
+    int32_t *hatz_t;           /* [P, T_max] */
+    int32_t *hatl_t;           /* [P, T_max] */
+    double  *hatx_t;           /* [P, T_max] */
 } hhmm_result;
 
 /* Library identity, e.g. "hhmm-mi355x 0.1.0 gfx950 abi 1". */

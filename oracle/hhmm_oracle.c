@@ -256,6 +256,11 @@ typedef struct pair_ctx {
     double *ffbs_u;     /* [T] caller uniforms of this pair */
     int32_t *zf;        /* [T] draws, 1-based (0 = undefined) */
     double *ff;         /* [T*K] filter f_t */
+    /* fitted-output draws (see fitted_draws below) */
+    double *hat_rand;   /* [T*3] caller uniform (hatz), uniform (hatl), normal deviate (hatx) */
+    double *hatpi;      /* [T*K] */
+    int32_t *hatz, *hatl; /* [T], 1-based */
+    double *hatx;       /* [T] */
 } pair_ctx;
 
 static void *xmalloc(size_t n)
@@ -315,6 +320,11 @@ static void ctx_alloc(pair_ctx *c, int K, int L, int M, int Tm, int Toos)
     c->ffbs_u = xmalloc(sizeof(double) * TT);
     c->zf = xmalloc(sizeof(int32_t) * TT);
     c->ff = xmalloc(sizeof(double) * tk);
+    c->hat_rand = xmalloc(sizeof(double) * (size_t)TT * 3);
+    c->hatpi = xmalloc(sizeof(double) * tk);
+    c->hatz = xmalloc(sizeof(int32_t) * TT);
+    c->hatl = xmalloc(sizeof(int32_t) * TT);
+    c->hatx = xmalloc(sizeof(double) * TT);
 }
 
 static void ctx_free(pair_ctx *c)
@@ -323,7 +333,8 @@ static void ctx_free(pair_ctx *c)
                     c->mu, c->sigma, c->w, c->b, c->sk, c->lambda, c->mukl, c->skl,
                     c->unalpha, c->alpha, c->unbeta, c->beta, c->ungamma, c->gamma, c->oblik,
                     c->Arow, c->logA, c->delta, c->acc, c->tmp, c->bp, c->zstar, c->oblik_t,
-                    c->unalpha_oos, c->alpha_oos, c->ffbs_u, c->zf, c->ff};
+                    c->unalpha_oos, c->alpha_oos, c->ffbs_u, c->zf, c->ff,
+                    c->hat_rand, c->hatpi, c->hatz, c->hatl, c->hatx};
     for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i)
         free(ptrs[i]);
 }
@@ -1033,6 +1044,58 @@ static void ffbs_contract(pair_ctx *c, int model)
 }
 
 /* ------------------------------------------------------------------ */
+/* Fitted-output draws                                   */
+/* ------------------------------------------------------------------ */
+
+/* Stan Math categorical_rng(theta, rng) with the caller's uniform u in
+ * place of uniform_01(rng): index = cumulative_sum(theta); b = 0;
+ * while (u > index[b]) b++ -- bounded to n - 1 (a u above a total that
+ * rounded below 1 takes the last category).  Returns 1-based. */
+static int stan_categorical(const double *theta, int n, double u)
+{
+    int b = 0;
+    double cum = theta[0];
+    while (b < n - 1 && u > cum) {
+        ++b;
+        cum = cum + theta[b];
+    }
+    return b + 1;
+}
+
+/* iohmm-reg.stan:131-148, iohmm-mix.stan:140-160, iohmm-hmix.stan:146-157:
+ *   reg_tk[t, j] = u_tm[t]' * to_vector(w_km[j]); hatpi_tk[t] = softmax(reg_tk[t]);
+ *   hatz_t[t] = categorical_rng(hatpi_tk[t]);
+ *   reg:  hatx_t[t] = normal_rng(u_tm[t]' * b_km[hatz_t[t]], s_k[hatz_t[t]]);
+ *   mix:  hatl_t[t] = categorical_rng(lambda_kl[hatz_t[t]]);
+ *         hatx_t[t] = normal_rng(mu_kl[hatz][hatl], s_kl[hatz][hatl]).
+ * normal_rng(mu, sigma) is boost's normal_distribution: unit deviate * sigma
+ * + mu, the unit deviate supplied by the caller (hat_rand[.,.,2]). */
+static void fitted_draws(pair_ctx *c, int model, int have_rand)
+{
+    const int K = c->K, T = c->T, M = c->M, L = c->L;
+    double *v = c->acc;
+    for (int t = 0; t < T; ++t) {
+        for (int j = 0; j < K; ++j)
+            v[j] = stan_dot(&c->u[(size_t)t * M], &c->w[(size_t)j * M], M);
+        stan_softmax(v, K, &TK(c->hatpi, t, 0));
+        if (!have_rand)
+            continue;
+        const double *rnd = &c->hat_rand[(size_t)t * 3];
+        const int z = stan_categorical(&TK(c->hatpi, t, 0), K, rnd[0]);
+        c->hatz[t] = z;
+        if (model == HHMM_MODEL_IOHMM_REG) {
+            const double mu = stan_dot(&c->u[(size_t)t * M], &c->b[(size_t)(z - 1) * M], M);
+            c->hatl[t] = 0;
+            c->hatx[t] = rnd[2] * c->sk[z - 1] + mu;
+        } else {
+            const int l = stan_categorical(&c->lambda[(size_t)(z - 1) * L], L, rnd[1]);
+            c->hatl[t] = l;
+            c->hatx[t] = rnd[2] * c->skl[(z - 1) * L + (l - 1)] + c->mukl[(z - 1) * L + (l - 1)];
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* Batch driver                                                         */
 /* ------------------------------------------------------------------ */
 
@@ -1064,6 +1127,12 @@ static void gather(pair_ctx *c, const hhmm_request *r, int64_t n, int64_t s)
         const size_t P = (size_t)num_pairs(r), pp = (size_t)(r->pairing == HHMM_PAIR_ZIP ? n : s + S * n);
         for (int t = 0; t < c->T; ++t)
             c->ffbs_u[t] = r->ffbs_u[pp + P * (size_t)t];
+    }
+    if (r->hat_rand) {
+        const size_t P = (size_t)num_pairs(r), pp = (size_t)(r->pairing == HHMM_PAIR_ZIP ? n : s + S * n);
+        for (int t = 0; t < c->T; ++t)
+            for (int q = 0; q < 3; ++q)
+                c->hat_rand[(size_t)t * 3 + q] = r->hat_rand[pp + P * ((size_t)t + (size_t)Tm * q)];
     }
     for (int t = 0; t < c->T_oos; ++t) {
         const size_t ix = (size_t)n + (size_t)N * t;
@@ -1140,6 +1209,16 @@ static void scatter(const pair_ctx *c, const hhmm_request *r, hhmm_result *o, in
     if ((out & HHMM_OUT_FFBS) && o->z_ffbs)
         for (int t = 0; t < T; ++t)
             o->z_ffbs[(size_t)p + (size_t)P * t] = c->zf[t];
+    PUT_TK(HHMM_OUT_HATPI, o->hatpi_tk, c->hatpi)
+    if ((out & HHMM_OUT_HATZ) && o->hatz_t)
+        for (int t = 0; t < T; ++t)
+            o->hatz_t[(size_t)p + (size_t)P * t] = c->hatz[t];
+    if ((out & HHMM_OUT_HATL) && o->hatl_t)
+        for (int t = 0; t < T; ++t)
+            o->hatl_t[(size_t)p + (size_t)P * t] = c->hatl[t];
+    if ((out & HHMM_OUT_HATX) && o->hatx_t)
+        for (int t = 0; t < T; ++t)
+            o->hatx_t[(size_t)p + (size_t)P * t] = c->hatx[t];
     if (o->pair_status)
         o->pair_status[p] = c->status;
 #undef PUT_TK
@@ -1162,6 +1241,8 @@ static void run_pair(pair_ctx *c, const hhmm_request *r)
     }
     if ((r->outputs & HHMM_OUT_FFBS) && r->ffbs_u)
         ffbs_contract(c, r->model);
+    if (r->outputs & (HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX))
+        fitted_draws(c, r->model, r->hat_rand != NULL);
 }
 
 /* Runs pairs [p0, p1) of the request; nthreads <= 0 uses the OpenMP default.

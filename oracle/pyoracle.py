@@ -46,10 +46,10 @@ def load(variant="cr"):
 
 
 def gqs(model, data, draws, pars=None, pairing="grid", nthreads=1, variant="cr", return_status=False,
-        pair_range=None, uniforms=None):
+        pair_range=None, uniforms=None, hat_rand=None):
     """Same contract as hhmm_amd.gqs, computed by the scalar CPU oracle."""
     lib = load(variant)
-    pr = PreparedRequest(model, data, draws, pars, pairing, uniforms=uniforms)
+    pr = PreparedRequest(model, data, draws, pars, pairing, uniforms=uniforms, hat_rand=hat_rand)
     if pair_range is None:
         st = lib.hhmm_oracle_run(C.byref(pr.req), C.byref(pr.res), nthreads)
     else:
