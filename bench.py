@@ -53,10 +53,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="also check a slice against the oracle")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "f1"],
                     help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
                          "printed as its own line: c3 iohmm-reg grid, c4 iohmm-hmix + FFBS, c5 Tayal T=1e6 "
-                         "(parallel scan over T)")
+                         "(parallel scan over T); f1 = the tick -> leg feature extractor (SURVEY §8 F1)")
+    ap.add_argument("--ticks", type=int, default=100_000_000, help="f1: ticks per GPU")
     ap.add_argument("--pars", default=None,
                     help="c3-c5 probes: comma-separated outputs instead of the workload's")
     ap.add_argument("--flags", type=int, default=0, help="c3-c5 probes: hhmm_request.flags")
@@ -217,6 +218,8 @@ def main():
     lib = hhmm_amd.load_library()
     assert lib.hhmm_init(1) == 0, lib.hhmm_last_error().decode()
 
+    if a.workload == "f1":
+        return features_workload(a, lib, dev, world, rank)
     if a.workload != "c2":
         return other_workload(a, lib, dev, world, rank)
     P, T = a.pairs, a.T
@@ -453,6 +456,85 @@ def other_workload(a, lib, dev, world, rank):
                          "traffic": None, "algorithmic_bytes_per_series_timestep": B, "duration_ms": dev_ms},
             "pair_failures": int((status != 0).sum().item()),
         }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def features_workload(a, lib, dev, world, rank):
+    """F1: extract_features (tayal2009/R/feature-extraction.R:8-133) over a
+    synthetic tick series resident in HBM; one step = the whole pipeline
+    (change points, compaction, per-leg rows and features) through
+    hhmm_extract_features_device.  Weak scaling: every rank owns its own ticks."""
+    from hhmm_amd import features as F
+    F.declare(lib)
+    n = a.ticks
+    price, size, tm = F.synth_ticks(n, seed=a.seed + 7919 * rank)
+    dp, ds, dt = (torch.from_numpy(v).to(dev) for v in (price, size, tm))
+    cols = {k: torch.empty(n, dtype=torch.float64 if t == "f64" else torch.int32, device=dev)
+            for k, t in F.COLUMNS.items()}
+    tk = F.Ticks(n, dp.data_ptr(), ds.data_ptr(), dt.data_ptr(), 0.25)
+    legs = F.Legs(n, 0, *[cols[k].data_ptr() for k in F.COLUMNS])
+    wsb = C.c_size_t(0)
+    assert lib.hhmm_features_workspace_size(n, C.byref(wsb)) == 0
+    ws = torch.empty(int(wsb.value), dtype=torch.uint8, device=dev)
+
+    def step():
+        st = lib.hhmm_extract_features_device(C.byref(tk), C.byref(legs), ws.data_ptr(), ws.numel(),
+                                              torch.cuda.current_stream().cuda_stream)
+        if st < 0:
+            raise RuntimeError(lib.hhmm_last_error().decode())
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record()
+    for _ in range(a.steps):
+        step()
+    ev[1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    dev_ms = ev[0].elapsed_time(ev[1]) / a.steps
+    m = int(legs.n_legs)
+    # algorithmic bytes: price + size per tick; per leg the two index times and 52 B of leg columns
+    B = 16.0 * n + 68.0 * m
+    if rank == 0:
+        line = {
+            "metric": "ticks/sec, tick -> zig-zag -> leg features (SURVEY §8 F1) -- evidence line, not the headline",
+            "value": world * n * a.steps / elapsed, "unit": "ticks/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic ticks (hhmm_amd.features.synth_ticks: 1-cent random walk, board lots, "
+                    "exponential gaps)",
+            "config": {"workload": f"F1 extract_features alpha=0.25, {n} ticks per GPU", "ticks_per_gpu": n,
+                       "legs": m},
+            "roofline": {"kernel": "whole pipeline (5 kernels)", "bound": "hbm",
+                         "achieved": B / (dev_ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": B / (dev_ms * 1e-3) / HBM_PEAK, "traffic": None,
+                         "algorithmic_bytes_per_tick": B / n, "duration_ms": dev_ms},
+        }
+        if not a.no_cpu_baseline and world == 1:
+            sys.path.insert(0, str(ROOT / "oracle"))
+            import pyoracle
+            ns = min(n, 20_000_000)
+            t1 = time.perf_counter()
+            pyoracle.extract_features(price[:ns], size[:ns], tm[:ns])
+            cs = time.perf_counter() - t1
+            line["cpu_baseline"] = {"value": ns / cs, "unit": "ticks/s", "cores": 1, "kind": "port",
+                                    "sample": f"first {ns} ticks of the same series, sequential C oracle "
+                                              f"(oracle/features_oracle.c), {cs:.1f} s"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -669,3 +669,144 @@ hhmm_status hhmm_selftest_cr_exp(const double *in, double *out, int64_t n)
 }
 
 } /* extern "C" */
+
+/* ------------------------------------------------------------------ */
+/* Feature extractor entry points (include/hhmm_features.h)            */
+/* ------------------------------------------------------------------ */
+
+extern "C" {
+
+static hhmm_status check_ticks(const hhmm_ticks *tk, const hhmm_legs *lg)
+{
+    if (!tk || !lg) {
+        set_error("NULL ticks / legs");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    if (tk->n < 3 || tk->n > 0x7fffffffLL) {
+        set_error("n = %lld ticks outside 3..2^31-1", (long long)tk->n);
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    if (!tk->price || !tk->size || !tk->time) {
+        set_error("price, size and time are required");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    if (lg->capacity < 0) {
+        set_error("negative leg capacity");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    return HHMM_OK;
+}
+
+hhmm_status hhmm_features_workspace_size(int64_t n, size_t *bytes)
+{
+    if (!bytes || n < 0) {
+        set_error("bad argument");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    *bytes = features_workspace_bytes(n);
+    return HHMM_OK;
+}
+
+hhmm_status hhmm_extract_features_device(const hhmm_ticks *ticks, hhmm_legs *legs, void *workspace,
+                                         size_t workspace_bytes_, void *stream)
+{
+    hhmm_status s = check_ticks(ticks, legs);
+    if (s != HHMM_OK)
+        return s;
+    if ((s = check_device()) != HHMM_OK)
+        return s;
+    return features_run_device(ticks, legs, workspace, workspace_bytes_, (hipStream_t)stream);
+}
+
+hhmm_status hhmm_extract_features(const hhmm_ticks *ticks, hhmm_legs *legs, int device)
+{
+    hhmm_status s = check_ticks(ticks, legs);
+    if (s != HHMM_OK)
+        return s;
+    if ((s = check_device()) != HHMM_OK)
+        return s;
+    int dev = device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess)
+        return hip_fail(hipGetLastError(), "hipGetDevice");
+    hipError_t e = hipSetDevice(dev);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipSetDevice");
+    const int64_t n = ticks->n;
+    const int64_t cap = legs->capacity;
+    std::vector<void *> owned;
+    auto cleanup = [&]() {
+        for (void *p : owned)
+            pool_put(p);
+    };
+    auto get = [&](size_t bytes) -> void * {
+        void *p = pool_get(dev, bytes ? bytes : 8);
+        if (p)
+            owned.push_back(p);
+        return p;
+    };
+    hhmm_ticks dt = *ticks;
+    const double *hin[3] = {ticks->price, ticks->size, ticks->time};
+    const double **din[3] = {&dt.price, &dt.size, &dt.time};
+    for (int i = 0; i < 3; ++i) {
+        void *p = get(sizeof(double) * (size_t)n);
+        if (!p) {
+            cleanup();
+            set_error("device allocation failed (ticks)");
+            return HHMM_ERR_OUT_OF_MEMORY;
+        }
+        e = hipMemcpy(p, hin[i], sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            cleanup();
+            return hip_fail(e, "hipMemcpy H2D (ticks)");
+        }
+        *din[i] = (const double *)p;
+    }
+    hhmm_legs dl = *legs;
+    struct Col {
+        void *host;
+        void **dev;
+        size_t es;
+    } cols[] = {{legs->price, (void **)&dl.price, 8},     {legs->start, (void **)&dl.start, 4},
+                {legs->end, (void **)&dl.end, 4},         {legs->size_av, (void **)&dl.size_av, 8},
+                {legs->f0, (void **)&dl.f0, 4},           {legs->f1, (void **)&dl.f1, 4},
+                {legs->f2, (void **)&dl.f2, 4},           {legs->feature, (void **)&dl.feature, 4},
+                {legs->trend, (void **)&dl.trend, 4},     {legs->x, (void **)&dl.x, 4},
+                {legs->sign, (void **)&dl.sign, 4}};
+    for (auto &c : cols) {
+        if (!c.host || cap == 0) {
+            *c.dev = nullptr;
+            continue;
+        }
+        void *p = get(c.es * (size_t)cap);
+        if (!p) {
+            cleanup();
+            set_error("device allocation failed (legs)");
+            return HHMM_ERR_OUT_OF_MEMORY;
+        }
+        *c.dev = p;
+    }
+    const size_t wsb = features_workspace_bytes(n);
+    void *ws = get(wsb);
+    if (!ws) {
+        cleanup();
+        set_error("workspace allocation of %zu bytes failed", wsb);
+        return HHMM_ERR_OUT_OF_MEMORY;
+    }
+    s = features_run_device(&dt, &dl, ws, wsb, nullptr);
+    legs->n_legs = dl.n_legs;
+    if (s == HHMM_OK) {
+        for (auto &c : cols) {
+            if (!*c.dev)
+                continue;
+            e = hipMemcpy(c.host, *c.dev, c.es * (size_t)dl.n_legs, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                cleanup();
+                return hip_fail(e, "hipMemcpy D2H (legs)");
+            }
+        }
+    }
+    cleanup();
+    return s;
+}
+
+} // extern "C"

@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "hhmm.h"
+#include "hhmm_features.h"
 
 namespace hhmm {
 
@@ -130,5 +131,9 @@ hhmm_status join_stream(hipStream_t st, hipStream_t side);
 hhmm_status selftest_cr_math(const double *in, double *out, int64_t n, int which);
 
 void set_error(const char *fmt, ...);
+
+/* Tick -> zig-zag -> leg feature extractor (hhmm_features.hip). */
+size_t features_workspace_bytes(int64_t n);
+hhmm_status features_run_device(const hhmm_ticks *tk, hhmm_legs *lg, void *ws, size_t ws_bytes, hipStream_t st);
 
 } // namespace hhmm

@@ -96,3 +96,24 @@ def log_array(x, variant="cr"):
     lib.hhmm_oracle_log_array(x.ctypes.data_as(C.POINTER(C.c_double)),
                               y.ctypes.data_as(C.POINTER(C.c_double)), x.size)
     return y
+
+
+LEG_FIELDS = {"price": "f64", "start": "i32", "end": "i32", "size_av": "f64", "f0": "i32", "f1": "i32",
+              "f2": "i32", "feature": "i32", "trend": "i32", "x": "i32", "sign": "i32"}
+
+
+def extract_features(price, size, time, alpha=0.25, variant="cr"):
+    """Sequential oracle of tayal2009/R/feature-extraction.R:8-133 -> dict of leg columns."""
+    import numpy as np
+    from hhmm_amd import features as F
+    lib = load(variant)
+    lib.hhmm_oracle_extract_features.argtypes = [C.POINTER(F.Ticks), C.POINTER(F.Legs)]
+    lib.hhmm_oracle_extract_features.restype = C.c_int
+    tk, keep = F.make_ticks(price, size, time, alpha)
+    n = tk.n
+    legs, out = F.make_legs(n)
+    st = lib.hhmm_oracle_extract_features(C.byref(tk), C.byref(legs))
+    if st != 0:
+        raise RuntimeError(f"oracle extract_features status {st} (legs {legs.n_legs})")
+    m = legs.n_legs
+    return {k: v[:m].copy() for k, v in out.items()}

@@ -14,19 +14,24 @@ from hhmm_amd import _abi, api, synth
 
 REPO = pathlib.Path(__file__).resolve().parent.parent
 HEADER = REPO / "include" / "hhmm.h"
+HEADERS = sorted((REPO / "include").glob("*.h"))
 
 
 def declared_functions():
-    text = HEADER.read_text()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(hhmm_[a-z0-9_]+)\s*\(", text)))
+    """Every function any include/*.h declares (hhmm.h, hhmm_features.h)."""
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names |= set(re.findall(r"\b(hhmm_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_declares_entry_points():
     names = declared_functions()
     for n in ("hhmm_run", "hhmm_run_device", "hhmm_workspace_size", "hhmm_validate", "hhmm_version",
               "hhmm_last_error", "hhmm_init", "hhmm_shutdown", "hhmm_num_pairs", "hhmm_selftest_cr_log",
-              "hhmm_selftest_cr_exp"):
+              "hhmm_selftest_cr_exp", "hhmm_extract_features", "hhmm_extract_features_device",
+              "hhmm_features_workspace_size"):
         assert n in names
 
 
@@ -41,13 +46,17 @@ def test_library_exports_every_declared_symbol(engine):
 
 
 def _c_layout(tmp_path):
+    from hhmm_amd import features as F
     fields = {
+        "hhmm_ticks": [f[0] for f in F.Ticks._fields_],
+        "hhmm_legs": [f[0] for f in F.Legs._fields_],
         "hhmm_data": [f[0] for f in _abi.Data._fields_],
         "hhmm_draws": [f[0] for f in _abi.Draws._fields_],
         "hhmm_request": [f[0] for f in _abi.Request._fields_],
         "hhmm_result": [f[0] for f in _abi.Result._fields_],
     }
-    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "hhmm.h"', "int main(void){"]
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "hhmm.h"', '#include "hhmm_features.h"',
+           "int main(void){"]
     for st, fs in fields.items():
         src.append(f'printf("{st} sizeof %zu\\n", sizeof({st}));')
         for f in fs:
@@ -63,8 +72,9 @@ def _c_layout(tmp_path):
 
 def test_struct_layout_matches_header(tmp_path):
     lay = _c_layout(tmp_path)
+    from hhmm_amd import features as F
     for cname, cls in (("hhmm_data", _abi.Data), ("hhmm_draws", _abi.Draws), ("hhmm_request", _abi.Request),
-                       ("hhmm_result", _abi.Result)):
+                       ("hhmm_result", _abi.Result), ("hhmm_ticks", F.Ticks), ("hhmm_legs", F.Legs)):
         assert lay[(cname, "sizeof")] == C.sizeof(cls), cname
         for f, _ in cls._fields_:
             assert lay[(cname, f)] == getattr(cls, f).offset, (cname, f)
