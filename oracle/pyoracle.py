@@ -117,3 +117,17 @@ def extract_features(price, size, time, alpha=0.25, variant="cr"):
         raise RuntimeError(f"oracle extract_features status {st} (legs {legs.n_legs})")
     m = legs.n_legs
     return {k: v[:m].copy() for k, v in out.items()}
+
+
+def neighbouring_forecast(x, oblik_t, h=1, threshold=0.05):
+    """Sequential oracle of hassan2005/R/forecast.R:1-31 (long-double sums, libm exp)."""
+    import numpy as np
+    from hhmm_amd import forecast as Fc
+    lib = load("libm")
+    lib.hhmm_oracle_neighbouring_forecast.argtypes = [C.POINTER(Fc.ForecastRequest), C.c_void_p]
+    lib.hhmm_oracle_neighbouring_forecast.restype = C.c_int
+    req, _keep, P = Fc.make_request(x, oblik_t, h, threshold)
+    out = np.empty(P)
+    if lib.hhmm_oracle_neighbouring_forecast(C.byref(req), out.ctypes.data) != 0:
+        raise RuntimeError("oracle rejected the forecast request")
+    return out
