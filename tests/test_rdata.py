@@ -1,0 +1,98 @@
+"""RDX2 reader for the reference's tick files (SURVEY.md §8 F1 input side;
+tayal2009/main.R:47-58 loads tayal2009/data/<SYM>/*.RData with `load()`).
+
+CPU only.  A hand-serialised xts (the same layout the reference's files carry:
+REALSXP matrix + dim / dimnames / index / class attributes, XDR, gzip) checks
+the decoder everywhere; when /root/reference is present the real G.TO files
+are decoded and pushed through the feature oracle, which must agree with the
+R-semantics transcription (tests/test_features.py) on real ticks.  The data
+(CC-BY-NC, tayal2009/data/LICENSE.md) is read in place, never copied.
+"""
+import gzip
+import pathlib
+import struct
+
+import numpy as np
+import pytest
+
+from hhmm_amd import rdata
+
+DATA = pathlib.Path("/root/reference/tayal2009/data")
+
+
+def _i(v):
+    return struct.pack(">i", v)
+
+
+def _flags(t, attr=False, tag=False, obj=False):
+    return _i(t | (1 << 9 if attr else 0) | (1 << 10 if tag else 0) | (1 << 8 if obj else 0))
+
+
+def _charsxp(s):
+    b = s.encode()
+    return _i(0x00040009) + _i(len(b)) + b
+
+
+def _sym(name):
+    return _i(rdata.SYMSXP) + _charsxp(name)
+
+
+def _strsxp(vals):
+    return _i(rdata.STRSXP) + _i(len(vals)) + b"".join(_charsxp(v) for v in vals)
+
+
+def _real(vals, attrs=b""):
+    v = np.asarray(vals, dtype=">f8")
+    return _flags(rdata.REALSXP, attr=bool(attrs)) + _i(v.size) + v.tobytes() + attrs
+
+
+def _pairlist(items):
+    out = b""
+    for tag, val in items:
+        out += _flags(rdata.LISTSXP, tag=True) + _sym(tag) + val
+    return out + _i(rdata.NILVALUE)
+
+
+def _xts_file(name, price, size, index):
+    n = len(price)
+    dim = _flags(rdata.INTSXP) + _i(2) + _i(n) + _i(2)
+    dimnames = _flags(rdata.VECSXP) + _i(2) + _i(rdata.NILVALUE) + _strsxp(["PRICE", "SIZE"])
+    attrs = _pairlist([("dim", dim), ("dimnames", dimnames), ("index", _real(index)),
+                       ("class", _strsxp(["xts", "zoo"]))])
+    body = _real(np.concatenate([price, size]), attrs)
+    raw = b"RDX2\nX\n" + _i(2) + _i(0x030303) + _i(0x020300) + _pairlist([(name, body)])
+    return gzip.compress(raw)
+
+
+def test_reader_roundtrip(tmp_path):
+    price = np.array([10.0, np.nan, 10.01, 10.0, 9.99])
+    size = np.array([100.0, 200.0, 300.0, np.nan, 500.0])
+    index = 1.17802622e9 + np.arange(5.0)
+    f = tmp_path / "2007.05.01.X.TO.RData"
+    f.write_bytes(_xts_file("X.TO", price, size, index))
+    objs = rdata.read_rdata(f)
+    assert list(objs) == ["X.TO"]
+    idx, cols = rdata.xts_columns(objs["X.TO"])
+    assert list(cols) == ["PRICE", "SIZE"] and np.array_equal(idx, index)
+    p, s, t = rdata.load_ticks(f)  # na.omit drops rows 2 and 4
+    assert np.array_equal(p, [10.0, 10.01, 9.99]) and np.array_equal(s, [100.0, 300.0, 500.0])
+    assert np.array_equal(t, index[[0, 2, 4]])
+
+
+def test_reader_refuses_code(tmp_path):
+    raw = b"RDX2\nX\n" + _i(2) + _i(0) + _i(0) + _flags(rdata.LISTSXP, tag=True) + _sym("f") + _i(3)
+    f = tmp_path / "closure.RData"
+    f.write_bytes(raw)
+    with pytest.raises(ValueError):
+        rdata.read_rdata(f)
+
+
+@pytest.mark.skipif(not DATA.exists(), reason="reference tick data not present (GPU box)")
+def test_real_ticks_through_feature_oracle(oracle):
+    import test_features
+    files = sorted((DATA / "G.TO").glob("*.RData"))[:3]
+    price, size, time = rdata.load_ticks(files)
+    assert price.size > 10_000
+    assert (size == np.round(size)).all()  # integer volumes: R's long-double sum is exact in double
+    got = oracle.extract_features(price, size, time, alpha=0.25)
+    test_features._assert_same(got, test_features.transcribe(price, size, time, 0.25))
