@@ -14,16 +14,20 @@
  *   2. leg_scan_kernel     one workgroup: exclusive scan of the tile counts;
  *   3. leg_scatter_kernel  the change-point tick indices in tick order (wave
  *                          ballot + popcount prefix, LDS wave offsets);
- *   4. leg_rows_kernel     lane per leg: start / end / closing price (:30-36),
- *                          size.av (:41-47) with R's difftime unit round trip;
- *   5. leg_features_kernel lane per leg: f0 (:50-51), f1 (:55-70), f2 (:73-89),
- *                          leg code (:92-125), trend (:128-130), and the Tayal
- *                          data coding x / sign (tayal2009/main.R:85-89).
+ *   4. leg_kernel          lane per leg: start / end / closing price (:30-36),
+ *                          size.av (:41-47) with R's difftime unit round trip,
+ *                          kept in LDS with a 4 + 1 leg halo; then f0 (:50-51),
+ *                          f1 (:55-70), f2 (:73-89), leg code (:92-125), trend
+ *                          (:128-130) and the Tayal coding x / sign
+ *                          (tayal2009/main.R:85-89).
  *
  * Bytes per tick (algorithmic): price 8 + size 8 (+ time 16 per leg and
  * 64 B of leg columns per leg).  The change flags need price[t-1], price[t-2]:
  * neighbouring lanes' loads, served from L1/L2, so price crosses HBM twice
- * (count + scatter) -- a single-pass decoupled look-back scan is the next step.
+ * (count + scatter).  A single-pass decoupled look-back variant (ticketed
+ * tiles, wave-parallel look-back over 64 predecessors) was measured at
+ * 5.2 ms against 1.69 ms for this three-kernel form on 10^8 ticks: the
+ * look-back chain through L2 dominates at 24k tiles.
  */
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -176,31 +180,22 @@ struct LegArgs {
     double alpha;
     const int32_t *chg;
     const int32_t *total; /* device: number of legs */
-    double *lp, *sav;     /* workspace copies of price / size_av per leg */
     double *o_price, *o_size_av;
     int32_t *o_start, *o_end, *o_f0, *o_f1, *o_f2, *o_feature, *o_trend, *o_x, *o_sign;
 };
 
-__global__ void __launch_bounds__(kFeatBlock) leg_rows_kernel(const LegArgs a)
+/* Row r of the zig-zag (0 <= r < m): closing price and size.av. */
+__device__ __forceinline__ void leg_row(const LegArgs &a, int64_t m, int64_t r, double &p, double &sav, int64_t &s,
+                                        int64_t &e)
 {
-    const int64_t m = *a.total;
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= m)
-        return;
     const int64_t cr = a.chg[r];
-    const double p = a.price[cr - 2];             /* price[which(direction.chg) - 1] (:30) */
-    const int64_t s = (r == 0) ? 1 : a.chg[r - 1]; /* start (:33) */
-    const int64_t e = (r == m - 1) ? a.n : cr - 1; /* end (:35-36) */
+    p = a.price[cr - 2];                    /* price[which(direction.chg) - 1] (:30) */
+    s = (r == 0) ? 1 : a.chg[r - 1];        /* start (:33) */
+    e = (r == m - 1) ? a.n : cr - 1;        /* end (:35-36) */
     double acc = 0.0;
     for (int64_t i = s - 1; i < e; ++i)
         acc += a.size[i];
-    const double sav = acc / (difftime_secs(a.time[e - 1], a.time[s - 1]) + 1.0);
-    a.lp[r] = p;
-    a.sav[r] = sav;
-    if (a.o_price) a.o_price[r] = p;
-    if (a.o_start) a.o_start[r] = (int32_t)s;
-    if (a.o_end) a.o_end[r] = (int32_t)e;
-    if (a.o_size_av) a.o_size_av[r] = sav;
+    sav = acc / (difftime_secs(a.time[e - 1], a.time[s - 1]) + 1.0); /* size.av (:41-47) */
 }
 
 /* ifelse(ratio - 1 > alpha, 1, ifelse(1 - ratio > alpha, -1, 0)), NA (NaN) -> 2 (:77-79). */
@@ -222,19 +217,46 @@ __constant__ int8_t kLegCode[2][3][3] = {
      {13, 14, 15},
      {10, 12, 17}}};
 
-__global__ void __launch_bounds__(kFeatBlock) leg_features_kernel(const LegArgs a)
+/* One workgroup = legs [r0, r0 + kFeatBlock): every lane forms its own row
+ * (start / end / price / size.av) into LDS, plus a halo of 4 legs before and
+ * 1 after (the f0 / f1 / ratio stencils), then the features -- the per-leg
+ * state never leaves the CU. */
+constexpr int kHaloLo = 4, kHaloHi = 1;
+
+__global__ void __launch_bounds__(kFeatBlock) leg_kernel(const LegArgs a)
 {
+    __shared__ double s_lp[kFeatBlock + kHaloLo + kHaloHi];
+    __shared__ double s_sav[kFeatBlock + kHaloLo + kHaloHi];
     const int64_t m = *a.total;
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * kFeatBlock;
+    for (int k = threadIdx.x; k < kFeatBlock + kHaloLo + kHaloHi; k += kFeatBlock) {
+        const int64_t r = r0 - kHaloLo + k;
+        double p = 0.0, sav = 0.0;
+        if (r >= 0 && r < m) {
+            int64_t st, en;
+            leg_row(a, m, r, p, sav, st, en);
+            if (k >= kHaloLo && k < kHaloLo + kFeatBlock) {
+                if (a.o_price) a.o_price[r] = p;
+                if (a.o_start) a.o_start[r] = (int32_t)st;
+                if (a.o_end) a.o_end[r] = (int32_t)en;
+                if (a.o_size_av) a.o_size_av[r] = sav;
+            }
+        }
+        s_lp[k] = p;
+        s_sav[k] = sav;
+    }
+    __syncthreads();
+    const int64_t r = r0 + threadIdx.x;
     if (r >= m)
         return;
-    const double *lp = a.lp;
+    const double *lp = s_lp + kHaloLo + threadIdx.x;  /* lp[j] = price of leg r + j */
+    const double *sv = s_sav + kHaloLo + threadIdx.x;
     /* f0 (:50-51): lag(price) < price ? max : min; f0[1] = opposite of f0[2] */
-    const int f0 = (r == 0) ? ((lp[0] < lp[1]) ? -1 : 1) : ((lp[r - 1] < lp[r]) ? 1 : -1);
+    const int f0 = (r == 0) ? ((lp[0] < lp[1]) ? -1 : 1) : ((lp[-1] < lp[0]) ? 1 : -1);
     /* f1 (:55-70) */
     int f1 = 0;
     if (r >= 4) {
-        const double e0 = lp[r - 4], e1 = lp[r - 3], e2 = lp[r - 2], e3 = lp[r - 1], e4 = lp[r];
+        const double e0 = lp[-4], e1 = lp[-3], e2 = lp[-2], e3 = lp[-1], e4 = lp[0];
         if (e0 < e2 && e2 < e4 && e1 < e3)
             f1 = 1;
         else if (e0 > e2 && e2 > e4 && e1 > e3)
@@ -243,7 +265,7 @@ __global__ void __launch_bounds__(kFeatBlock) leg_features_kernel(const LegArgs 
     /* f2 (:73-89): assignments only where every comparison is TRUE (NA never assigns) */
     int f2 = 0;
     if (r >= 2) {
-        const double v0 = a.sav[r], v1 = a.sav[r - 1], v2 = a.sav[r - 2];
+        const double v0 = sv[0], v1 = sv[-1], v2 = sv[-2];
         const int s1 = discretize(v0 / v1, a.alpha), s2 = discretize(v0 / v2, a.alpha),
                   s3 = discretize(v1 / v2, a.alpha);
         const bool ok = s1 != 2 && s2 != 2 && s3 != 2;
@@ -269,8 +291,7 @@ static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t features_workspace_bytes(int64_t n)
 {
-    return align256(sizeof(int32_t) * (size_t)(feat_tiles(n) + 1)) + align256(sizeof(int32_t) * (size_t)n) +
-           2 * align256(sizeof(double) * (size_t)n);
+    return align256(sizeof(int32_t) * (size_t)(feat_tiles(n) + 1)) + align256(sizeof(int32_t) * (size_t)n);
 }
 
 /* Enqueues the pipeline on `st` (device pointers); returns the leg count via
@@ -287,10 +308,6 @@ hhmm_status features_run_device(const hhmm_ticks *tk, hhmm_legs *lg, void *ws, s
     int32_t *counts = reinterpret_cast<int32_t *>(w);
     w += align256(sizeof(int32_t) * (size_t)(nt + 1));
     int32_t *chg = reinterpret_cast<int32_t *>(w);
-    w += align256(sizeof(int32_t) * (size_t)n);
-    double *lp = reinterpret_cast<double *>(w);
-    w += align256(sizeof(double) * (size_t)n);
-    double *sav = reinterpret_cast<double *>(w);
 
     hipLaunchKernelGGL(leg_count_kernel, dim3((unsigned)nt), dim3(kFeatBlock), 0, st, tk->price, n, counts);
     hipLaunchKernelGGL(leg_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nt);
@@ -322,8 +339,6 @@ hhmm_status features_run_device(const hhmm_ticks *tk, hhmm_legs *lg, void *ws, s
     a.alpha = tk->alpha;
     a.chg = chg;
     a.total = counts + nt;
-    a.lp = lp;
-    a.sav = sav;
     a.o_price = lg->price;
     a.o_size_av = lg->size_av;
     a.o_start = lg->start;
@@ -336,8 +351,7 @@ hhmm_status features_run_device(const hhmm_ticks *tk, hhmm_legs *lg, void *ws, s
     a.o_x = lg->x;
     a.o_sign = lg->sign;
     const dim3 grid((unsigned)((m + kFeatBlock - 1) / kFeatBlock));
-    hipLaunchKernelGGL(leg_rows_kernel, grid, dim3(kFeatBlock), 0, st, a);
-    hipLaunchKernelGGL(leg_features_kernel, grid, dim3(kFeatBlock), 0, st, a);
+    hipLaunchKernelGGL(leg_kernel, grid, dim3(kFeatBlock), 0, st, a);
     e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("feature extraction launch: %s", hipGetErrorString(e));
