@@ -131,3 +131,19 @@ def neighbouring_forecast(x, oblik_t, h=1, threshold=0.05):
     if lib.hhmm_oracle_neighbouring_forecast(C.byref(req), out.ctypes.data) != 0:
         raise RuntimeError("oracle rejected the forecast request")
     return out
+
+
+def constrain_draws(model, theta, K, L=0, M=0, variant="cr"):
+    """Oracle of the parameters-block constraining transforms (oracle/params_oracle.c)."""
+    import numpy as np
+    from hhmm_amd import params as Pm
+    lib = load(variant)
+    lib.hhmm_oracle_constrain.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_void_p,
+                                          C.POINTER(Pm.ParamOut)]
+    lib.hhmm_oracle_constrain.restype = C.c_int64
+    th = np.asfortranarray(theta, dtype=np.float64)
+    po, out = Pm.alloc_outputs(model, th.shape[0], K, L, M)
+    n = lib.hhmm_oracle_constrain(_abi.MODELS[model], K, L, M, th.shape[0], th.ctypes.data, C.byref(po))
+    if n != th.shape[1]:
+        raise RuntimeError(f"oracle consumed {n} values per draw, theta has {th.shape[1]}")
+    return out

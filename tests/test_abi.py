@@ -32,7 +32,8 @@ def test_header_declares_entry_points():
               "hhmm_last_error", "hhmm_init", "hhmm_shutdown", "hhmm_num_pairs", "hhmm_selftest_cr_log",
               "hhmm_selftest_cr_exp", "hhmm_extract_features", "hhmm_extract_features_device",
               "hhmm_features_workspace_size", "hhmm_neighbouring_forecast",
-              "hhmm_neighbouring_forecast_device"):
+              "hhmm_neighbouring_forecast_device", "hhmm_num_unconstrained", "hhmm_constrain_draws",
+              "hhmm_constrain_draws_device"):
         assert n in names
 
 
@@ -49,17 +50,19 @@ def test_library_exports_every_declared_symbol(engine):
 def _c_layout(tmp_path):
     from hhmm_amd import features as F
     from hhmm_amd import forecast as Fc
+    from hhmm_amd import params as Pm
     fields = {
         "hhmm_ticks": [f[0] for f in F.Ticks._fields_],
         "hhmm_legs": [f[0] for f in F.Legs._fields_],
         "hhmm_forecast_request": [f[0] for f in Fc.ForecastRequest._fields_],
+        "hhmm_param_out": [f[0] for f in Pm.ParamOut._fields_],
         "hhmm_data": [f[0] for f in _abi.Data._fields_],
         "hhmm_draws": [f[0] for f in _abi.Draws._fields_],
         "hhmm_request": [f[0] for f in _abi.Request._fields_],
         "hhmm_result": [f[0] for f in _abi.Result._fields_],
     }
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "hhmm.h"', '#include "hhmm_features.h"',
-           '#include "hhmm_forecast.h"',
+           '#include "hhmm_forecast.h"', '#include "hhmm_params.h"',
            "int main(void){"]
     for st, fs in fields.items():
         src.append(f'printf("{st} sizeof %zu\\n", sizeof({st}));')
@@ -78,9 +81,10 @@ def test_struct_layout_matches_header(tmp_path):
     lay = _c_layout(tmp_path)
     from hhmm_amd import features as F
     from hhmm_amd import forecast as Fc
+    from hhmm_amd import params as Pm
     for cname, cls in (("hhmm_data", _abi.Data), ("hhmm_draws", _abi.Draws), ("hhmm_request", _abi.Request),
                        ("hhmm_result", _abi.Result), ("hhmm_ticks", F.Ticks), ("hhmm_legs", F.Legs),
-                       ("hhmm_forecast_request", Fc.ForecastRequest)):
+                       ("hhmm_forecast_request", Fc.ForecastRequest), ("hhmm_param_out", Pm.ParamOut)):
         assert lay[(cname, "sizeof")] == C.sizeof(cls), cname
         for f, _ in cls._fields_:
             assert lay[(cname, f)] == getattr(cls, f).offset, (cname, f)
