@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--pars", default=None,
                     help="c3-c5 probes: comma-separated outputs instead of the workload's")
     ap.add_argument("--flags", type=int, default=0, help="c3-c5 probes: hhmm_request.flags")
+    ap.add_argument("--vit-priority", type=int, default=0,
+                    help="stream priority of the Viterbi stream (torch: -1 high, 0 default)")
+    ap.add_argument("--fb-first", action="store_true", help="enqueue the forward-backward before the Viterbi")
+    ap.add_argument("--vit-flags", type=int, default=0,
+                    help="hhmm_request.flags of the Viterbi request (e.g. 16 = HHMM_FLAG_VIT_STATES)")
     ap.add_argument("--split", action="store_true",
                     help="run the forward-backward and Viterbi one after the other on one stream")
     return ap.parse_args()
@@ -225,14 +230,16 @@ def main():
     P, T = a.pairs, a.T
     x, draws = make_batch(P, T, a.seed + 7919 * rank, dev)
     run = DeviceRun(lib, x, draws, P, T, dev)
+    run.reqs["viterbi"][0].flags = a.vit_flags
     torch.cuda.synchronize()
 
     s0 = torch.cuda.current_stream()
-    s1 = torch.cuda.Stream()
+    s1 = torch.cuda.Stream(priority=a.vit_priority)
 
     def step(ev=None):
-        """One pass of the hot path.  ev = 5 events: step start, fb start/end
-        (recorded on fb's stream), viterbi start/end (on viterbi's stream)."""
+        """One pass of the hot path.  ev = 6 events: step start, fb start/end
+        (recorded on fb's stream), viterbi start/end (on viterbi's stream),
+        and the join (fb's stream, after waiting for the Viterbi)."""
         if ev:
             ev[0].record(s0)
         if a.split:
@@ -249,20 +256,29 @@ def main():
         fork = torch.cuda.Event()
         fork.record(s0)
         s1.wait_event(fork)
+
+        def fb():
+            if ev:
+                ev[1].record(s0)
+            run.launch("fb")
+            if ev:
+                ev[2].record(s0)
+
+        if a.fb_first:
+            fb()
         with torch.cuda.stream(s1):
             if ev:
                 ev[3].record(s1)
             run.launch("viterbi")
             if ev:
                 ev[4].record(s1)
-        if ev:
-            ev[1].record(s0)
-        run.launch("fb")
-        if ev:
-            ev[2].record(s0)
+        if not a.fb_first:
+            fb()
         join = torch.cuda.Event()
         join.record(s1)
         s0.wait_event(join)
+        if ev:
+            ev[5].record(s0)  # after the join: the pair's end whichever kernel finishes last
         if world > 1:
             import torch.distributed as dist
             s = run.out["loglik"].sum().reshape(1)
@@ -274,7 +290,7 @@ def main():
     if a.check:
         check_slice(run, x, draws, P, T)
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(a.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(a.steps)]
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -288,7 +304,7 @@ def main():
     elapsed = time.perf_counter() - t0
     fb_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     vit_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
-    pair_ms = float(np.mean([e[0].elapsed_time(e[4]) if a.split else e[0].elapsed_time(e[2]) for e in evs]))
+    pair_ms = float(np.mean([e[0].elapsed_time(e[4]) if a.split else e[0].elapsed_time(e[5]) for e in evs]))
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -331,7 +347,7 @@ def main():
             "config": {"workload": "C2 hmm-multinom K=4 L=9, 1M pairs x T=1000 per GPU (zip pairing)",
                        "pairs_per_gpu": P, "T": T, "outputs": "gamma_tk zstar_t loglik logp_zstar",
                        "parallelism": f"pairs sharded over {world} GPU(s)",
-                       "schedule": "fb and viterbi sequential" if a.split else "fb || viterbi (two streams)"},
+                       "schedule": "fb and viterbi sequential" if a.split else ("fb || viterbi (two streams" + (", fb enqueued first" if a.fb_first else "") + (f", viterbi stream priority {a.vit_priority}" if a.vit_priority else "") + ")")},
             "whole_step_roofline_frac": whole_b * world * units * a.steps / elapsed / (HBM_PEAK * world),
             "kernels_ms": kernels_ms,
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
