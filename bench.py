@@ -310,6 +310,19 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     bad = int((run.out["pair_status"] != 0).sum().item())
+    # after the timed region: each kernel alone once (untimed for `value`), so the
+    # line also carries the north star's "batched forward-backward" roofline
+    solo = {}
+    for name in ("fb", "viterbi"):
+        ts = []
+        for _ in range(3):  # back to back on one stream; median of three launches
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s0)
+            run.launch(name)
+            e1.record(s0)
+            ts.append((e0, e1))
+        torch.cuda.synchronize()
+        solo[name] = float(np.median([e0.elapsed_time(e1) for e0, e1 in ts]))
 
     if rank == 0:
         fb_b, vit_b, whole_b = bytes_per_step(T)
@@ -355,6 +368,11 @@ def main():
                          "traffic": traffic, "algorithmic_bytes_per_series_timestep": dom_b,
                          "duration_ms": dom_ms},
             "pair_failures": bad,
+            "alone_after_timing": {
+                "fb_kernel": {"ms": solo["fb"], "algorithmic_bytes_per_series_timestep": fb_b,
+                              "roofline_frac": fb_b * units / (solo["fb"] * 1e-3) / HBM_PEAK},
+                "viterbi_kernel": {"ms": solo["viterbi"], "algorithmic_bytes_per_series_timestep": vit_b,
+                                   "roofline_frac": vit_b * units / (solo["viterbi"] * 1e-3) / HBM_PEAK}},
         }
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(T, a.cpu_seconds, a.seed)

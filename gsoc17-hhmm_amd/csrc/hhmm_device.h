@@ -11,6 +11,7 @@
 
 #ifndef HHMM_MATH_FN
 #define HHMM_MATH_FN static __device__ __forceinline__
+#define HHMM_MATH_COLD static __device__ __attribute__((noinline))
 #define HHMM_MATH_TABLE static __constant__
 #endif
 #include "hhmm_crmath.h"

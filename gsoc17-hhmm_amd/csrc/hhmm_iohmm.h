@@ -230,7 +230,7 @@ __device__ __forceinline__ void io_load(const DevArgs &a, uint32_t n, int t, dou
 }
 
 template <int FAM, int K, int MMAX, bool EXACT>
-__global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
+__device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 {
     HIP_DYNAMIC_SHARED(double2, lds)
     constexpr int BITS = bp_bits(K);
@@ -494,6 +494,23 @@ __global__ void __launch_bounds__(kBlock) iohmm_kernel(const DevArgs a)
         viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dl, word);
 }
 
+/* The regression family's exact sweep needs ~290 registers: uncapped it runs
+ * one wave per SIMD.  Capped at two waves (256 registers, a 144-byte spill)
+ * it ran C3 in 87 ms against 156 ms on one box; the mixture family runs
+ * faster uncapped (C4: 147 against 160 ms), so only the regression kernel
+ * carries the cap. */
+template <int K, int MMAX, bool EXACT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) iohmm_reg_kernel(const DevArgs a)
+{
+    iohmm_sweep<IO_REG, K, MMAX, EXACT>(a);
+}
+
+template <int K, int MMAX, bool EXACT>
+__global__ void __launch_bounds__(kBlock) iohmm_mix_kernel(const DevArgs a)
+{
+    iohmm_sweep<IO_MIX, K, MMAX, EXACT>(a);
+}
+
 /* ------------------------------------------------------------------ */
 /* Host-side launch                                                      */
 /* ------------------------------------------------------------------ */
@@ -511,10 +528,13 @@ static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
     }
     const int threads = 64 * waves;
     const dim3 grid((unsigned)((a.P + threads - 1) / threads));
-    hipLaunchKernelGGL((iohmm_kernel<FAM, K, MMAX, EXACT>), grid, dim3(threads), per_wave * waves, st, a);
+    if constexpr (FAM == IO_REG)
+        hipLaunchKernelGGL((iohmm_reg_kernel<K, MMAX, EXACT>), grid, dim3(threads), per_wave * waves, st, a);
+    else
+        hipLaunchKernelGGL((iohmm_mix_kernel<K, MMAX, EXACT>), grid, dim3(threads), per_wave * waves, st, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        set_error("iohmm_kernel launch: %s", hipGetErrorString(e));
+        set_error("iohmm kernel launch: %s", hipGetErrorString(e));
         return HHMM_ERR_HIP;
     }
     return HHMM_OK;
