@@ -76,6 +76,39 @@ __device__ __forceinline__ const T &at(const T *row, uint32_t byte_off)
     return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(row) + byte_off);
 }
 
+/* Store of a write-once output element (gamma, zstar): no kernel re-reads it,
+ * so it is a nontemporal (streaming) store -- 3 % off both the forward-backward
+ * and the Viterbi at C2 (tools/ab_bench.py, one box, interleaved). */
+template <typename T>
+__device__ __forceinline__ void put_out(T *row, uint32_t byte_off, T v)
+{
+    __builtin_nontemporal_store(v, reinterpret_cast<T *>(reinterpret_cast<char *>(row) + byte_off));
+}
+
+/* Scratch written by one sweep and read back once by the next (alpha
+ * checkpoints, Viterbi back-pointer words).  HHMM_NT_TMP puts streaming hints
+ * on both sides; it is off because it cost the forward-backward 6.5 % at C2
+ * (7.97 against 7.48 ms, the checkpoints are re-read out of the caches) and
+ * left the Viterbi unchanged. */
+template <typename T>
+__device__ __forceinline__ void put_tmp(T *row, uint32_t byte_off, T v)
+{
+#ifdef HHMM_NT_TMP
+    __builtin_nontemporal_store(v, reinterpret_cast<T *>(reinterpret_cast<char *>(row) + byte_off));
+#else
+    at(row, byte_off) = v;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ T get_tmp(const T *row, uint32_t byte_off)
+{
+#ifdef HHMM_NT_TMP
+    return __builtin_nontemporal_load(reinterpret_cast<const T *>(reinterpret_cast<const char *>(row) + byte_off));
+#else
+    return at(row, byte_off);
+#endif
+}
+
 /* Power-of-two renormalisation of a K-vector after every step: the largest
  * entry is brought into [0.5, 1) by an exact ldexp and the removed exponent
  * is accumulated in `ex`.  Keeping the max near 1 (rather than letting it
@@ -138,7 +171,7 @@ __device__ __forceinline__ void store_tk(double *out, const DevArgs &a, int64_t 
 {
 #pragma unroll
     for (int k = 0; k < K; ++k)
-        at(out + a.P * ((int64_t)t + (int64_t)a.Tout * k), (uint32_t)p * 8u) = v[k];
+        put_out(out + a.P * ((int64_t)t + (int64_t)a.Tout * k), (uint32_t)p * 8u, v[k]);
 }
 
 /* 1/x to ~1 ulp: v_rcp_f64 + two Newton steps (tolerance 1e-9 outputs only);
@@ -238,14 +271,14 @@ __device__ __forceinline__ void vit_back_flush(const DevArgs &a, int64_t p, int 
                           (zb[4 * m + 2] & -(int)(j == 2)) | (zb[4 * m + 3] & -(int)(j == 3));
             const int t = t0 + 4 * m + j;
             if (t < Tp)
-                at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = v;
+                put_out(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u, v);
         }
     } else {
 #pragma unroll
         for (int u = 0; u < CV; ++u) {
             const int t = t0 + u;
             if (t < Tp)
-                at(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u) = zb[u];
+                put_out(a.zstar + a.P * (int64_t)t, (uint32_t)p * 4u, zb[u]);
         }
     }
 }
@@ -266,7 +299,7 @@ __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, in
     const int nfull = Tw_min / CV;
     const int nchunk = (Tw_max + CV - 1) / CV;
     if ((Tp - 1) % SPW != SPW - 1) /* partial last word */
-        a.bp[p + a.P * (int64_t)((Tp - 1) / SPW)] = word;
+        put_tmp(a.bp + a.P * (int64_t)((Tp - 1) / SPW), (uint32_t)p * 4u, word);
 
     /* logp_zstar = max(delta_tk[T]); zstar[T] = LAST j attaining it (hmm.stan:120-124). */
     const double lp = stan_max_vec<K>(dl);
@@ -298,11 +331,11 @@ __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, in
     const int clast = nchunk - 1;
 #pragma unroll
     for (int i = 0; i < WPC; ++i)
-        w[i] = at(a.bp + a.P * (int64_t)min(max(clast * WPC + i, 0), wmax), (uint32_t)p * 4u);
+        w[i] = get_tmp(a.bp + a.P * (int64_t)min(max(clast * WPC + i, 0), wmax), (uint32_t)p * 4u);
     for (int c = clast; c >= 0; --c) {
 #pragma unroll
         for (int i = 0; i < WPC; ++i)
-            wn[i] = at(a.bp + a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax), (uint32_t)p * 4u);
+            wn[i] = get_tmp(a.bp + a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax), (uint32_t)p * 4u);
         if (c < clast)
             vit_back_flush<CV, QUAD>(a, p, Tp, c + 1, zb);
         if (c < nfull)

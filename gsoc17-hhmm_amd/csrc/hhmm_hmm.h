@@ -556,9 +556,9 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
                 const int64_t row = fb_big(MODE) ? (c - ln.cb) / (kBigChunk / C) : (c - ln.cb);
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    at(a.ckpt + ln.Qs * (row * K + k), (uint32_t)ln.q * 8u) = al[k];
+                    put_tmp(a.ckpt + ln.Qs * (row * K + k), (uint32_t)ln.q * 8u, al[k]);
                 if constexpr (fb_base(MODE) == FB_FULL)
-                    at(a.ckpt_ls + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 8u) = lsc + kLn2 * ex;
+                    put_tmp(a.ckpt_ls + ln.Qs * (int64_t)(c - ln.cb), (uint32_t)ln.q * 8u, lsc + kLn2 * ex);
             }
             if (fb_pack(MODE) && u == 0) {
                 /* the chunk's C <= 8 symbols, 4 bits each, for the backward sweep */
@@ -770,7 +770,7 @@ __device__ __forceinline__ void fb_backward_big(const DevArgs &a, const FbLane<M
         const int bb = max(blk, 0);
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            ck[k] = at(a.ckpt + ln.Qs * ((int64_t)bb * K + k), (uint32_t)ln.q * 8u);
+            ck[k] = get_tmp(a.ckpt + ln.Qs * ((int64_t)bb * K + k), (uint32_t)ln.q * 8u);
 #pragma unroll
         for (int i = 0; i < NW; ++i)
             w[i] = at(a.xpk + ln.Qs * (int64_t)(bb * NW + i), (uint32_t)ln.q * 4u);
@@ -862,9 +862,9 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
         const int cc = clast - cb;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            ck[k] = at(a.ckpt + ln.Qs * ((int64_t)cc * K + k), (uint32_t)ln.q * 8u);
+            ck[k] = get_tmp(a.ckpt + ln.Qs * ((int64_t)cc * K + k), (uint32_t)ln.q * 8u);
         if constexpr (fb_base(MODE) == FB_FULL)
-            ck_ls = at(a.ckpt_ls + ln.Qs * (int64_t)cc, (uint32_t)ln.q * 8u);
+            ck_ls = get_tmp(a.ckpt_ls + ln.Qs * (int64_t)cc, (uint32_t)ln.q * 8u);
     }
     /* FFBS: the caller's uniforms, prefetched one chunk ahead like the observations */
     double uu[fb_ffbs(MODE) ? C : 1], un[fb_ffbs(MODE) ? C : 1];
@@ -888,9 +888,9 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
             const int cc = max(c - 1, cb) - cb;
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                cn[k] = at(a.ckpt + ln.Qs * ((int64_t)cc * K + k), (uint32_t)ln.q * 8u);
+                cn[k] = get_tmp(a.ckpt + ln.Qs * ((int64_t)cc * K + k), (uint32_t)ln.q * 8u);
             if constexpr (fb_base(MODE) == FB_FULL)
-                cn_ls = at(a.ckpt_ls + ln.Qs * (int64_t)cc, (uint32_t)ln.q * 8u);
+                cn_ls = get_tmp(a.ckpt_ls + ln.Qs * (int64_t)cc, (uint32_t)ln.q * 8u);
         }
         if (c < nfull)
             bwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, ck, ck_ls, be, blsc, bex, uu, onext, z);
@@ -1042,7 +1042,7 @@ __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const
             if (!(u == 0 && c == 0))
                 vit_step<MODEL, K>(dl, pp, le, cur[u], word, u % SPW);
             if (u % SPW == SPW - 1) {
-                at(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u) = word;
+                put_tmp(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u, word);
                 word = 0;
             }
         }
@@ -1202,7 +1202,7 @@ __device__ __forceinline__ void sp_flush_words(const DevArgs &a, int64_t p, int 
     for (int i = 0; i < CS / SPW; ++i) {
         const int t = c * CS + i * SPW + SPW - 1;
         if (t < Tp)
-            at(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u) = wb[i];
+            put_tmp(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u, wb[i]);
     }
 }
 
@@ -1588,7 +1588,7 @@ __global__ void __launch_bounds__(kBlock) fb_log_kernel(const DevArgs a)
                 } else if (v == 0) {
 #pragma unroll
                     for (int k = 0; k < K; ++k)
-                        at(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)p * 8u) = u[k];
+                        put_tmp(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)p * 8u, u[k]);
                 }
             }
         }
@@ -1610,7 +1610,7 @@ __global__ void __launch_bounds__(kBlock) fb_log_kernel(const DevArgs a)
         double abuf[C][K];
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            abuf[0][k] = at(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)p * 8u);
+            abuf[0][k] = get_tmp(a.ckpt + a.P * ((int64_t)c * K + k), (uint32_t)p * 8u);
 #pragma unroll
         for (int v = 1; v < C; ++v) {
             if (c * C + v < Tp) {
