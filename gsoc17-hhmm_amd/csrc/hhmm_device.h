@@ -326,9 +326,48 @@ __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, in
      * are wave-uniform, clamped to the allocation (a short lane's extra rows
      * are never consumed) */
     const int wmax = a.Tmax / SPW;
-    uint32_t w[WPC], wn[WPC];
     int zb[CV];
     const int clast = nchunk - 1;
+    if constexpr (QUAD) {
+        /* Few pairs, long T (C5): one wave per SIMD, nothing else hides the
+         * word loads' HBM latency, and one chunk of backtrack (CV steps of
+         * dependent shifts) is far shorter than it.  So the words come in
+         * groups of G chunks, the next group prefetched while this one runs. */
+        constexpr int G = 8;
+        uint32_t w[G * WPC], wn[G * WPC];
+        const int glast = clast / G;
+#pragma unroll
+        for (int i = 0; i < G * WPC; ++i)
+            w[i] = get_tmp(a.bp + a.P * (int64_t)min(max(glast * G * WPC + i, 0), wmax), (uint32_t)p * 4u);
+        for (int g = glast; g >= 0; --g) {
+#pragma unroll
+            for (int i = 0; i < G * WPC; ++i)
+                wn[i] = get_tmp(a.bp + a.P * (int64_t)min(max((g - 1) * G * WPC + i, 0), wmax), (uint32_t)p * 4u);
+#pragma unroll
+            for (int cc = G - 1; cc >= 0; --cc) {
+                const int c = g * G + cc;
+                if (c > clast)
+                    continue;
+                if (c < clast)
+                    vit_back_flush<CV, QUAD>(a, p, Tp, c + 1, zb);
+                uint32_t wc[WPC];
+#pragma unroll
+                for (int i = 0; i < WPC; ++i)
+                    wc[i] = w[cc * WPC + i];
+                if (c < nfull)
+                    vit_back_chunk<K, CV, true>(Tp, c, wc, z, zb);
+                else
+                    vit_back_chunk<K, CV, false>(Tp, c, wc, z, zb);
+            }
+#pragma unroll
+            for (int i = 0; i < G * WPC; ++i)
+                w[i] = wn[i];
+        }
+        if (clast >= 0)
+            vit_back_flush<CV, QUAD>(a, p, Tp, 0, zb);
+        return;
+    }
+    uint32_t w[WPC], wn[WPC];
 #pragma unroll
     for (int i = 0; i < WPC; ++i)
         w[i] = get_tmp(a.bp + a.P * (int64_t)min(max(clast * WPC + i, 0), wmax), (uint32_t)p * 4u);
