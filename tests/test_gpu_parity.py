@@ -223,6 +223,21 @@ def test_viterbi_layouts_ragged(engine, oracle, model, layout):
     compare_all(got, ref, pars + ["pair_status"])
 
 
+@pytest.mark.parametrize("model", ["hmm-multinom", "hhmm-tayal2009"])
+def test_viterbi_states_backtrack_groups(engine, oracle, model):
+    """The state-parallel decoder's backtrack reads its back-pointer words in
+    groups of 8 chunks x 16 steps: series lengths on both sides of one and two
+    group boundaries (ragged within the wave) stay bit-exact with the oracle."""
+    import hhmm_amd
+    N, S, T = 6, 7, 257
+    data, draws = synth.GENERATORS[model](N=N, S=S, T=T)
+    data["T"] = np.array([127, 128, 129, 255, 256, 257], dtype=np.int32)
+    pars = ["zstar_t", "logp_zstar"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=_abi.FLAG_VIT_STATES, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
 @pytest.mark.parametrize("layout", ["lanes", "states"])
 def test_viterbi_layouts_invalid_backpointer(engine, oracle, layout):
     import hhmm_amd
