@@ -499,8 +499,11 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
  * it ran C3 in 87 ms against 156 ms on one box; the mixture family runs
  * faster uncapped (C4: 147 against 160 ms), so only the regression kernel
  * carries the cap. */
+#ifndef HHMM_IO_REG_WAVES
+#define HHMM_IO_REG_WAVES 2
+#endif
 template <int K, int MMAX, bool EXACT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) iohmm_reg_kernel(const DevArgs a)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HHMM_IO_REG_WAVES))) iohmm_reg_kernel(const DevArgs a)
 {
     iohmm_sweep<IO_REG, K, MMAX, EXACT>(a);
 }
