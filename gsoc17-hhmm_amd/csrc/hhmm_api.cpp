@@ -618,6 +618,9 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
 
     s = launch_all(&dreq, &dres, P, ws, nullptr);
     if (s != HHMM_OK) {
+        /* a failed launch may follow one that is still running: drain the
+         * device before the pooled buffers can be handed to another request */
+        (void)hipDeviceSynchronize();
         cleanup();
         return s;
     }

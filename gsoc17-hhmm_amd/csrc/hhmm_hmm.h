@@ -2157,22 +2157,37 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
      * the VALU-bound decoder's workgroups fill in beside the HBM-bound
      * forward-backward's instead of strictly after them. */
     const bool vit = (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) != 0;
+    /* Both launch shapes are checked before either kernel is enqueued, so an
+     * unsupported shape never leaves a kernel running on the side stream
+     * while the caller reclaims its buffers. */
+    if (any_fwd) {
+        LaunchShape chk;
+        if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, chk)) {
+            set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
+            return HHMM_ERR_UNSUPPORTED;
+        }
+    }
     hipStream_t vs = st;
     if (vit && any_fwd && !(a.flags & HHMM_FLAG_NO_FUSE)) {
         s = fork_stream(st, &vs);
         if (s != HHMM_OK)
             return s;
         s = launch_viterbi<MODEL, K>(a, vs);
-        if (s != HHMM_OK)
+        if (s != HHMM_OK) {
+            join_stream(st, vs);
             return s;
+        }
     }
     if (any_fwd) {
         if (a.scan_cl > 0 && !(out & HHMM_OUT_FFBS))
             s = launch_fb_scan<MODEL, K>(a, !needs_backward(MODEL, out), st);
         else
             s = launch_fb<MODEL, K>(a, !needs_backward(MODEL, out), st);
-        if (s != HHMM_OK)
+        if (s != HHMM_OK) {
+            if (vs != st)
+                join_stream(st, vs); /* the caller's stream still orders the running decoder */
             return s;
+        }
     }
     if (vs != st)
         return join_stream(st, vs);

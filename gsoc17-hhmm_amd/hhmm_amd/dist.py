@@ -42,6 +42,17 @@ def slice_series(data, b, e):
     return out
 
 
+def default_device(group=None):
+    """Where the collective buffers live: the rank's current GPU under nccl
+    (RCCL rejects host tensors), the host under gloo."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def slice_draws(draws, b, e):
     return {k: np.asarray(v)[b:e] for k, v in draws.items()}
 
@@ -70,7 +81,7 @@ def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=No
     ldraws = draws if pairing == "grid" else slice_draws(draws, b, e)
     local = compute(model, ldata, ldraws, pars=pars, pairing=pairing) if e > b else {}
 
-    dev = device if device is not None else torch.device("cpu")
+    dev = device if device is not None else default_device(group)
     summed = None
     if "loglik" in pars:
         s_len = S if pairing == "grid" else N
