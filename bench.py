@@ -52,11 +52,14 @@ def parse():
     ap.add_argument("--seed", type=int, default=synth.SEED)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check", action="store_true", help="also check a slice against the oracle")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "f1"],
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the 64-pair oracle check of the timed data (run after warmup, outside the "
+                         "timed region)")
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "f1"],
                     help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
-                         "printed as its own line: c3 iohmm-reg grid, c4 iohmm-hmix + FFBS, c5 Tayal T=1e6 "
-                         "(parallel scan over T); f1 = the tick -> leg feature extractor (SURVEY §8 F1)")
+                         "printed as its own line: c1 hmm Gaussian K=3 T=500, c3 iohmm-reg grid, c4 iohmm-hmix "
+                         "+ FFBS, c5 Tayal T=1e6 (parallel scan over T); f1 = the tick -> leg feature extractor "
+                         "(SURVEY §8 F1)")
     ap.add_argument("--ticks", type=int, default=100_000_000, help="f1: ticks per GPU")
     ap.add_argument("--pars", default=None,
                     help="c3-c5 probes: comma-separated outputs instead of the workload's")
@@ -168,29 +171,46 @@ def bytes_per_step(T):
     return fb, vit, whole
 
 
-def cpu_baseline(T, target_s, seed):
-    """Stanc-faithful CPU oracle (libm log, in-loop log/LSE as Stan) on a
-    bounded sample of the same workload (same shapes, host cores)."""
+def timed_oracle(model, gen, pars, pairing, threads, target_s, n0, cap, uniforms=None):
+    """Times the oracle's libm build on a bounded sample: a calibration run of
+    n0 units (series or draws, per `gen`), then one sized for ~target_s."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
+
+    def run(n, seed_off):
+        data, draws, P, T, u = gen(n, seed_off)
+        t0 = time.perf_counter()
+        pyoracle.gqs(model, data, draws, pars=pars, pairing=pairing, nthreads=threads, variant="libm",
+                     uniforms=u)
+        return time.perf_counter() - t0, P, T
+
+    run(n0, 0)  # warm (page-in, thread pool)
+    dt, P, T = run(n0, 0)
+    n = int(max(n0, min(cap, n0 * target_s / max(dt, 1e-3))))
+    n = (n // threads) * threads or threads
+    dt, P, T = run(n, 1)
+    return P * T / dt, P, T, dt
+
+
+def cpu_baseline(T, target_s, seed):
+    """Stanc-faithful CPU oracle (libm log, in-loop log/LSE as Stan) on a
+    bounded sample of the same workload (same shapes, host cores): all the
+    process's cores (the reported value) and one core beside it."""
     threads = len(os.sched_getaffinity(0))
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
-    n = 8 * threads
-    data, draws = synth.hmm_multinom(N=n, S=n, T=T, K=K, L=L, seed=seed)
-    pyoracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", nthreads=threads, variant="libm")
-    t0 = time.perf_counter()
-    pyoracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", nthreads=threads, variant="libm")
-    dt = time.perf_counter() - t0
-    n2 = int(max(n, min(200_000, n * target_s / max(dt, 1e-3))))
-    n2 = (n2 // threads) * threads or threads
-    data, draws = synth.hmm_multinom(N=n2, S=n2, T=T, K=K, L=L, seed=seed + 1)
-    t0 = time.perf_counter()
-    pyoracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", nthreads=threads, variant="libm")
-    dt = time.perf_counter() - t0
-    return {"value": n2 * T / dt, "unit": "series-timesteps/s", "cores": threads, "kind": "port",
-            "sample": f"{n2} pairs x T={T} (hmm-multinom K=4 L=9, zip), FB+gamma+Viterbi, "
-                      f"{dt:.1f} s on {threads} threads, oracle libm-log build"}
+
+    def gen(n, off):
+        data, draws = synth.hmm_multinom(N=n, S=n, T=T, K=K, L=L, seed=seed + off)
+        return data, draws, n, T, None
+
+    v, P, _, dt = timed_oracle("hmm-multinom", gen, pars, "zip", threads, target_s, 8 * threads, 200_000)
+    v1, P1, _, dt1 = timed_oracle("hmm-multinom", gen, pars, "zip", 1, target_s / 3, 8, 20_000)
+    return {"value": v, "unit": "series-timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{P} pairs x T={T} (hmm-multinom K=4 L=9, zip), FB+gamma+Viterbi, "
+                      f"{dt:.1f} s on {threads} threads, oracle libm-log build",
+            "single_core": {"value": v1, "cores": 1, "sample": f"{P1} pairs x T={T}, {dt1:.1f} s on 1 thread"},
+            "cpu_model": cpu_model()}
 
 
 def load_traffic(kernel, P, T):
@@ -287,8 +307,9 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if a.check:
-        check_slice(run, x, draws, P, T)
+    checked = None
+    if not a.no_check and rank == 0:
+        checked = check_slice(run, x, draws, P, T)
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(a.steps)]
     if world > 1:
@@ -368,6 +389,7 @@ def main():
                          "traffic": traffic, "algorithmic_bytes_per_series_timestep": dom_b,
                          "duration_ms": dom_ms},
             "pair_failures": bad,
+            "check": checked,
             "alone_after_timing": {
                 "fb_kernel": {"ms": solo["fb"], "algorithmic_bytes_per_series_timestep": fb_b,
                               "roofline_frac": fb_b * units / (solo["fb"] * 1e-3) / HBM_PEAK},
@@ -381,11 +403,25 @@ def main():
         dist.destroy_process_group()
 
 
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 # ---------------------------------------------------------------------------
 # The other BASELINE configs (evidence lines; C2 above is the metric)
 # ---------------------------------------------------------------------------
 
 WORKLOADS = {
+    "c1": ("hmm", dict(N=1, S=1000, T=500, K=3), "grid",
+           ["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
+           lambda T, S: 3 * 8 + 4 + 8 / S + (8 * (3 + 9 + 3 + 3) + 16) / T,
+           "C1 hmm Gaussian K=3 T=500, 1 series x 1000 draws (hmm/main.R), grid"),
     # name: (model, generator kwargs per GPU, pairing, outputs, algorithmic bytes per series-timestep
     #        (SURVEY.md §8d), description)
     "c3": ("iohmm-reg", dict(N=1250, S=4000, T=300, K=4, M=4), "grid",
@@ -412,10 +448,7 @@ def other_workload(a, lib, dev, world, rank):
     if a.pars:
         pars = a.pars.split(",")
         desc += f" [probe: outputs {a.pars}, flags {a.flags}]"
-    if model.startswith("iohmm"):
-        data, draws = synth.GENERATORS[model](seed=a.seed + 7919 * rank, **kw)
-    else:
-        data, draws = synth.tayal(seed=a.seed + 7919 * rank, **kw)
+    data, draws = synth.GENERATORS[model](seed=a.seed + 7919 * rank, **kw)
     T = kw["T"]
     # the request's input pointers from the host mirror (outputs are device-only)
     host = hhmm_amd.api.PreparedRequest(model, data, draws, ["loglik"], pairing)
@@ -490,9 +523,33 @@ def other_workload(a, lib, dev, world, rank):
                          "traffic": None, "algorithmic_bytes_per_series_timestep": B, "duration_ms": dev_ms},
             "pair_failures": int((status != 0).sum().item()),
         }
+        if not a.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline_grid(model, data, draws, pars, T, a.cpu_seconds, a.seed)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_baseline_grid(model, data, draws, pars, T, target_s, seed):
+    """The oracle (libm build) on a bounded number of the workload's draws of
+    its first series (same T and shapes), all the process's cores."""
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    xkey = "x_t" if model.startswith("iohmm") else "x"
+    d1 = {k: (np.asarray(v)[:1] if k in ("x", "x_t", "g", "sign", "u_tm") else v) for k, v in data.items()}
+    S = next(np.asarray(v).shape[0] for v in draws.values())
+    assert np.asarray(d1[xkey]).shape[0] == 1
+
+    def gen(n, off):
+        n = min(n, S)
+        dr = {k: np.asarray(v)[:n] for k, v in draws.items()}
+        u = synth.ffbs_uniforms(n, T, seed=seed + off) if "z_ffbs" in pars else None
+        return d1, dr, n, T, u
+
+    v, P, _, dt = timed_oracle(model, gen, pars, "grid", threads, target_s, threads, S)
+    return {"value": v, "unit": "series-timesteps/s", "cores": threads, "kind": "port",
+            "sample": f"{P} draws x 1 series x T={T} ({model}, outputs {','.join(pars)}), {dt:.1f} s on "
+                      f"{threads} threads, oracle libm-log build", "cpu_model": cpu_model()}
 
 
 def features_workload(a, lib, dev, world, rank):
@@ -575,26 +632,31 @@ def features_workload(a, lib, dev, world, rank):
 
 
 def check_slice(run, x, draws, P, T):
-    """Compares the first 64 pairs with the oracle (test infrastructure)."""
+    """Compares 64 pairs of the data the timed steps ran on (the first 32 and
+    32 spread over the batch) with the oracle, after warmup and outside the
+    timed region (test infrastructure; raises on a mismatch)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     sys.path.insert(0, str(ROOT / "tests"))
     import pyoracle
     from tolerances import compare
-    n = min(64, P)
-    data = {"K": K, "L": L, "x": x[:, :n].T.cpu().numpy()}
-    dr = {k: v[..., :n].permute(*reversed(range(v.dim()))).cpu().numpy() for k, v in draws.items()}
+    idx = np.unique(np.concatenate([np.arange(min(32, P)), np.linspace(0, P - 1, 32).astype(np.int64)]))
+    ii = torch.as_tensor(idx, device=x.device)
+    data = {"K": K, "L": L, "x": x[:, ii].T.cpu().numpy()}
+    dr = {k: v[..., ii].permute(*reversed(range(v.dim()))).cpu().numpy() for k, v in draws.items()}
     dr["p_1k"] = dr["p_1k"][:, 0, :]
     ref = pyoracle.gqs("hmm-multinom", data, dr, pars=["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
                        pairing="zip", nthreads=8)
     got = {
-        "loglik": run.out["loglik"][:n].cpu().numpy(),
-        "logp_zstar": run.out["logp_zstar"][:n].cpu().numpy(),
-        "zstar_t": run.out["zstar_t"][:, :n].T.cpu().numpy(),
-        "gamma_tk": run.out["gamma_tk"][:, :, :n].permute(2, 1, 0).cpu().numpy(),
+        "loglik": run.out["loglik"][ii].cpu().numpy(),
+        "logp_zstar": run.out["logp_zstar"][ii].cpu().numpy(),
+        "zstar_t": run.out["zstar_t"][:, ii].T.cpu().numpy(),
+        "gamma_tk": run.out["gamma_tk"][:, :, ii].permute(2, 1, 0).cpu().numpy(),
     }
     for k in got:
         compare(k, got[k], ref[k])
-    print(f"check: first {n} pairs match the oracle", file=sys.stderr, flush=True)
+    msg = f"{idx.size} pairs of the timed batch match the oracle (loglik, gamma_tk, zstar_t, logp_zstar)"
+    print("check:", msg, file=sys.stderr, flush=True)
+    return msg
 
 
 if __name__ == "__main__":

@@ -33,6 +33,18 @@ class HHMMError(RuntimeError):
         self.status = status
 
 
+def _init_torch_first():
+    """PyTorch-ROCm ships its own HIP runtime next to the one libhhmm.so links
+    (/opt/rocm).  Both work in one process only when torch's initialises the
+    device first (measured on MI355X: the other order leaves torch with "No HIP
+    GPUs are available"), so a process that has imported torch gets its device
+    context before the engine's first HIP call."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def load_library(path=None):
     """Loads libhhmm.so; raises ImportError if it has not been built."""
     global _lib
@@ -43,6 +55,7 @@ def load_library(path=None):
         raise ImportError(
             f"libhhmm.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the engine has no CPU fallback)")
+    _init_torch_first()
     lib = _abi.declare(C.CDLL(str(p)))
     if path is None:
         _lib = lib

@@ -89,3 +89,43 @@ def synth_ticks(n, seed=9000, tick=0.01, p0=20.0):
     gaps[g.random(n) < 0.002] *= 1500.0  # occasional long pauses (mins / hours)
     time = 1178020800.0 + np.cumsum(gaps)  # 2007-05-01 (tayal2009/data file dates)
     return price, size, time
+
+
+def index_ticks(legs, price):
+    """0-based tick of each zig-zag row's xts index.
+
+    The reference builds the table as `price[which(direction.chg) - 1, ]`
+    (feature-extraction.R:30), so row n carries the time of the tick before the
+    n-th change point: the leg's own end for every row but the last (whose end
+    is overwritten with nrow(price), :36).  The last change point is found
+    again from the prices (host side, O(n))."""
+    end = np.asarray(legs["end"], dtype=np.int64)
+    m = end.size
+    out = np.empty(m, dtype=np.int64)
+    if m == 0:
+        return out
+    out[:-1] = end[:-1] - 1
+    p = np.asarray(price, dtype=np.float64)
+    d = np.sign(np.diff(p))                      # direction of ticks 2..n (:20-24)
+    prev = np.concatenate([[0.0], d[:-1]])       # lag(direction); tick 1 is direction.lt
+    chg = np.flatnonzero((d != 0) & (d != prev)) + 1  # 0-based ticks where direction.chg
+    out[-1] = chg[-1] - 1
+    return out
+
+
+def xts_window(times, spec, tz="America/Toronto"):
+    """Boolean mask of the rows an xts ISO-8601 range subset `x[spec]` keeps,
+    e.g. '2007-05-04 09:30:00/2007-05-10 16:30:00' in the index's time zone
+    (tayal2009/main.Rmd:73, :406; indexTZ set at main.R:52): from the first
+    instant through the end of the last second named."""
+    import datetime
+    import zoneinfo
+    zone = zoneinfo.ZoneInfo(tz)
+    lo_s, hi_s = spec.split("/")
+
+    def epoch(s):
+        return datetime.datetime.strptime(s.strip(), "%Y-%m-%d %H:%M:%S").replace(tzinfo=zone).timestamp()
+
+    lo, hi = epoch(lo_s), epoch(hi_s) + 1.0
+    t = np.asarray(times, dtype=np.float64)
+    return (t >= lo) & (t < hi)

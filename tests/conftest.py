@@ -29,5 +29,6 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def engine():
+    import torch  # noqa: F401  (its HIP runtime initialises first: hhmm_amd.api._init_torch_first)
     import hhmm_amd
     return hhmm_amd.load_library()

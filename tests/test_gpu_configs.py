@@ -1,0 +1,196 @@
+"""GPU parity at the BASELINE.json configurations (C1-C5, SURVEY.md §8 d).
+
+Each config runs through the C ABI at its own shape -- the production
+dispatch the bench uses (lane or state Viterbi, FB_BIG checkpoints, the
+parallel scan over T) -- and is compared with the CPU oracle on the same
+inputs: at full size where the oracle finishes in seconds (C1, C4 shape),
+on a bounded slice of pairs otherwise (C2, C3, C5), plus size-independent
+properties on the full C2 and C5 batches (pair_status, finite posteriors,
+gamma rows summing to 1, zstar in 1..K with zstar_t[1] = K,
+logp_zstar <= loglik) and oracle parity on pairs sampled from those full
+batches.  Tolerances: tests/tolerances.py (1e-9 relative; paths bit-exact).
+"""
+import os
+import pathlib
+import sys
+
+import numpy as np
+import pytest
+
+from hhmm_amd import _abi, synth
+from tolerances import compare, compare_all
+
+pytestmark = pytest.mark.gpu
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+HOT = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+
+
+def threads():
+    n = len(os.sched_getaffinity(0))
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def gpu_and_oracle(engine, oracle, model, data, draws, pars, pairing="grid", flags=0, uniforms=None):
+    import hhmm_amd
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, pairing=pairing, lib=engine, return_status=True,
+                       flags=flags, uniforms=uniforms)
+    ref = oracle.gqs(model, data, draws, pars=pars, pairing=pairing, return_status=True, nthreads=threads(),
+                     uniforms=uniforms)
+    return got, ref
+
+
+def _log_softmax(v):
+    m = np.max(v, axis=-1, keepdims=True)
+    return v - (m + np.log(np.sum(np.exp(v - m), axis=-1, keepdims=True)))
+
+
+def compare_tayal_gamma(got, ref):
+    """Tayal's gamma = normalize(alpha .* beta) is 0/0 = NaN wherever the
+    reference's disagreeing forward/backward masks drive the
+    overlap of alpha and beta below the double range.  NaN rows must agree,
+    except rows whose exact overlap max_k alpha_k beta_k (from the oracle's
+    log-space unalpha_tk / unbeta_tk) is below e^-700 ~ 1e-304: there the
+    result depends on the last bits of products at the subnormal edge.  Every
+    row that is finite on both sides is within tolerance."""
+    g, r = got["gamma_tk"], ref["gamma_tk"]
+    n1, n2 = np.isnan(g).any(axis=-1), np.isnan(r).any(axis=-1)
+    diff = n1 != n2
+    if diff.any():
+        over = np.max(_log_softmax(ref["unalpha_tk"]) + _log_softmax(ref["unbeta_tk"]), axis=-1)
+        assert (over[diff] < -700.0).all(), \
+            f"NaN rows differ away from the underflow edge (max log overlap {over[diff].max():.1f})"
+    assert diff.mean() < 1e-3, f"NaN rows differ: {diff.sum()} of {diff.size}"
+    ok = ~(n1 | n2)
+    compare("gamma_tk", g[ok], r[ok])
+
+
+# ---- C1: hmm/main.R Gaussian HMM, K=3, T=500, 1 series x 1000 draws -------------------
+
+def test_c1_full_size(engine, oracle):
+    data, draws = synth.hmm_gauss(N=1, S=1000, T=500, K=3)
+    pars = synth.PARS["hmm"]
+    got, ref = gpu_and_oracle(engine, oracle, "hmm", data, draws, pars)
+    compare_all(got, ref, pars + ["pair_status"])
+    assert got["status"] == ref["status"]
+
+
+# ---- C2: hmm-multinom K=4, L=9, T=1000 ---------------------------------------------------
+
+@pytest.mark.parametrize("flags", [0, _abi.FLAG_VIT_LANES], ids=["auto", "lane-viterbi"])
+def test_c2_slice(engine, oracle, flags):
+    """A 4096-pair zip slice; `lane-viterbi` forces the lane-per-pair decoder
+    the full 1M-pair batch dispatches to (P >= 131072)."""
+    data, draws = synth.hmm_multinom(N=4096, S=4096, T=1000, K=4, L=9)
+    got, ref = gpu_and_oracle(engine, oracle, "hmm-multinom", data, draws, HOT, pairing="zip", flags=flags)
+    compare_all(got, ref, HOT + ["pair_status"])
+
+
+def _bench_module():
+    sys.path.insert(0, str(REPO))
+    import bench
+    return bench
+
+
+def test_c2_full_batch(engine, oracle):
+    """The bench's exact workload: 1,000,000 pairs x T=1000 built on the
+    device, both requests (fb + Viterbi) through hhmm_run_device.  Properties
+    over the whole batch, oracle parity on 48 pairs sampled across it."""
+    import torch
+    bench = _bench_module()
+    P, T, K, L = 1_000_000, 1000, 4, 9
+    dev = torch.device("cuda", torch.cuda.current_device())
+    x, draws = bench.make_batch(P, T, synth.SEED, dev)
+    run = bench.DeviceRun(engine, x, draws, P, T, dev)
+    run.launch("fb")
+    run.launch("viterbi")
+    torch.cuda.synchronize()
+    out = run.out
+    assert int((out["pair_status"] != 0).sum()) == 0
+    ll, lz = out["loglik"], out["logp_zstar"]
+    assert bool(torch.isfinite(ll).all()) and bool(torch.isfinite(lz).all())
+    assert bool((lz <= ll + 1e-9 * ll.abs()).all()), "a Viterbi path more probable than the whole likelihood"
+    zs = out["zstar_t"]
+    assert int(zs.min()) >= 1 and int(zs.max()) <= K
+    assert bool((zs[0] == K).all()), "zstar_t[1] = K for every pair (SURVEY App. A Q3)"
+    g = out["gamma_tk"]  # (K, T, P)
+    for k in range(K):
+        gk = g[k]
+        assert bool(torch.isfinite(gk).all()) and float(gk.min()) >= 0.0 and float(gk.max()) <= 1.0
+    rs = g.sum(0)
+    assert float((rs - 1.0).abs().max()) < 1e-12
+    del rs
+    rng = np.random.default_rng(2)
+    idx = np.unique(np.concatenate([[0, 63, 64, P - 1], rng.choice(P, 44, replace=False)]))
+    ii = torch.as_tensor(idx, device=dev)
+    data = {"K": K, "L": L, "x": x[:, ii].T.cpu().numpy()}
+    dr = {k: v[..., ii].permute(*reversed(range(v.dim()))).cpu().numpy() for k, v in draws.items()}
+    dr["p_1k"] = dr["p_1k"][:, 0, :]
+    ref = oracle.gqs("hmm-multinom", data, dr, pars=HOT, pairing="zip", nthreads=threads())
+    got = {"loglik": ll[ii].cpu().numpy(), "logp_zstar": lz[ii].cpu().numpy(),
+           "zstar_t": zs[:, ii].T.cpu().numpy(), "gamma_tk": g[:, :, ii].permute(2, 1, 0).cpu().numpy()}
+    compare_all(got, ref, HOT)
+
+
+# ---- C3: iohmm-reg K=4, M=4, T=300, grid of series x 4000 draws --------------------------
+
+def test_c3_grid(engine, oracle):
+    data, draws = synth.iohmm_reg(N=8, S=4000, T=300, K=4, M=4)
+    got, ref = gpu_and_oracle(engine, oracle, "iohmm-reg", data, draws, HOT)
+    compare_all(got, ref, HOT + ["pair_status"])
+
+
+# ---- C4: iohmm-hmix K=4, L=3, M=4, T=10k, batched FFBS -----------------------------------
+
+def test_c4_ffbs(engine, oracle):
+    data, draws = synth.iohmm_mix(N=2, S=64, T=10_000, K=4, L=3, M=4)
+    pars = ["loglik", "gamma_tk", "z_ffbs", "oblik_t", "zstar_t", "logp_zstar"]
+    u = synth.ffbs_uniforms(2 * 64, 10_000)
+    got, ref = gpu_and_oracle(engine, oracle, "iohmm-hmix", data, draws, pars, uniforms=u)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+# ---- C5: tayal2009 flattened HHMM, T=1e6 -------------------------------------------------
+
+@pytest.fixture(scope="module")
+def c5_data():
+    return synth.tayal(N=1, S=250, T=1_000_000)
+
+
+def test_c5_few_pairs(engine, oracle, c5_data):
+    """T = 10^6 on 4 pairs: the automatic dispatch takes the parallel scan over
+    T for the forward-backward and the state-parallel Viterbi."""
+    data, draws = c5_data
+    d4 = {k: np.asarray(v)[:4] for k, v in draws.items()}
+    import hhmm_amd
+    got = hhmm_amd.gqs("hhmm-tayal2009", data, d4, pars=HOT, lib=engine, return_status=True)
+    ref = oracle.gqs("hhmm-tayal2009", data, d4, pars=HOT + ["unalpha_tk", "unbeta_tk"], return_status=True,
+                     nthreads=threads())
+    compare_all(got, ref, ["loglik", "zstar_t", "logp_zstar", "pair_status"])
+    compare_tayal_gamma(got, ref)
+
+
+def test_c5_full_shape(engine, oracle, c5_data):
+    """The bench's C5 batch (250 draws x T = 10^6) in place on the device:
+    properties over every pair, oracle parity on 3 of them."""
+    import torch
+    from devrun import DeviceRequest
+    data, draws = c5_data
+    r = DeviceRequest(engine, "hhmm-tayal2009", data, draws, HOT)
+    r.run()
+    assert int((r.status != 0).sum()) == 0
+    ll, lz, zs = r.out["loglik"], r.out["logp_zstar"], r.out["zstar_t"]
+    assert bool(torch.isfinite(ll).all()) and bool(torch.isfinite(lz).all())
+    assert bool((lz <= ll + 1e-9 * ll.abs()).all())
+    assert int(zs.min()) >= 1 and int(zs.max()) <= 4 and bool((zs[0] == 4).all())
+    g = r.out["gamma_tk"]
+    rs = g.sum(0)
+    fin = torch.isfinite(rs)
+    assert float((rs[fin] - 1.0).abs().max()) < 1e-12
+    del rs, fin
+    idx = [0, 131, 249]
+    dsub = {k: np.asarray(v)[idx] for k, v in draws.items()}
+    ref = oracle.gqs("hhmm-tayal2009", data, dsub, pars=HOT + ["unalpha_tk", "unbeta_tk"], nthreads=3)
+    got = {k: r.host_pairs(k, idx) for k in HOT}
+    compare_all(got, ref, ["loglik", "zstar_t", "logp_zstar"])
+    compare_tayal_gamma(got, ref)

@@ -96,3 +96,25 @@ def test_real_ticks_through_feature_oracle(oracle):
     assert (size == np.round(size)).all()  # integer volumes: R's long-double sum is exact in double
     got = oracle.extract_features(price, size, time, alpha=0.25)
     test_features._assert_same(got, test_features.transcribe(price, size, time, 0.25))
+
+
+# tayal2009/main.Rmd:65-74 -- the data set and windows its rendered report (main.pdf) uses
+RMD_DAYS = ("2007.05.04", "2007.05.07", "2007.05.08", "2007.05.09", "2007.05.10", "2007.05.11")
+RMD_INS = "2007-05-04 09:30:00/2007-05-10 16:30:00"
+RMD_OOS = "2007-05-11 09:30:00/2007-05-11 16:30:00"
+
+
+@pytest.mark.skipif(not DATA.exists(), reason="reference tick data not present (GPU box)")
+def test_in_sample_zigzag_count_matches_report(oracle):
+    """Reference-held pin for F1: main.Rmd:410 prints nrow(zig.ins), and the
+    rendered tayal2009/main.pdf reads "In-sample dataset reduced to 8386
+    zig-zags".  The chain is the report's own: load() + rbind + na.omit of the
+    six files (:386-395), extract_features(tdata, 0.25) (:405), zig[ins] with
+    the index in America/Toronto (:406, main.R:52)."""
+    from hhmm_amd import features as F
+    files = [DATA / "G.TO" / f"{d}.G.TO.RData" for d in RMD_DAYS]
+    price, size, time = rdata.load_ticks(files)
+    legs = oracle.extract_features(price, size, time, alpha=0.25)
+    when = time[F.index_ticks(legs, price)]
+    assert int(F.xts_window(when, RMD_INS).sum()) == 8386
+    assert int(F.xts_window(when, RMD_OOS).sum()) > 0
