@@ -286,8 +286,8 @@ __device__ __forceinline__ void vit_back_flush(const DevArgs &a, int64_t p, int 
 /* Viterbi epilogue shared by every Viterbi pass: flushes the partial last
  * back-pointer word, logp_zstar = max(delta_T) with Eigen's SSE2 maxCoeff NaN
  * rule, zstar_T = the LAST j attaining it (e.g. hmm/stan/hmm.stan:120-124),
- * pair_status, then the backtrack chunk by chunk with the words prefetched one
- * chunk ahead (hmm.stan:126-128).  QUAD: the state-parallel decoder's lane
+ * pair_status, then the backtrack chunk by chunk with the words prefetched a
+ * group of chunks ahead (hmm.stan:126-128).  QUAD: the state-parallel decoder's lane
  * quads (every lane of a quad holds the same delta_T and word). */
 template <int K, bool QUAD = false>
 __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, int Tp, int Tw_min, int Tw_max,
@@ -322,17 +322,18 @@ __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, in
             a.zstar[p + a.P * (int64_t)t] = 0;
         return;
     }
-    /* backtrack, chunk by chunk, words prefetched one chunk ahead; word rows
-     * are wave-uniform, clamped to the allocation (a short lane's extra rows
-     * are never consumed) */
+    /* backtrack, chunk by chunk; word rows are wave-uniform, clamped to the
+     * allocation (a short lane's extra rows are never consumed) */
     const int wmax = a.Tmax / SPW;
     int zb[CV];
     const int clast = nchunk - 1;
-    if constexpr (QUAD) {
-        /* Few pairs, long T (C5): one wave per SIMD, nothing else hides the
-         * word loads' HBM latency, and one chunk of backtrack (CV steps of
-         * dependent shifts) is far shorter than it.  So the words come in
-         * groups of G chunks, the next group prefetched while this one runs. */
+    {
+        /* The words come in groups of G chunks, the next group prefetched
+         * while this one runs: one chunk of backtrack (CV steps of dependent
+         * shifts) is far shorter than an HBM round trip, so a one-chunk
+         * prefetch leaves the wave waiting on every chunk (C5: one wave per
+         * SIMD and nothing else to hide it; C2: the lane decoder's backtrack
+         * phase, T/CV round trips per pair). */
         constexpr int G = 8;
         uint32_t w[G * WPC], wn[G * WPC];
         const int glast = clast / G;
@@ -365,28 +366,7 @@ __device__ __forceinline__ void viterbi_epilogue(const DevArgs &a, int64_t p, in
         }
         if (clast >= 0)
             vit_back_flush<CV, QUAD>(a, p, Tp, 0, zb);
-        return;
     }
-    uint32_t w[WPC], wn[WPC];
-#pragma unroll
-    for (int i = 0; i < WPC; ++i)
-        w[i] = get_tmp(a.bp + a.P * (int64_t)min(max(clast * WPC + i, 0), wmax), (uint32_t)p * 4u);
-    for (int c = clast; c >= 0; --c) {
-#pragma unroll
-        for (int i = 0; i < WPC; ++i)
-            wn[i] = get_tmp(a.bp + a.P * (int64_t)min(max((c - 1) * WPC + i, 0), wmax), (uint32_t)p * 4u);
-        if (c < clast)
-            vit_back_flush<CV, QUAD>(a, p, Tp, c + 1, zb);
-        if (c < nfull)
-            vit_back_chunk<K, CV, true>(Tp, c, w, z, zb);
-        else
-            vit_back_chunk<K, CV, false>(Tp, c, w, z, zb);
-#pragma unroll
-        for (int i = 0; i < WPC; ++i)
-            w[i] = wn[i];
-    }
-    if (clast >= 0)
-        vit_back_flush<CV, QUAD>(a, p, Tp, 0, zb);
 }
 
 } // namespace hhmm

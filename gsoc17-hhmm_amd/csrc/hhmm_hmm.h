@@ -137,7 +137,11 @@ __device__ __forceinline__ double draw2(const double *arr, const DevArgs &a, int
 }
 
 /* Loads p_1k, A_ij (Tayal: expands p_11 / A_row, hhmm-tayal2009.stan:30-44)
- * and the Gaussian constants.  LOG = true puts log A in params.A. */
+ * and the Gaussian constants.  LOG = true puts log A in params.A.
+ * Every global load is issued before the first log consumes one: with the
+ * load -> correctly rounded log pairs interleaved, hipcc waits vmcnt(0) per
+ * parameter, i.e. one HBM round trip per entry (K^2 + K of them) before the
+ * first step. */
 template <int MODEL, int K, bool LOG>
 __device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevArgs &a, int64_t d)
 {
@@ -157,44 +161,70 @@ __device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevA
             for (int j = 0; j < 4; ++j)
                 pp.A[i][j] = LOG ? hhmm_cr_log(A[i][j]) : A[i][j];
     } else {
+        double raw[K][K];
 #pragma unroll
         for (int k = 0; k < K; ++k)
             pp.p[k] = draw1<K>(a.p_1k, a, d, k);
 #pragma unroll
         for (int i = 0; i < K; ++i)
 #pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const double v = draw2<K>(a.A_ij, a, d, i, j, K);
-                pp.A[i][j] = LOG ? hhmm_cr_log(v) : v;
-            }
-    }
-    if constexpr (ModelTraits<MODEL>::kGauss) {
+            for (int j = 0; j < K; ++j)
+                raw[i][j] = draw2<K>(a.A_ij, a, d, i, j, K);
+        double mu[ModelTraits<MODEL>::kGauss ? K : 1], sg[ModelTraits<MODEL>::kGauss ? K : 1];
+        if constexpr (ModelTraits<MODEL>::kGauss) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double sg = draw1<K>(a.sigma_k, a, d, k);
-            pp.mu[k] = draw1<K>(a.mu_k, a, d, k);
-            pp.isig[k] = 1.0 / sg;
-            pp.lsig[k] = hhmm_cr_log(sg);
-            pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - pp.lsig[k];
+            for (int k = 0; k < K; ++k) {
+                sg[k] = draw1<K>(a.sigma_k, a, d, k);
+                mu[k] = draw1<K>(a.mu_k, a, d, k);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                pp.A[i][j] = LOG ? hhmm_cr_log(raw[i][j]) : raw[i][j];
+        if constexpr (ModelTraits<MODEL>::kGauss) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                pp.mu[k] = mu[k];
+                pp.isig[k] = 1.0 / sg[k];
+                pp.lsig[k] = hhmm_cr_log(sg[k]);
+                pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - pp.lsig[k];
+            }
         }
     }
 }
 
-/* Fills this lane's LDS slab with phi_k (LOG: log phi_k). */
+/* Fills this lane's LDS slab with phi_k (LOG: log phi_k).  Rows are fetched
+ * kRowBatch at a time, all loads of a batch in flight together (a load per
+ * row followed by its LDS store costs one HBM round trip per row). */
+constexpr int kRowBatch = 4;
 template <int K, bool LOG>
 __device__ __forceinline__ void fill_table(double2 *slab, const DevArgs &a, int64_t d)
 {
     constexpr int KP = (K + 1) / 2;
-    for (int l = 0; l < a.L; ++l) {
+    for (int l0 = 0; l0 < a.L; l0 += kRowBatch) {
+        double v[kRowBatch][2 * KP];
 #pragma unroll
-        for (int kp = 0; kp < KP; ++kp) {
-            double v0 = draw2<K>(a.phi_k, a, d, 2 * kp, l, K);
-            double v1 = (2 * kp + 1 < K) ? draw2<K>(a.phi_k, a, d, 2 * kp + 1, l, K) : 0.0;
-            if (LOG) {
-                v0 = hhmm_cr_log(v0);
-                v1 = hhmm_cr_log(v1);
+        for (int r = 0; r < kRowBatch; ++r) {
+            const int l = min(l0 + r, a.L - 1); /* clamped: a short last batch re-reads row L-1 */
+#pragma unroll
+            for (int k = 0; k < 2 * KP; ++k)
+                v[r][k] = (k < K) ? draw2<K>(a.phi_k, a, d, k, l, K) : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < kRowBatch; ++r) {
+            if (l0 + r < a.L) {
+#pragma unroll
+                for (int kp = 0; kp < KP; ++kp) {
+                    double v0 = v[r][2 * kp], v1 = v[r][2 * kp + 1];
+                    if (LOG) {
+                        v0 = hhmm_cr_log(v0);
+                        v1 = hhmm_cr_log(v1);
+                    }
+                    slab[((l0 + r) * KP + kp) * 64] = make_double2(v0, v1);
+                }
             }
-            slab[(l * KP + kp) * 64] = make_double2(v0, v1);
         }
     }
 }
@@ -203,8 +233,10 @@ template <int K>
 __device__ __forceinline__ void read_table(const double2 *slab, int x, int L, double (&e)[K])
 {
     constexpr int KP = (K + 1) / 2;
-    const int row = min(max(x, 1), L) - 1;
-    const double2 *r = slab + row * KP * 64;
+    /* row x (1-based, clamped) from the slab's base one row back, so the
+     * state pairs sit at non-negative immediate offsets of one address */
+    const int xc = min(max(x, 1), L);
+    const double2 *r = (slab - KP * 64) + xc * (KP * 64);
 #pragma unroll
     for (int kp = 0; kp < KP; ++kp) {
         const double2 v = r[kp * 64];
@@ -414,6 +446,8 @@ constexpr int fb_base(int mode) { return mode & 3; }
 constexpr bool fb_ffbs(int mode) { return (mode & FB_FFBS) != 0; }
 constexpr bool fb_pack(int mode) { return (mode & FB_PACK) != 0; }
 constexpr bool fb_big(int mode) { return (mode & FB_BIG) != 0; }
+constexpr int kFwdGroup = 4;  /* forward chunks per observation prefetch group */
+constexpr int kVitGroup = 2;  /* Viterbi chunks per observation prefetch group */
 constexpr int kBigChunk = 16; /* checkpoint interval of FB_BIG (a multiple of fb_chunk(K) = 8) */
 constexpr int kGroup = 2;     /* pass 1 keeps every kGroup-th state (32 steps / groups of 4 need
                                * ~300 VGPRs: occupancy 1) */
@@ -813,17 +847,42 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
 
     /* ---- forward sweep ---- */
     int ex = 0;       /* sum of binary exponents removed */
-    Obs cur[C];
-    load_chunk<MODEL, C, AUX>(cur, sp, cb * C);
+    /* Full chunks go kFwdGroup at a time with the next group's observations
+     * in flight: one chunk of forward steps (~40 VALU each) is far shorter
+     * than an HBM round trip under load, so a one-chunk prefetch stalled
+     * every chunk (the forward sweep alone measured 2.6 ms at C2 against
+     * ~0.9 ms of issue).  The last, partial chunks keep the one-ahead loop. */
+    constexpr int D = kFwdGroup;
+    Obs grp[D][C];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        load_chunk<MODEL, C, AUX>(grp[i], sp, (cb + i) * C);
     Em<K> ecur;
-    emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, cur[0], ecur);
-    for (int c = cb; c < nchunk; ++c) {
+    emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, grp[0][0], ecur);
+    int c = cb;
+    for (; c + D <= nfull; c += D) {
+        Obs nxt[D][C];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            load_chunk<MODEL, C, AUX>(nxt[i], sp, (c + D + i) * C);
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            fwd_chunk<MODEL, K, C, MODE, true>(a, ln, c + i, grp[i], (i + 1 < D) ? grp[i + 1 < D ? i + 1 : 0][0]
+                                                                              : nxt[0][0], ecur, al, lsc, ex);
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int u = 0; u < C; ++u)
+                grp[i][u] = nxt[i][u];
+    }
+    Obs cur[C];
+#pragma unroll
+    for (int u = 0; u < C; ++u)
+        cur[u] = grp[0][u];
+    for (; c < nchunk; ++c) { /* < D full chunks, then the partial ones (one code copy) */
         Obs nxt[C];
         load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C);
-        if (c < nfull)
-            fwd_chunk<MODEL, K, C, MODE, true>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
-        else
-            fwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
+        fwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
 #pragma unroll
         for (int u = 0; u < C; ++u)
             cur[u] = nxt[u];
@@ -984,10 +1043,14 @@ __device__ __forceinline__ void emit_log(const PairParams<MODEL, K> &pp, const d
  * back-pointer differs only where every candidate is -inf / NaN (the
  * reference leaves it unset, here 0), which the epilogue flags through
  * delta_T = -inf exactly as before. */
-template <int MODEL, int K>
+template <int MODEL, int K, bool NANIN = false>
 __device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
                                          const Obs &o, uint32_t &word, int slot)
 {
+    /* NANIN: delta_{t-1} may hold NaN -- only the step after the t = 1 row of
+     * Q3.  Every later delta is a max over candidates that include a non-NaN
+     * one (state K's row at t = 2, then every state), so the running max can
+     * start from the first candidate instead of from fmax(-inf, candidate). */
     constexpr int BITS = bp_bits(K);
     constexpr int STEPB = K * BITS;
     double nd[K];
@@ -1011,7 +1074,7 @@ __device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL
                 cand = (dl[i] + pp.A[i][j]) + le[j];
             }
             if (i == 0) {
-                best = fmax(best, cand);
+                best = NANIN ? fmax(best, cand) : cand;
             } else {
                 const bool gt = cand > best;
                 best = fmax(best, cand);
@@ -1026,7 +1089,7 @@ __device__ __forceinline__ void vit_step(double (&dl)[K], const PairParams<MODEL
         dl[j] = nd[j];
 }
 
-template <int MODEL, int K, int CV, bool FULLC>
+template <int MODEL, int K, int CV, bool FULLC, bool FIRST = false>
 __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const PairParams<MODEL, K> &pp,
                                               const double2 *slab, int Tp, int c, const Obs (&cur)[CV],
                                               const Obs &nxt0, double (&le)[K], double (&dl)[K], uint32_t &word)
@@ -1039,8 +1102,11 @@ __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const
         double ln[K];
         emit_log<MODEL, K>(pp, slab, a.L, (u + 1 < CV) ? cur[u + 1 < CV ? u + 1 : 0] : nxt0, ln);
         if (FULLC || t < Tp) {
-            if (!(u == 0 && c == 0))
-                vit_step<MODEL, K>(dl, pp, le, cur[u], word, u % SPW);
+            /* FIRST: chunk 0, whose step 0 is the init row and step 1 the NaN step */
+            if (FIRST && u == 1)
+                vit_step<MODEL, K, true>(dl, pp, le, cur[u], word, u % SPW);
+            else if (!(FIRST && u == 0))
+                vit_step<MODEL, K, false>(dl, pp, le, cur[u], word, u % SPW);
             if (u % SPW == SPW - 1) {
                 put_tmp(a.bp + a.P * (int64_t)(t / SPW), (uint32_t)p * 4u, word);
                 word = 0;
@@ -1083,6 +1149,13 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
     double dl[K];
     Obs cur[CV];
     load_chunk<MODEL, CV, VAUX>(cur, sp, 0);
+    /* chunks 1.. go kVitGroup at a time with the next group's observations in
+     * flight (a one-chunk prefetch is shorter than an HBM round trip) */
+    constexpr int D = kVitGroup;
+    Obs grp[D][CV];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        load_chunk<MODEL, CV, VAUX>(grp[i], sp, (1 + i) * CV);
     double le[K];
     emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
 #pragma unroll
@@ -1090,13 +1163,31 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
         dl[k] = dev_nan();
     dl[K - 1] = le[K - 1];
     uint32_t word = 0;
-    for (int c = 0; c < nchunk; ++c) {
+    /* chunk 0: the t = 1 row and the NaN step (Q3) */
+    vit_fwd_chunk<MODEL, K, CV, false, true>(a, p, pp, slab, Tp, 0, cur, grp[0][0], le, dl, word);
+    int c = 1;
+    for (; c + D <= nfull; c += D) {
+        Obs nxt[D][CV];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            load_chunk<MODEL, CV, VAUX>(nxt[i], sp, (c + D + i) * CV);
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c + i, grp[i],
+                                              (i + 1 < D) ? grp[i + 1 < D ? i + 1 : 0][0] : nxt[0][0], le, dl, word);
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int u = 0; u < CV; ++u)
+                grp[i][u] = nxt[i][u];
+    }
+#pragma unroll
+    for (int u = 0; u < CV; ++u)
+        cur[u] = grp[0][u];
+    for (; c < nchunk; ++c) { /* < D full chunks, then the partial ones (one code copy) */
         Obs nxt[CV];
         load_chunk<MODEL, CV, VAUX>(nxt, sp, (c + 1) * CV);
-        if (c < nfull)
-            vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
-        else
-            vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
+        vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
 #pragma unroll
         for (int u = 0; u < CV; ++u)
             cur[u] = nxt[u];

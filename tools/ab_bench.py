@@ -4,7 +4,8 @@
 
   python tools/ab_bench.py NAME=path/to/libhhmm.so [NAME=...] [--rounds 5] [--pairs 1000000] [--T 1000]
 
-Each variant runs the bench.py C2 step (fb_kernel, then viterbi_kernel) on
+Each variant runs the bench.py C2 step (fb_kernel, then viterbi_kernel, then
+the two concurrently on two streams as bench.py does: "pair") on
 the same resident inputs; rounds are interleaved A B C A B C ...; per-kernel
 HIP-event times are reported as median / min over rounds.  Variants also
 cross-check each other's outputs (gamma within 1e-12, zstar exact).
@@ -38,7 +39,21 @@ def main():
         libs[name] = hhmm_amd.load_library(path)
     x, draws = bench.make_batch(a.pairs, a.T, 9000, dev)
     runs = {n: bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev) for n, lib in libs.items()}
-    times = {n: {"fb": [], "vit": []} for n in runs}
+    times = {n: {"fb": [], "vit": [], "pair": []} for n in runs}
+    s0 = torch.cuda.current_stream()
+    s1 = torch.cuda.Stream()
+
+    def pair(run):
+        """bench.py's step: viterbi on a side stream beside fb, forked and joined"""
+        fork = torch.cuda.Event()
+        fork.record(s0)
+        s1.wait_event(fork)
+        with torch.cuda.stream(s1):
+            run.launch("viterbi")
+        run.launch("fb")
+        join = torch.cuda.Event()
+        join.record(s1)
+        s0.wait_event(join)
     ref = None
     for r in range(a.rounds + 1):
         for n, run in runs.items():
@@ -62,6 +77,13 @@ def main():
                 continue
             times[n]["fb"].append(ev[0].elapsed_time(ev[1]))
             times[n]["vit"].append(ev[1].elapsed_time(ev[2]))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(s0)
+            pair(run)
+            e1.record(s0)
+            torch.cuda.synchronize()
+            times[n]["pair"].append(e0.elapsed_time(e1))
     out = {}
     for n, t in times.items():
         out[n] = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for k, v in t.items()}
