@@ -5,12 +5,12 @@ Workload (BASELINE.json configs[1], the metric's single-GPU config C2):
 hmm/stan/hmm-multinom.stan, K=4, L=9, 1,000,000 (series, draw) pairs
 (one posterior draw per series, HHMM_PAIR_ZIP) x T=1000, fp64.  One step =
 one pass of the hot path over the whole batch with inputs resident in HBM,
-through the C ABI (hhmm_run_device): the forward-backward request (gamma_tk
-[P,T,K], loglik [P]; fb_kernel) on torch's current stream and the Viterbi
-request (zstar_t [P,T], logp_zstar [P]; viterbi_kernel) on a second stream
-forked from it and joined back, so the VALU-bound decoder runs beside the
-HBM-bound forward-backward (what the library itself does for a single
-request asking for both).  --split runs them one after the other.
+through the C ABI (hhmm_run_device): ONE request for gamma_tk [P,T,K],
+loglik [P], zstar_t [P,T] and logp_zstar [P], which the library runs as
+fb_kernel on the caller's stream beside viterbi_kernel on a side stream
+(forked and joined).  --fused times the same request with HHMM_FLAG_FUSED
+(fbv_kernel: one sweep, x read once); both halves alone and the other
+schedule are reported after the timed region.
 
 Multi-GPU (torch.distributed.run, one process per GPU): every rank evaluates
 its own 1M pairs (weak scaling, no data-path collective); the per-step
@@ -64,13 +64,8 @@ def parse():
     ap.add_argument("--pars", default=None,
                     help="c3-c5 probes: comma-separated outputs instead of the workload's")
     ap.add_argument("--flags", type=int, default=0, help="c3-c5 probes: hhmm_request.flags")
-    ap.add_argument("--vit-priority", type=int, default=0,
-                    help="stream priority of the Viterbi stream (torch: -1 high, 0 default)")
-    ap.add_argument("--fb-first", action="store_true", help="enqueue the forward-backward before the Viterbi")
-    ap.add_argument("--vit-flags", type=int, default=0,
-                    help="hhmm_request.flags of the Viterbi request (e.g. 16 = HHMM_FLAG_VIT_STATES)")
-    ap.add_argument("--split", action="store_true",
-                    help="run the forward-backward and Viterbi one after the other on one stream")
+    ap.add_argument("--fused", action="store_true",
+                    help="time the one-kernel fused sweep (HHMM_FLAG_FUSED) instead of the two-kernel schedule")
     return ap.parse_args()
 
 
@@ -118,7 +113,12 @@ def make_batch(P, T, seed, dev):
 
 
 class DeviceRun:
-    """Holds device buffers and two prepared requests (FB and Viterbi)."""
+    """Device buffers and four prepared requests over the same batch and
+    outputs: "step" (gamma_tk, loglik, zstar_t, logp_zstar in ONE request:
+    the library runs fb_kernel and viterbi_kernel, the latter on a side
+    stream forked from and joined into the caller's), "fused" (the same
+    request with HHMM_FLAG_FUSED: one fused forward-backward + Viterbi sweep),
+    and the two halves alone ("fb", "viterbi")."""
 
     def __init__(self, lib, x, draws, P, T, dev):
         self.lib = lib
@@ -129,13 +129,17 @@ class DeviceRun:
             "logp_zstar": torch.empty(P, dtype=torch.float64, device=dev),
             "pair_status": torch.zeros(P, dtype=torch.int32, device=dev),
         }
+        hot = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
         self.reqs = {}
-        for name, outs in (("fb", ["loglik", "gamma_tk"]), ("viterbi", ["zstar_t", "logp_zstar"])):
+        self._ws = {}
+        for name, outs, flags in (("step", hot, 0), ("fused", hot, _abi.FLAG_FUSED),
+                                  ("fb", ["loglik", "gamma_tk"], 0), ("viterbi", ["zstar_t", "logp_zstar"], 0)):
             r = _abi.Request()
             r.abi_version = _abi.ABI_VERSION
             r.model = _abi.MODELS["hmm-multinom"]
             r.pairing = _abi.PAIR_ZIP
             r.device = -1
+            r.flags = flags
             r.data.n_series = P
             r.data.T_max = T
             r.data.K = K
@@ -151,8 +155,11 @@ class DeviceRun:
             res.pair_status = self.out["pair_status"].data_ptr()
             ws = C.c_size_t(0)
             assert lib.hhmm_workspace_size(C.byref(r), C.byref(ws)) == 0
-            wsbuf = torch.empty(max(int(ws.value), 256), dtype=torch.uint8, device=dev)
-            self.reqs[name] = (r, res, wsbuf)
+            # one workspace per size (the requests run one at a time on one stream)
+            need = max(int(ws.value), 256)
+            if need not in self._ws:
+                self._ws[need] = torch.empty(need, dtype=torch.uint8, device=dev)
+            self.reqs[name] = (r, res, self._ws[need])
 
     def launch(self, name):
         r, res, ws = self.reqs[name]
@@ -250,55 +257,19 @@ def main():
     P, T = a.pairs, a.T
     x, draws = make_batch(P, T, a.seed + 7919 * rank, dev)
     run = DeviceRun(lib, x, draws, P, T, dev)
-    run.reqs["viterbi"][0].flags = a.vit_flags
     torch.cuda.synchronize()
-
     s0 = torch.cuda.current_stream()
-    s1 = torch.cuda.Stream(priority=a.vit_priority)
+    name = "fused" if a.fused else "step"
 
     def step(ev=None):
-        """One pass of the hot path.  ev = 6 events: step start, fb start/end
-        (recorded on fb's stream), viterbi start/end (on viterbi's stream),
-        and the join (fb's stream, after waiting for the Viterbi)."""
+        """One pass of the hot path: one request for gamma_tk, loglik, zstar_t
+        and logp_zstar (two kernels, joined on the launch stream; --fused:
+        the one-kernel sweep), bracketed by events on the launch stream."""
         if ev:
             ev[0].record(s0)
-        if a.split:
-            if ev:
-                ev[1].record(s0)
-            run.launch("fb")
-            if ev:
-                ev[2].record(s0)
-                ev[3].record(s0)
-            run.launch("viterbi")
-            if ev:
-                ev[4].record(s0)
-            return
-        fork = torch.cuda.Event()
-        fork.record(s0)
-        s1.wait_event(fork)
-
-        def fb():
-            if ev:
-                ev[1].record(s0)
-            run.launch("fb")
-            if ev:
-                ev[2].record(s0)
-
-        if a.fb_first:
-            fb()
-        with torch.cuda.stream(s1):
-            if ev:
-                ev[3].record(s1)
-            run.launch("viterbi")
-            if ev:
-                ev[4].record(s1)
-        if not a.fb_first:
-            fb()
-        join = torch.cuda.Event()
-        join.record(s1)
-        s0.wait_event(join)
+        run.launch(name)
         if ev:
-            ev[5].record(s0)  # after the join: the pair's end whichever kernel finishes last
+            ev[1].record(s0)
         if world > 1:
             import torch.distributed as dist
             s = run.out["loglik"].sum().reshape(1)
@@ -311,7 +282,7 @@ def main():
     if not a.no_check and rank == 0:
         checked = check_slice(run, x, draws, P, T)
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(a.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(a.steps)]
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -323,48 +294,39 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    fb_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    vit_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
-    pair_ms = float(np.mean([e[0].elapsed_time(e[4]) if a.split else e[0].elapsed_time(e[5]) for e in evs]))
+    step_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     bad = int((run.out["pair_status"] != 0).sum().item())
-    # after the timed region: each kernel alone once (untimed for `value`), so the
-    # line also carries the north star's "batched forward-backward" roofline
+    # after the timed region: the other schedules once each (untimed for `value`):
+    # the two halves alone (the north star's "batched forward-backward") and the
+    # two-kernel schedule
     solo = {}
-    for name in ("fb", "viterbi"):
+    for nm in ("fb", "viterbi", "step" if a.fused else "fused"):
         ts = []
         for _ in range(3):  # back to back on one stream; median of three launches
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s0)
-            run.launch(name)
+            run.launch(nm)
             e1.record(s0)
             ts.append((e0, e1))
         torch.cuda.synchronize()
-        solo[name] = float(np.median([e0.elapsed_time(e1) for e0, e1 in ts]))
+        solo[nm] = float(np.median([e0.elapsed_time(e1) for e0, e1 in ts]))
 
     if rank == 0:
         fb_b, vit_b, whole_b = bytes_per_step(T)
         units = P * T
-        kernels_ms = {"fb_kernel": fb_ms, "viterbi_kernel": vit_ms}
-        if a.split:  # sequential: the dominant kernel alone
-            if fb_ms >= vit_ms:
-                dom, dom_ms, dom_b = "fb_kernel", fb_ms, fb_b
-            else:
-                dom, dom_ms, dom_b = "viterbi_kernel", vit_ms, vit_b
-            traffic = load_traffic(dom, P, T)
+        dom = "fbv_kernel" if a.fused else "fb_kernel+viterbi_kernel"
+        if a.fused:
+            traffic = load_traffic("fbv_kernel", P, T)
         else:
-            # concurrent: the two launches overlap for the whole step, so the
-            # unit is the launch pair -- the step's algorithmic bytes over the
-            # fork-to-join time (HIP events on the launch streams); traffic =
-            # both kernels' PMC bytes
-            dom, dom_ms, dom_b = "fb_kernel+viterbi_kernel", pair_ms, whole_b
             t1, t2 = load_traffic("fb_kernel", P, T), load_traffic("viterbi_kernel", P, T)
             traffic = (t1 + t2) if (t1 is not None and t2 is not None) else None
-        achieved = dom_b * units / (dom_ms * 1e-3)
+        achieved = whole_b * units / (step_ms * 1e-3)
         value = world * units * a.steps / elapsed
+        other = "step" if a.fused else "fused"
         line = {
             "metric": "series-timesteps/sec forward-backward+Viterbi (K=4) at 1/2/4/8 GPU; % HBM roofline",
             "value": value,
@@ -381,20 +343,22 @@ def main():
             "config": {"workload": "C2 hmm-multinom K=4 L=9, 1M pairs x T=1000 per GPU (zip pairing)",
                        "pairs_per_gpu": P, "T": T, "outputs": "gamma_tk zstar_t loglik logp_zstar",
                        "parallelism": f"pairs sharded over {world} GPU(s)",
-                       "schedule": "fb and viterbi sequential" if a.split else ("fb || viterbi (two streams" + (", fb enqueued first" if a.fb_first else "") + (f", viterbi stream priority {a.vit_priority}" if a.vit_priority else "") + ")")},
+                       "schedule": ("fused forward-backward + Viterbi sweep (one kernel, HHMM_FLAG_FUSED)"
+                                    if a.fused else "fb_kernel || viterbi_kernel (library side stream)")},
             "whole_step_roofline_frac": whole_b * world * units * a.steps / elapsed / (HBM_PEAK * world),
-            "kernels_ms": kernels_ms,
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": traffic, "algorithmic_bytes_per_series_timestep": dom_b,
-                         "duration_ms": dom_ms},
+                         "traffic": traffic, "algorithmic_bytes_per_series_timestep": whole_b,
+                         "duration_ms": step_ms},
             "pair_failures": bad,
             "check": checked,
             "alone_after_timing": {
                 "fb_kernel": {"ms": solo["fb"], "algorithmic_bytes_per_series_timestep": fb_b,
                               "roofline_frac": fb_b * units / (solo["fb"] * 1e-3) / HBM_PEAK},
                 "viterbi_kernel": {"ms": solo["viterbi"], "algorithmic_bytes_per_series_timestep": vit_b,
-                                   "roofline_frac": vit_b * units / (solo["viterbi"] * 1e-3) / HBM_PEAK}},
+                                   "roofline_frac": vit_b * units / (solo["viterbi"] * 1e-3) / HBM_PEAK},
+                ("fused sweep (HHMM_FLAG_FUSED)" if other == "fused" else "two-kernel schedule"):
+                    {"ms": solo[other], "roofline_frac": whole_b * units / (solo[other] * 1e-3) / HBM_PEAK}},
         }
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(T, a.cpu_seconds, a.seed)

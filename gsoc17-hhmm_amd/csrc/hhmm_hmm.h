@@ -37,6 +37,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -1201,6 +1204,214 @@ __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
     viterbi_block<MODEL, K>(a, blockIdx.x);
 }
 
+/* ---- fused forward-backward + Viterbi (C2's profile) -------------------- *
+ * One lane, one pair, ONE pass over the observations for both halves of the
+ * hot path (hmm-multinom.stan:27-132): the forward sweep runs the scaled
+ * linear-space filter (fwd_chunk) and the max-plus recursion (vit_fwd_chunk)
+ * on the same observation registers, so x crosses HBM once instead of twice;
+ * the backward sweep (FB_BIG blocks of kBigChunk steps) emits gamma and
+ * backtracks the path over the same blocks, so the back-pointer words ride
+ * the checkpoint prefetch.  Both emission tables (phi and log phi, K*L
+ * doubles each) sit in the wave's LDS slab, which holds the kernel at one
+ * wave per SIMD; both halves produce exactly what fb_kernel and
+ * viterbi_kernel produce (same functions, same operation order).
+ * K = 4 (fb_chunk = vit_chunk = 8, two back-pointer words per chunk).
+ * Measured: 11.3 ms at C2 against 10.4 ms for the two concurrent kernels --
+ * every wave runs the VALU-bound forward half and then the HBM-bound backward
+ * half in lockstep with the others, so the pipes take turns instead of
+ * overlapping -- hence opt-in (HHMM_FLAG_FUSED). */
+template <int MODEL, int K>
+constexpr bool fbv_ok()
+{
+    return fb_big_ok<MODEL, K>() && vit_chunk(K) == fb_chunk(K);
+}
+
+template <int MODEL, int K>
+__device__ __forceinline__ void fbv_block(const DevArgs &a, uint32_t block)
+{
+    constexpr int MODE = FB_GAMMA | FB_PACK | FB_BIG;
+    constexpr int C = fb_chunk(K);
+    constexpr int SPW = bp_steps_per_word(K);
+    constexpr int WPC = C / SPW;
+    constexpr int B = kBigChunk, NW = B / 8, CPB = B / C; /* chunks per block */
+    constexpr int KP = (K + 1) / 2;
+    static_assert(vit_chunk(K) == C && B % C == 0, "fused sweep: one chunk size for both halves");
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t p = min((int64_t)block * blockDim.x + threadIdx.x, a.P - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const size_t tab = (size_t)a.L * KP * 64; /* double2 per table per wave */
+    double2 *slab = lds + (size_t)wave * 2 * tab + lane;
+    const double2 *lslab = slab + tab;
+
+    FbLane<MODEL, K> ln;
+    ln.p = p;
+    ln.L = a.L;
+    ln.t0 = 0;
+    ln.Tp = pair_len(a, n);
+    ln.cb = 0;
+    ln.q = p;
+    ln.Qs = a.P;
+    ln.slab = slab;
+    PairParams<MODEL, K> lpp; /* log A for the max-plus half */
+    load_params<MODEL, K, false>(ln.pp, a, d);
+    load_params<MODEL, K, true>(lpp, a, d);
+    fill_table<K, false>(slab, a, d);
+    fill_table<K, true>(slab + tab, a, d);
+    const SeriesPtrs sp = series_ptrs<MODEL, false>(a, n);
+    const int Tp = ln.Tp;
+    const int Tw_min = wave_min(Tp);
+    const int Tw_max = wave_max(Tp);
+    const int nfull = Tw_min / C;
+    const int nchunk = (Tw_max + C - 1) / C;
+
+    /* ---- forward sweep: filter + max-plus on one pass of x ---- */
+    double al[K], lsc = 0.0;
+    int ex = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        al[k] = 0.0;
+    constexpr int D = kFwdGroup;
+    Obs cur[C];
+    load_chunk<MODEL, C, false>(cur, sp, 0);
+    Obs grp[D][C];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        load_chunk<MODEL, C, false>(grp[i], sp, (1 + i) * C);
+    Em<K> ecur;
+    emit_prob<MODEL, K>(ln.pp, slab, a.L, cur[0], ecur);
+    double le[K], dl[K];
+    emit_log<MODEL, K>(lpp, lslab, a.L, cur[0], le);
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k)
+        dl[k] = dev_nan(); /* delta_tk[1, K] only (Q3, hmm-multinom.stan:105-106) */
+    dl[K - 1] = le[K - 1];
+    uint32_t word = 0;
+    fwd_chunk<MODEL, K, C, MODE, false>(a, ln, 0, cur, grp[0][0], ecur, al, lsc, ex);
+    vit_fwd_chunk<MODEL, K, C, false, true>(a, p, lpp, lslab, Tp, 0, cur, grp[0][0], le, dl, word);
+    int c = 1;
+    for (; c + D <= nfull; c += D) {
+        Obs nxt[D][C];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            load_chunk<MODEL, C, false>(nxt[i], sp, (c + D + i) * C);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const Obs &n0 = (i + 1 < D) ? grp[i + 1 < D ? i + 1 : 0][0] : nxt[0][0];
+            fwd_chunk<MODEL, K, C, MODE, true>(a, ln, c + i, grp[i], n0, ecur, al, lsc, ex);
+            vit_fwd_chunk<MODEL, K, C, true>(a, p, lpp, lslab, Tp, c + i, grp[i], n0, le, dl, word);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int u = 0; u < C; ++u)
+                grp[i][u] = nxt[i][u];
+    }
+#pragma unroll
+    for (int u = 0; u < C; ++u)
+        cur[u] = grp[0][u];
+    for (; c < nchunk; ++c) {
+        Obs nxt[C];
+        load_chunk<MODEL, C, false>(nxt, sp, (c + 1) * C);
+        fwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
+        vit_fwd_chunk<MODEL, K, C, false>(a, p, lpp, lslab, Tp, c, cur, nxt[0], le, dl, word);
+#pragma unroll
+        for (int u = 0; u < C; ++u)
+            cur[u] = nxt[u];
+    }
+    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+        a.loglik[p] = log(vsum<K>(al)) + (lsc + kLn2 * ex);
+
+    /* ---- Viterbi end (as viterbi_epilogue): partial word, logp_zstar, zstar_T ---- */
+    if ((Tp - 1) % SPW != SPW - 1)
+        put_tmp(a.bp + a.P * (int64_t)((Tp - 1) / SPW), (uint32_t)p * 4u, word);
+    const double lpz = stan_max_vec<K>(dl);
+    int z = -1;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (dl[j] == lpz)
+            z = j;
+    const bool invalid = (z < 0) || (Tp >= 2 && lpz == dev_ninf());
+    if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
+        a.logp_zstar[p] = lpz;
+    if (a.pair_status)
+        a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+    const bool want_z = (a.outputs & HHMM_OUT_ZSTAR) && a.zstar;
+    if (invalid)
+        z = 0; /* the path is all zeros (pair flagged), the walk below is discarded */
+
+    /* ---- backward sweep + backtrack, kBigChunk-step blocks from the end ---- */
+    double be[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1) */
+    int bex = 0;
+    const int nblk = (Tw_max + B - 1) / B;
+    const int nfullb = Tw_min / B;
+    const int wmax = a.Tmax / SPW;
+    auto load_blk = [&](int blk, double (&ck)[K], uint32_t (&w)[NW], uint32_t (&bw)[CPB * WPC]) {
+        const int bb = max(blk, 0);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ck[k] = get_tmp(a.ckpt + ln.Qs * ((int64_t)bb * K + k), (uint32_t)p * 8u);
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = at(a.xpk + ln.Qs * (int64_t)(bb * NW + i), (uint32_t)p * 4u);
+#pragma unroll
+        for (int i = 0; i < CPB * WPC; ++i)
+            bw[i] = get_tmp(a.bp + a.P * (int64_t)min(bb * CPB * WPC + i, wmax), (uint32_t)p * 4u);
+    };
+    double ck[K], ckn[K];
+    uint32_t w[NW], wn[NW], bw[CPB * WPC], bwn[CPB * WPC];
+    load_blk(nblk - 1, ck, w, bw);
+    for (int blk = nblk - 1; blk >= 0; --blk) {
+        load_blk(blk - 1, ckn, wn, bwn);
+        if (blk < nfullb)
+            bwd_block_big<MODEL, K, MODE, true>(a, ln, blk * B, w, ck, be, bex);
+        else
+            bwd_block_big<MODEL, K, MODE, false>(a, ln, blk * B, w, ck, be, bex);
+#pragma unroll
+        for (int cc = CPB - 1; cc >= 0; --cc) {
+            const int cidx = blk * CPB + cc;
+            int zb[C];
+            uint32_t wc[WPC];
+#pragma unroll
+            for (int i = 0; i < WPC; ++i)
+                wc[i] = bw[cc * WPC + i];
+            if (cidx < nfull)
+                vit_back_chunk<K, C, true>(Tp, cidx, wc, z, zb);
+            else
+                vit_back_chunk<K, C, false>(Tp, cidx, wc, z, zb);
+            if (want_z) {
+                if (invalid) {
+#pragma unroll
+                    for (int u = 0; u < C; ++u)
+                        zb[u] = 0;
+                }
+                vit_back_flush<C, false>(a, p, Tp, cidx, zb);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ck[k] = ckn[k];
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = wn[i];
+#pragma unroll
+        for (int i = 0; i < CPB * WPC; ++i)
+            bw[i] = bwn[i];
+    }
+}
+
+template <int MODEL, int K>
+__global__ void __launch_bounds__(kBlock) fbv_kernel(const DevArgs a)
+{
+    if constexpr (fbv_ok<MODEL, K>())
+        fbv_block<MODEL, K>(a, blockIdx.x);
+}
+
 
 /* ---- state-parallel Viterbi (few pairs, long T; C5) ------------------- *
  * One lane per (pair, state j): a pair's K <= 4 states sit in one lane quad.
@@ -2054,6 +2265,15 @@ struct LaunchShape {
     size_t lds;
 };
 
+/* Probe knob (tools/ab_bench.py --env): a minimum LDS request per workgroup
+ * in KiB from the environment variable `name`, which caps how many of the
+ * kernel's workgroups share a CU (and so leaves room for the other kernel's). */
+static size_t lds_floor(const char *name)
+{
+    const char *v = getenv(name);
+    return v ? (size_t)atoi(v) * 1024 : 0;
+}
+
 static bool shape_for(const DevArgs &a, bool discrete, LaunchShape &s)
 {
     const int KP = (a.K + 1) / 2;
@@ -2080,6 +2300,7 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
+    s.lds = std::max(s.lds, std::min(lds_floor("HHMM_PROBE_FB_LDS_KB"), kLdsLimit));
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     const bool ffbs = (a.outputs & HHMM_OUT_FFBS) != 0;
     if (a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) {
@@ -2195,10 +2416,34 @@ static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
+    s.lds = std::max(s.lds, std::min(lds_floor("HHMM_PROBE_VIT_LDS_KB"), kLdsLimit));
     hipLaunchKernelGGL((viterbi_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("viterbi_kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+/* The fused forward-backward + Viterbi sweep: both emission tables per wave. */
+template <int MODEL, int K>
+static hhmm_status launch_fbv(const DevArgs &a, hipStream_t st)
+{
+    const size_t per_wave = 2 * (size_t)a.L * ((K + 1) / 2) * 64 * sizeof(double2);
+    int waves = 4;
+    while (waves > 0 && per_wave * waves > kLdsLimit)
+        --waves;
+    if (waves == 0) {
+        set_error("emission tables 2*K*L = 2*%d*%d do not fit in LDS", a.K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const int threads = 64 * waves;
+    hipLaunchKernelGGL((fbv_kernel<MODEL, K>), dim3((unsigned)((a.P + threads - 1) / threads)), dim3(threads),
+                       per_wave * waves, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("fbv_kernel launch: %s", hipGetErrorString(e));
         return HHMM_ERR_HIP;
     }
     return HHMM_OK;
@@ -2257,6 +2502,14 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
             set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
             return HHMM_ERR_UNSUPPORTED;
         }
+    }
+    if constexpr (fbv_ok<MODEL, K>()) {
+        /* gamma (+ loglik) and the path in one request, on request: the fused sweep */
+        const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA |
+                               HHMM_OUT_UNGAMMA | HHMM_OUT_FFBS;
+        if (vit && (out & HHMM_OUT_GAMMA) && !(out & extra) && a.xpk && a.scan_cl == 0 &&
+            (a.flags & HHMM_FLAG_FUSED) && !use_vit_states(a))
+            return launch_fbv<MODEL, K>(a, st);
     }
     hipStream_t vs = st;
     if (vit && any_fwd && !(a.flags & HHMM_FLAG_NO_FUSE)) {

@@ -41,6 +41,7 @@ FLAG_SCAN_OFF = 1 << 1
 FLAG_NO_FUSE = 1 << 2
 FLAG_VIT_LANES = 1 << 3
 FLAG_VIT_STATES = 1 << 4
+FLAG_FUSED = 1 << 5
 
 
 def flag_scan_chunk_log2(n):

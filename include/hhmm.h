@@ -185,6 +185,13 @@ typedef struct hhmm_draws {
  * pair; results are bit-identical either way.  These force one or the other. */
 #define HHMM_FLAG_VIT_LANES (1u << 3)
 #define HHMM_FLAG_VIT_STATES (1u << 4)
+/* hmm-multinom at K = 4 with gamma_tk (+ loglik) and zstar_t / logp_zstar in one
+ * request (the C2 profile, lane decoder): run both halves as ONE fused sweep
+ * over a single pass of x instead of two concurrent kernels (identical
+ * results).  Measured slower on MI355X (C2: 11.3 against 10.4 ms; both
+ * emission tables in LDS hold the fused kernel at one wave per SIMD), so the
+ * two-kernel schedule is the default. */
+#define HHMM_FLAG_FUSED (1u << 5)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */

@@ -77,10 +77,12 @@ def test_c1_full_size(engine, oracle):
 
 # ---- C2: hmm-multinom K=4, L=9, T=1000 ---------------------------------------------------
 
-@pytest.mark.parametrize("flags", [0, _abi.FLAG_VIT_LANES], ids=["auto", "lane-viterbi"])
+@pytest.mark.parametrize("flags", [0, _abi.FLAG_VIT_LANES, _abi.FLAG_VIT_LANES | _abi.FLAG_FUSED],
+                         ids=["auto", "lane", "lane-fused"])
 def test_c2_slice(engine, oracle, flags):
-    """A 4096-pair zip slice; `lane-viterbi` forces the lane-per-pair decoder
-    the full 1M-pair batch dispatches to (P >= 131072)."""
+    """A 4096-pair zip slice; `lane` forces the lane-per-pair decoder the full
+    1M-pair batch dispatches to (P >= 131072); `lane-fused` the same as the
+    one-kernel forward-backward + Viterbi sweep (HHMM_FLAG_FUSED)."""
     data, draws = synth.hmm_multinom(N=4096, S=4096, T=1000, K=4, L=9)
     got, ref = gpu_and_oracle(engine, oracle, "hmm-multinom", data, draws, HOT, pairing="zip", flags=flags)
     compare_all(got, ref, HOT + ["pair_status"])
@@ -94,16 +96,16 @@ def _bench_module():
 
 def test_c2_full_batch(engine, oracle):
     """The bench's exact workload: 1,000,000 pairs x T=1000 built on the
-    device, both requests (fb + Viterbi) through hhmm_run_device.  Properties
-    over the whole batch, oracle parity on 48 pairs sampled across it."""
+    device, the bench's one request through hhmm_run_device.  Properties
+    over the whole batch, oracle parity on 48 pairs sampled across it, and
+    the fused sweep (HHMM_FLAG_FUSED) bit-identical to it on every pair."""
     import torch
     bench = _bench_module()
     P, T, K, L = 1_000_000, 1000, 4, 9
     dev = torch.device("cuda", torch.cuda.current_device())
     x, draws = bench.make_batch(P, T, synth.SEED, dev)
     run = bench.DeviceRun(engine, x, draws, P, T, dev)
-    run.launch("fb")
-    run.launch("viterbi")
+    run.launch("step")
     torch.cuda.synchronize()
     out = run.out
     assert int((out["pair_status"] != 0).sum()) == 0
@@ -130,6 +132,14 @@ def test_c2_full_batch(engine, oracle):
     got = {"loglik": ll[ii].cpu().numpy(), "logp_zstar": lz[ii].cpu().numpy(),
            "zstar_t": zs[:, ii].T.cpu().numpy(), "gamma_tk": g[:, :, ii].permute(2, 1, 0).cpu().numpy()}
     compare_all(got, ref, HOT)
+    # the fused sweep gives the same bits
+    z1, ll1, lz1 = zs.clone(), ll.clone(), lz.clone()
+    gs1 = g[:, :, ii].clone()
+    gsum1 = g.sum(dim=(0, 1))
+    run.launch("fused")
+    torch.cuda.synchronize()
+    assert torch.equal(zs, z1) and torch.equal(ll, ll1) and torch.equal(lz, lz1)
+    assert torch.equal(g[:, :, ii], gs1) and torch.equal(g.sum(dim=(0, 1)), gsum1)
 
 
 # ---- C3: iohmm-reg K=4, M=4, T=300, grid of series x 4000 draws --------------------------

@@ -2,7 +2,10 @@
 """Interleaved A/B timing of libhhmm variants in ONE process on ONE device
 (cdna_hip_programming.md §5.4 rule 24: cross-box numbers are not comparable).
 
-  python tools/ab_bench.py NAME=path/to/libhhmm.so [NAME=...] [--rounds 5] [--pairs 1000000] [--T 1000]
+  python tools/ab_bench.py NAME=path/to/libhhmm.so[@VAR=VAL,...] [NAME=...] [--rounds 5] [--pairs 1000000] [--T 1000]
+
+(@VAR=VAL sets environment variables around that variant's launches, e.g. the
+HHMM_PROBE_*_LDS_KB occupancy probes of hhmm_hmm.h)
 
 Each variant runs the bench.py C2 step (fb_kernel, then viterbi_kernel, then
 the two concurrently on two streams as bench.py does: "pair") on
@@ -12,6 +15,7 @@ cross-check each other's outputs (gamma within 1e-12, zstar exact).
 """
 import argparse
 import json
+import os
 import pathlib
 import sys
 
@@ -34,8 +38,12 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     libs = {}
+    envs = {}
     for v in a.variants:
         name, path = v.split("=", 1)
+        if "@" in path:  # NAME=lib.so@VAR=VAL,VAR=VAL: environment set around this variant's launches
+            path, ev = path.split("@", 1)
+            envs[name] = dict(kv.split("=", 1) for kv in ev.split(","))
         libs[name] = hhmm_amd.load_library(path)
     x, draws = bench.make_batch(a.pairs, a.T, 9000, dev)
     runs = {n: bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev) for n, lib in libs.items()}
@@ -57,6 +65,9 @@ def main():
     ref = None
     for r in range(a.rounds + 1):
         for n, run in runs.items():
+            for k in set().union(*envs.values()) if envs else ():
+                os.environ.pop(k, None)
+            os.environ.update(envs.get(n, {}))
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             torch.cuda.synchronize()
             ev[0].record()
