@@ -55,11 +55,11 @@ def parse():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the 64-pair oracle check of the timed data (run after warmup, outside the "
                          "timed region)")
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "f1"],
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "n1", "f1"],
                     help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
                          "printed as its own line: c1 hmm Gaussian K=3 T=500, c3 iohmm-reg grid, c4 iohmm-hmix "
-                         "+ FFBS, c5 Tayal T=1e6 (parallel scan over T); f1 = the tick -> leg feature extractor "
-                         "(SURVEY §8 F1)")
+                         "+ FFBS, c5 Tayal T=1e6 (parallel scan over T); n1 = hmm-multinom at K=23 (SURVEY §8 N1); "
+                         "f1 = the tick -> leg feature extractor (SURVEY §8 F1)")
     ap.add_argument("--ticks", type=int, default=100_000_000, help="f1: ticks per GPU")
     ap.add_argument("--pars", default=None,
                     help="c3-c5 probes: comma-separated outputs instead of the workload's")
@@ -396,6 +396,10 @@ WORKLOADS = {
            ["loglik", "gamma_tk", "z_ffbs"],
            lambda T, S: 32 + 4 + 8 + (8 + 32) / S + 8 * (4 + 4 * 4 + 3 * 4 * 3) / T,
            "C4 iohmm-hmix K=4 L=3 M=4 T=10k, 16 series x 4096 draws, batched FFBS"),
+    "n1": ("hmm-multinom", dict(N=1000, S=100, T=1000, K=23, L=9), "grid",
+           ["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
+           lambda T, S: 23 * 8 + 4 + 4 / S + 8 * (23 + 23 * 23 + 23 * 9) / T,
+           "N1 hmm-multinom K=23 L=9 T=1000 (large-K state-parallel kernels), 1000 series x 100 draws, grid"),
     "c5": ("hhmm-tayal2009", dict(N=1, S=250, T=1_000_000, L=9), "grid",
            ["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
            lambda T, S: 32 + 4 + 8 / S + (8 * (1 + 4 + 36) + 16) / T,

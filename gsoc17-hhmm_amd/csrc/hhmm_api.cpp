@@ -233,6 +233,8 @@ static int64_t npairs(const hhmm_request *r)
         return r->data.n_series == r->draws.n_draws ? r->data.n_series : -1;
     if (r->pairing == HHMM_PAIR_GRID)
         return r->data.n_series * r->draws.n_draws;
+    if (r->pairing == HHMM_PAIR_BLOCK)
+        return r->draws.n_draws % r->data.n_series == 0 ? r->draws.n_draws : -1;
     return -1;
 }
 
@@ -258,13 +260,16 @@ static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool ho
     REQUIRE(r && o, "request and result must be non-NULL");
     REQUIRE(r->abi_version == HHMM_ABI_VERSION, "abi_version %u != %u", r->abi_version, HHMM_ABI_VERSION);
     REQUIRE(r->model >= 1 && r->model <= 9, "unknown model id %d", r->model);
-    REQUIRE(r->pairing == HHMM_PAIR_GRID || r->pairing == HHMM_PAIR_ZIP, "unknown pairing %d", r->pairing);
+    REQUIRE(r->pairing == HHMM_PAIR_GRID || r->pairing == HHMM_PAIR_ZIP || r->pairing == HHMM_PAIR_BLOCK,
+            "unknown pairing %d", r->pairing);
     const hhmm_data &d = r->data;
     const hhmm_draws &w = r->draws;
     REQUIRE(d.n_series >= 1, "n_series must be >= 1");
     REQUIRE(w.n_draws >= 1, "n_draws must be >= 1");
-    REQUIRE(npairs(r) >= 1, "ZIP pairing needs n_series == n_draws (%lld vs %lld)", (long long)d.n_series,
-            (long long)w.n_draws);
+    REQUIRE(npairs(r) >= 1, "%s pairing needs %s (n_series %lld, n_draws %lld)",
+            r->pairing == HHMM_PAIR_ZIP ? "ZIP" : "BLOCK",
+            r->pairing == HHMM_PAIR_ZIP ? "n_series == n_draws" : "n_draws a multiple of n_series",
+            (long long)d.n_series, (long long)w.n_draws);
     REQUIRE(d.T_max >= 1, "T_max must be >= 1 (int<lower=1> T)");
     /* kernels address rows as uniform base + 32-bit lane offset (8-byte elements) */
     REQUIRE(npairs(r) <= (int64_t(1) << 28) && d.n_series <= (int64_t(1) << 28) && w.n_draws <= (int64_t(1) << 28),

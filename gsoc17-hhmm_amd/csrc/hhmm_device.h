@@ -152,6 +152,9 @@ __device__ __forceinline__ void pair_coords(const DevArgs &a, int64_t p, int64_t
     if (a.pairing == HHMM_PAIR_ZIP) {
         n = p;
         d = p;
+    } else if (a.pairing == HHMM_PAIR_BLOCK) { /* series n's own block of S / N draws */
+        n = p / (a.S / a.N);
+        d = p;
     } else {
         n = p / a.S;
         d = p - n * a.S;

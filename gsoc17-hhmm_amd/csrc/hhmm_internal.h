@@ -18,7 +18,7 @@ struct DevArgs {
     int64_t P;          /* pairs */
     int64_t N;          /* series */
     int64_t S;          /* draws */
-    int32_t pairing;    /* HHMM_PAIR_GRID / ZIP */
+    int32_t pairing;    /* HHMM_PAIR_GRID / ZIP / BLOCK */
     int32_t model;
     int32_t K, L, M;
     int32_t Tmax;       /* padded extent of the time axis of the data arrays in use */
@@ -87,7 +87,8 @@ constexpr int fb_chunk(int K) { return K <= 4 ? 8 : 4; }
 constexpr int bp_bits(int K) { return K <= 2 ? 1 : (K <= 4 ? 2 : (K <= 8 ? 3 : 4)); }
 constexpr int bp_steps_per_word(int K) { return 32 / (K * bp_bits(K)); }
 
-constexpr int kMaxK = 8;
+constexpr int kMaxK = 8;       /* lane-per-pair kernels (hhmm_hmm.h, hhmm_iohmm.h) */
+constexpr int kMaxKLarge = 32; /* state-parallel HMM-family kernels (hhmm_large.h) */
 constexpr int kBlock = 256;
 constexpr size_t kLdsLimit = 160 * 1024;
 
@@ -110,6 +111,8 @@ hhmm_status run_semisup_lo(const DevArgs &a, const hhmm_request *req, const hhmm
 hhmm_status run_semisup_hi(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
 hhmm_status run_tayal(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
 hhmm_status run_tayal_lite(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
+/* hmm / hmm-multinom at kMaxK < K <= kMaxKLarge (hhmm_m_large.hip) */
+hhmm_status run_large(const DevArgs &a, hipStream_t st);
 
 /* IOHMM family (iohmm-reg / -mix / -hmix / -hmix-lite), hhmm_iohmm.hip. */
 hhmm_status launch_iohmm(const DevArgs &a, hipStream_t stream);

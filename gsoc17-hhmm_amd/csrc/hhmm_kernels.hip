@@ -80,6 +80,10 @@ static bool is_iohmm_model(int model)
 static int nchunk_of(int K, int T) { return (T + fb_chunk(K) - 1) / fb_chunk(K); }
 static int nword_of(int K, int T) { return T / bp_steps_per_word(K) + 1; }
 
+/* K > kMaxK (hhmm_large.h): 8-step checkpoints [rows][K][P], one back-pointer
+ * byte per (pair, state, t) in rows of T_max rounded up to 16 */
+static bool large_k(int K) { return K > kMaxK; }
+
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 /* Parallel scan over T for the HMM-family forward-backward:
@@ -93,8 +97,8 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
     const uint32_t fb_out = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
                             HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
     /* the log-scale outputs run the sequential log-space recursion (hhmm_hmm.h) */
-    if (!family || (flags & HHMM_FLAG_SCAN_OFF) || (outputs & (HHMM_OUT_FFBS | HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) ||
-        !(outputs & fb_out))
+    if (!family || K > kMaxK || (flags & HHMM_FLAG_SCAN_OFF) ||
+        (outputs & (HHMM_OUT_FFBS | HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) || !(outputs & fb_out))
         return sp;
     const int C = fb_chunk(K);
     const int log2cl = (int)((flags >> 8) & 0xffu);
@@ -139,6 +143,14 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     };
     const size_t d = sizeof(double);
     w.sp = scan_plan(model, K, Tmax, P, outputs, flags);
+    if (large_k(K)) {
+        if (needs_ckpt(model, outputs))
+            w.ckpt = take((size_t)((Tmax + 7) / 8) * K * P * d);
+        if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
+            w.bp = take((size_t)P * K * (size_t)((Tmax + 15) & ~15));
+        w.total = off + 256;
+        return w;
+    }
     if (w.sp.cl > 0) {
         /* phase-3 checkpoint columns: one per (pair rounded up to whole waves, chunk) */
         const size_t nc = (size_t)w.sp.nc, G = (size_t)scan_lanes_per_chunk(P) * nc,
@@ -264,6 +276,17 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
     DevArgs a = make_args(req, res, P);
     bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max, (uint32_t)req->flags);
     const bool lo = a.K <= 4;
+    if (a.K > kMaxK) {
+        if (req->model != HHMM_MODEL_HMM_GAUSS && req->model != HHMM_MODEL_HMM_MULTINOM) {
+            set_error("K = %d: the device path of model %d supports K <= %d", a.K, req->model, kMaxK);
+            return HHMM_ERR_UNSUPPORTED;
+        }
+        if (a.K > kMaxKLarge) {
+            set_error("K = %d: the device path supports K <= %d", a.K, kMaxKLarge);
+            return HHMM_ERR_UNSUPPORTED;
+        }
+        return run_large(a, st);
+    }
     switch (req->model) {
     case HHMM_MODEL_HMM_GAUSS: return lo ? run_gauss_lo(a, req, res, st) : run_gauss_hi(a, req, res, st);
     case HHMM_MODEL_HMM_MULTINOM: return lo ? run_multinom_lo(a, req, res, st) : run_multinom_hi(a, req, res, st);

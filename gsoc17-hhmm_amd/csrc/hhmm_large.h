@@ -1,0 +1,592 @@
+/*
+ * hhmm_large.h -- the HMM family at large K (8 < K <= 32):
+ * hmm/stan/hmm.stan and hmm/stan/hmm-multinom.stan with free `int<lower=1> K`
+ * (hmm-multinom.stan:9), e.g. the 23-state flattened HHMMs the reference
+ * discusses (log.md:657, tayal2009/main.Rmd:310-346).
+ *
+ * Layout: a GROUP of G = 32 lanes owns one (series, draw) pair, lane j state
+ * j (lanes j >= K idle), two pairs per wave.  The K x K transition matrix is
+ * split by column and row over the group: lane j keeps column j (forward,
+ * Viterbi) and row j (backward) in registers.  Each step the group exchanges
+ * its state vector through a per-pair LDS slot -- every lane writes its
+ * entry, then reads all K back as broadcast ds_read_b128 -- and reduces
+ * across the group with 32-lane shuffles (renormalisation max, gamma sum).
+ * The emission table (multinomial: phi[l][j] per pair) sits in LDS so lane
+ * j reads its own state's column for the step's symbol.
+ *
+ * Arithmetic is the lane-per-pair kernels' (hhmm_hmm.h) with the K-vector
+ * spread over lanes: the same linear-space scaled filter (K FMAs in the same
+ * i order, an exact power-of-two renormalisation per step), the same
+ * checkpoint-and-recompute backward sweep, and for the Viterbi the same
+ * candidate order (delta + log A) + emission with strict '>' and the Q3 NaN
+ * row -- so paths and logp_zstar are bit-identical to the oracle.
+ * Back-pointers are one byte per (pair, state, t), [P][K][T_max] (16-byte
+ * aligned rows); the backtrack walks them kLBack steps at a time, each lane
+ * holding its state's bytes of the chunk and the path state passed by a
+ * shuffle per step.
+ *
+ * Outputs: loglik, alpha_tk, beta_tk, ungamma_tk, gamma_tk, zstar_t,
+ * logp_zstar (the log-scale unalpha / unbeta and FFBS stay on K <= 8).
+ * Bound: VALU -- K^2 FMAs per pair-step (529 at K = 23) against 8K output
+ * bytes; the output stores are 8 B per lane (two pairs per wave).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "hhmm_device.h"
+
+namespace hhmm {
+
+constexpr int kLG = 32;     /* lanes per pair */
+constexpr int kLChunk = 8;  /* steps per forward checkpoint */
+constexpr int kLBack = 16;  /* backtrack steps per back-pointer chunk */
+
+/* bytes per (pair, state) back-pointer row */
+__host__ __device__ constexpr int lk_row_bytes(int Tmax) { return (Tmax + 15) & ~15; }
+
+template <int MODEL>
+struct LkTraits {
+    static constexpr bool kGauss = (MODEL == HHMM_MODEL_HMM_GAUSS);
+};
+
+/* group reductions over the 32 lanes of a pair (the pair's lanes are one
+ * aligned 32-lane half of the wave) */
+__device__ __forceinline__ double grp_max(double v)
+{
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1)
+        v = fmax(v, __shfl_xor(v, off, kLG));
+    return v;
+}
+__device__ __forceinline__ double grp_sum(double v)
+{
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1)
+        v += __shfl_xor(v, off, kLG);
+    return v;
+}
+
+/* Per-lane state of one pair's group. */
+template <int MODEL>
+struct LkLane {
+    int j;          /* this lane's state (>= K: idle) */
+    bool on;        /* j < K */
+    int64_t p, n, d;
+    int Tp, K, L;
+    double col[kLG]; /* A[i][j] (probabilities; Viterbi: log) */
+    double row[kLG]; /* A[j][i] (backward) */
+    double pj;       /* p_1k[j] */
+    double mu, isig, c0, lsig; /* gauss, state j */
+    double *xch;     /* this pair's LDS exchange slots: 2 x kLG doubles */
+    const double *tab; /* multinomial: this pair's [L][kLG] emission table */
+};
+
+template <int MODEL>
+__device__ __forceinline__ void lk_setup(LkLane<MODEL> &ln, const DevArgs &a, double *lds, bool LOG)
+{
+    const int tid = threadIdx.x;
+    const int g = tid / kLG;                 /* group in the workgroup */
+    const int gpb = blockDim.x / kLG;        /* groups per workgroup */
+    ln.j = tid % kLG;
+    ln.K = a.K;
+    ln.L = a.L;
+    ln.on = ln.j < a.K;
+    ln.p = min((int64_t)blockIdx.x * gpb + g, a.P - 1);
+    pair_coords(a, ln.p, ln.n, ln.d);
+    ln.Tp = pair_len(a, ln.n);
+    const int jj = ln.on ? ln.j : 0;
+    const int64_t S = a.S, d = ln.d;
+    double rawc[kLG], rawr[kLG];
+#pragma unroll
+    for (int i = 0; i < kLG; ++i) {
+        rawc[i] = 0.0;
+        rawr[i] = 0.0;
+        if (i < a.K) {
+            rawc[i] = a.A_ij[d + S * ((int64_t)i + (int64_t)a.K * jj)];
+            rawr[i] = a.A_ij[d + S * ((int64_t)jj + (int64_t)a.K * i)];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kLG; ++i) {
+        ln.col[i] = (LOG && i < a.K) ? hhmm_cr_log(rawc[i]) : rawc[i];
+        ln.row[i] = rawr[i];
+    }
+    ln.pj = a.p_1k[d + S * jj];
+    if constexpr (LkTraits<MODEL>::kGauss) {
+        const double sg = a.sigma_k[d + S * jj];
+        ln.mu = a.mu_k[d + S * jj];
+        ln.isig = 1.0 / sg;
+        ln.lsig = hhmm_cr_log(sg);
+        ln.c0 = HHMM_NEG_LOG_SQRT_TWO_PI - ln.lsig;
+    }
+    /* LDS: [groups][2][kLG] exchange, then [groups][L][kLG] tables */
+    ln.xch = lds + (size_t)g * 2 * kLG;
+    double *tab = lds + (size_t)gpb * 2 * kLG + (size_t)g * a.L * kLG;
+    ln.tab = tab;
+    if constexpr (!LkTraits<MODEL>::kGauss) {
+        for (int l0 = 0; l0 < a.L; l0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                v[r] = a.phi_k[d + S * ((int64_t)jj + (int64_t)a.K * min(l0 + r, a.L - 1))];
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (l0 + r < a.L)
+                    tab[(l0 + r) * kLG + ln.j] = (LOG && ln.on) ? hhmm_cr_log(v[r]) : v[r];
+        }
+    }
+    __syncthreads();
+}
+
+/* Observations come a block of kLG steps at a time: lane j of the group
+ * loads step 32b + j (clamped, unconditional), one load instruction per 32
+ * steps, issued a block ahead; step t's symbol is then one shuffle from lane
+ * t % 32 of the group. */
+template <int MODEL>
+struct LkObs {
+    int x;
+    double xr;
+};
+
+template <int MODEL>
+__device__ __forceinline__ LkObs<MODEL> lk_block(const LkLane<MODEL> &ln, const DevArgs &a, int b)
+{
+    const int tc = min(max(b * kLG + ln.j, 0), a.Tmax - 1);
+    LkObs<MODEL> o;
+    o.x = 1;
+    o.xr = 0.0;
+    if constexpr (LkTraits<MODEL>::kGauss)
+        o.xr = a.xr[ln.n + a.N * (int64_t)tc];
+    else
+        o.x = a.x[ln.n + a.N * (int64_t)tc];
+    return o;
+}
+
+template <int MODEL>
+__device__ __forceinline__ void lk_get(const LkObs<MODEL> &blk, int u, int &x, double &xr)
+{
+    x = 1;
+    xr = 0.0;
+    if constexpr (LkTraits<MODEL>::kGauss)
+        xr = __shfl(blk.xr, u, kLG);
+    else
+        x = __shfl(blk.x, u, kLG);
+}
+
+/* Stan's normal_lpdf(y | mu_j, sigma_j), as gauss_lpdf. */
+template <int MODEL>
+__device__ __forceinline__ double lk_lpdf(const LkLane<MODEL> &ln, double y)
+{
+    const double z = (y - ln.mu) * ln.isig;
+    const double z2 = z * z;
+    return ln.c0 + (-0.5 * z2);
+}
+
+/* Linear-space emission e_t(j) and its log scale m (gauss: densities over
+ * their group max, as emit_prob); idle lanes 0. */
+template <int MODEL>
+__device__ __forceinline__ double lk_emit(const LkLane<MODEL> &ln, int x, double xr, double &m)
+{
+    if constexpr (LkTraits<MODEL>::kGauss) {
+        const double lp = ln.on ? lk_lpdf(ln, xr) : dev_ninf();
+        m = grp_max(lp);
+        return ln.on ? exp(lp - m) : 0.0;
+    } else {
+        m = 0.0;
+        const int xc = min(max(x, 1), ln.L);
+        return ln.on ? ln.tab[(xc - 1) * kLG + ln.j] : 0.0;
+    }
+}
+
+/* The group's K-vector v (this lane's entry) through LDS slot `slot`: w[i] =
+ * v of state i for i < K (0 beyond). */
+__device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, double v, double (&w)[kLG], int K)
+{
+    double *s = xch + slot * kLG;
+    s[j] = v;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < kLG; i += 2) {
+        if (i < K) {
+            const double2 q = *reinterpret_cast<const double2 *>(s + i);
+            w[i] = q.x;
+            w[i + 1] = (i + 1 < K) ? q.y : 0.0;
+        } else {
+            w[i] = 0.0;
+            w[i + 1] = 0.0;
+        }
+    }
+}
+
+/* Power-of-two renormalisation over the group (renorm<K>). */
+__device__ __forceinline__ double grp_renorm(double v, int &ex)
+{
+    const double mx = grp_max(v);
+    const int e = __builtin_amdgcn_frexp_exp(mx);
+    ex += e;
+    return ldexp(v, -e);
+}
+
+/* alpha_t(j) = e_t(j) * sum_i alpha_{t-1}(i) A(i, j): the fma chain of fwd_step_raw. */
+template <int MODEL>
+__device__ __forceinline__ double lk_fwd(const LkLane<MODEL> &ln, const double (&w)[kLG], double e)
+{
+    double acc = w[0] * ln.col[0];
+#pragma unroll
+    for (int i = 1; i < kLG; ++i)
+        if (i < ln.K)
+            acc = fma(w[i], ln.col[i], acc);
+    return ln.on ? acc * e : 0.0;
+}
+
+/* beta_{t-1}(j) = sum_i A(j, i) b_i, b_i = e_t(i) beta_t(i) (bwd_step). */
+template <int MODEL>
+__device__ __forceinline__ double lk_bwd(const LkLane<MODEL> &ln, const double (&w)[kLG])
+{
+    double acc = ln.row[0] * w[0];
+#pragma unroll
+    for (int i = 1; i < kLG; ++i)
+        if (i < ln.K)
+            acc = fma(ln.row[i], w[i], acc);
+    return ln.on ? acc : 0.0;
+}
+
+template <int MODEL>
+__device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLane<MODEL> &ln, int t, double v)
+{
+    if (ln.on && out)
+        out[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
+}
+
+/* Forward-backward: loglik, alpha, beta, ungamma, gamma. */
+template <int MODEL>
+__global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
+{
+    HIP_DYNAMIC_SHARED(double, lds)
+    LkLane<MODEL> ln;
+    lk_setup<MODEL>(ln, a, lds, false);
+    const uint32_t out = a.outputs;
+    const bool need_bwd = (out & (HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
+    const int Tp = ln.Tp; /* per pair: uniform over the group (the wave's two groups may differ) */
+    const int K = ln.K;
+    double w[kLG];
+    int slot = 0;
+    auto ckpt = [&](int c) -> double & { return a.ckpt[ln.p + a.P * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
+
+    /* ---- forward: alpha_1 (hmm.stan:30 Q2 / hmm-multinom.stan:31), then the recursion ---- */
+    LkObs<MODEL> bcur = lk_block<MODEL>(ln, a, 0), bnxt = lk_block<MODEL>(ln, a, 1);
+    double al, lsc = 0.0;
+    int ex = 0;
+    {
+        int x;
+        double xr, m;
+        lk_get<MODEL>(bcur, 0, x, xr);
+        if constexpr (LkTraits<MODEL>::kGauss) {
+            /* log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k): alpha_1 = p_1k */
+            const double z = (xr - ln.mu) * ln.isig;
+            const double tk = ln.on ? (HHMM_NEG_LOG_SQRT_TWO_PI - ln.lsig) + (-0.5 * (z * z)) : 0.0;
+            lsc += grp_sum(tk);
+            al = ln.on ? ln.pj : 0.0;
+        } else {
+            const double e = lk_emit<MODEL>(ln, x, xr, m);
+            al = ln.on ? ln.pj * e : 0.0;
+        }
+        al = grp_renorm(al, ex);
+    }
+    if (need_bwd) {
+        if (ln.on)
+            ckpt(0) = al;
+    } else if ((out & HHMM_OUT_ALPHA) && a.alpha) {
+        lk_put<MODEL>(a.alpha, a, ln, 0, al / grp_sum(al));
+    }
+    for (int t = 1; t < Tp; ++t) {
+        const int u = t % kLG;
+        if (u == 0) { /* group-uniform: next block of observations, prefetch the one after */
+            bcur = bnxt;
+            bnxt = lk_block<MODEL>(ln, a, t / kLG + 1);
+        }
+        int x;
+        double xr, m;
+        lk_get<MODEL>(bcur, u, x, xr);
+        const double e = lk_emit<MODEL>(ln, x, xr, m);
+        grp_exchange(ln.xch, slot, ln.j, al, w, K);
+        slot ^= 1;
+        lsc += m;
+        al = grp_renorm(lk_fwd<MODEL>(ln, w, e), ex);
+        if (!need_bwd) {
+            if ((out & HHMM_OUT_ALPHA) && a.alpha)
+                lk_put<MODEL>(a.alpha, a, ln, t, al / grp_sum(al));
+        } else if (t % kLChunk == 0 && ln.on) {
+            ckpt(t / kLChunk) = al;
+        }
+    }
+    {
+        const double sa = grp_sum(al); /* every lane takes part in the shuffle */
+        if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0)
+            a.loglik[ln.p] = log(sa) + (lsc + kLn2 * ex);
+    }
+    if (!need_bwd)
+        return;
+
+    /* ---- backward sweep, chunk by chunk from the end: recompute alpha from
+     * the checkpoint (prefetched a chunk ahead), then walk the chunk
+     * backwards emitting the posteriors and stepping beta (bwd_chunk) ---- */
+    double be = ln.on ? 1.0 : 0.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
+    int bex = 0;
+    constexpr int CPB = kLG / kLChunk; /* chunks per observation block */
+    const int nck = (Tp + kLChunk - 1) / kLChunk;
+    int cb = (nck - 1) / CPB;
+    LkObs<MODEL> ob = lk_block<MODEL>(ln, a, cb), obp = lk_block<MODEL>(ln, a, cb - 1);
+    double ck = ckpt(nck - 1), ckn = ckpt(max(nck - 2, 0));
+    for (int c = nck - 1; c >= 0; --c) {
+        if (c / CPB != cb) { /* group-uniform: step back one observation block */
+            cb = c / CPB;
+            ob = obp;
+            obp = lk_block<MODEL>(ln, a, cb - 1);
+        }
+        const int t0 = c * kLChunk;
+        const int ub = t0 % kLG; /* the chunk's first step inside the block */
+        double es[kLChunk];
+#pragma unroll
+        for (int u = 0; u < kLChunk; ++u) {
+            int x;
+            double xr, m;
+            lk_get<MODEL>(ob, ub + u, x, xr);
+            es[u] = lk_emit<MODEL>(ln, x, xr, m);
+        }
+        double abuf[kLChunk];
+        abuf[0] = ln.on ? ck : 0.0;
+        ck = ckn;
+        ckn = ckpt(max(c - 2, 0));
+        int exb = 0;
+#pragma unroll
+        for (int u = 1; u < kLChunk; ++u) {
+            abuf[u] = 0.0;
+            if (t0 + u < Tp) { /* group-uniform */
+                grp_exchange(ln.xch, slot, ln.j, abuf[u - 1], w, K);
+                slot ^= 1;
+                abuf[u] = grp_renorm(lk_fwd<MODEL>(ln, w, es[u]), exb);
+            }
+        }
+#pragma unroll
+        for (int u = kLChunk - 1; u >= 0; --u) {
+            const int t = t0 + u;
+            if (t >= Tp)
+                continue;
+            const double av = abuf[u];
+            const double sa = grp_sum(av), sb = grp_sum(be);
+            if ((out & HHMM_OUT_ALPHA) && a.alpha)
+                lk_put<MODEL>(a.alpha, a, ln, t, av / sa);
+            if ((out & HHMM_OUT_BETA) && a.beta)
+                lk_put<MODEL>(a.beta, a, ln, t, be / sb);
+            if (out & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
+                /* gamma = normalize(alpha .* beta) from the normalised vectors (hmm.stan:89-96) */
+                const double ug = (av / sa) * (be / sb);
+                if ((out & HHMM_OUT_UNGAMMA) && a.ungamma)
+                    lk_put<MODEL>(a.ungamma, a, ln, t, ug);
+                if ((out & HHMM_OUT_GAMMA) && a.gamma) {
+                    const double sg = grp_sum(ug);
+                    lk_put<MODEL>(a.gamma, a, ln, t, ug / sg);
+                }
+            }
+            if (t > 0) {
+                grp_exchange(ln.xch, slot, ln.j, es[u] * be, w, K);
+                slot ^= 1;
+                be = grp_renorm(lk_bwd<MODEL>(ln, w), bex);
+            }
+        }
+    }
+}
+
+/* ---- Viterbi (hmm.stan:98-130; hmm-multinom.stan:100-132) ---- */
+
+/* SSE2 maxCoeff order of stan_max_vec for a runtime K (oracle stan_max_vec). */
+__device__ __forceinline__ double stan_max_rt(const double (&d)[kLG], int n)
+{
+    if (n < 2)
+        return d[0];
+    const int aligned = n & ~1, aligned2 = n & ~3;
+    double r0a = d[0], r0b = d[1];
+    if (aligned > 2) {
+        double r1a = d[2], r1b = d[3];
+#pragma unroll
+        for (int i = 4; i + 4 <= kLG; i += 4) {
+            if (i < aligned2) {
+                r0a = sse_max(r0a, d[i]);
+                r0b = sse_max(r0b, d[i + 1]);
+                r1a = sse_max(r1a, d[i + 2]);
+                r1b = sse_max(r1b, d[i + 3]);
+            }
+        }
+        r0a = sse_max(r0a, r1a);
+        r0b = sse_max(r0b, r1b);
+        if (aligned > aligned2) {
+#pragma unroll
+            for (int q = 4; q + 2 <= kLG; q += 4)
+                if (q == aligned2) {
+                    r0a = sse_max(r0a, d[q]);
+                    r0b = sse_max(r0b, d[q + 1]);
+                }
+        }
+    }
+    double res = sse_max(r0a, r0b);
+#pragma unroll
+    for (int i = 2; i < kLG; ++i)
+        if (i >= aligned && i < n)
+            res = std_max(res, d[i]);
+    return res;
+}
+
+template <int MODEL>
+__global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
+{
+    HIP_DYNAMIC_SHARED(double, lds)
+    LkLane<MODEL> ln;
+    lk_setup<MODEL>(ln, a, lds, true);
+    const int Tp = ln.Tp;
+    const int K = ln.K;
+    double w[kLG];
+    int slot = 0;
+    auto emit_log = [&](int x, double xr) -> double {
+        if constexpr (LkTraits<MODEL>::kGauss)
+            return ln.on ? lk_lpdf(ln, xr) : 0.0;
+        else
+            return ln.on ? ln.tab[(min(max(x, 1), ln.L) - 1) * kLG + ln.j] : 0.0;
+    };
+    /* back-pointers [P][K][Tb] bytes, Tb = T_max rounded up to 16: a state's
+     * bytes are contiguous in t and its row 16-byte aligned */
+    const int Tb = lk_row_bytes(a.Tmax);
+    uint8_t *bp = reinterpret_cast<uint8_t *>(a.bp) + ((int64_t)ln.p * K + (ln.on ? ln.j : 0)) * Tb;
+
+    /* delta_tk[1, K] = emission of state K only (Q3: the others keep NaN) */
+    LkObs<MODEL> bcur = lk_block<MODEL>(ln, a, 0), bnxt = lk_block<MODEL>(ln, a, 1);
+    int x;
+    double xr;
+    lk_get<MODEL>(bcur, 0, x, xr);
+    const double le0 = emit_log(x, xr);
+    double dl = (ln.j == K - 1) ? le0 : dev_nan();
+    for (int t = 1; t < Tp; ++t) {
+        const int u = t % kLG;
+        if (u == 0) {
+            bcur = bnxt;
+            bnxt = lk_block<MODEL>(ln, a, t / kLG + 1);
+        }
+        lk_get<MODEL>(bcur, u, x, xr);
+        const double le = emit_log(x, xr);
+        grp_exchange(ln.xch, slot, ln.j, dl, w, K);
+        slot ^= 1;
+        /* candidate (delta + log A) + emission, strict '>' from -inf; the
+         * running max as fmax (vit_step): NaN never wins, first i on ties */
+        double best = dev_ninf();
+        int arg = 0;
+#pragma unroll
+        for (int i = 0; i < kLG; ++i) {
+            if (i < K) {
+                const double cand = (w[i] + ln.col[i]) + le;
+                const bool gt = cand > best;
+                best = fmax(best, cand);
+                arg = gt ? i : arg;
+            }
+        }
+        dl = ln.on ? best : dev_ninf();
+        if (ln.on)
+            bp[t] = (uint8_t)arg;
+    }
+    /* logp_zstar = max(delta_T) (SSE2 order); zstar_T = LAST j attaining it */
+    grp_exchange(ln.xch, slot, ln.j, dl, w, K);
+    const double lp = stan_max_rt(w, K);
+    int z = -1;
+#pragma unroll
+    for (int j = 0; j < kLG; ++j)
+        if (j < K && w[j] == lp)
+            z = j;
+    const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
+    if (ln.j == 0) {
+        if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
+            a.logp_zstar[ln.p] = lp;
+        if (a.pair_status)
+            a.pair_status[ln.p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+    }
+    if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
+        return;
+    if (invalid) {
+        for (int t = ln.j; t < Tp; t += kLG)
+            a.zstar[ln.p + a.P * (int64_t)t] = 0;
+        return;
+    }
+    /* backtrack, kLBack steps at a time: lane s holds state s's bytes of the
+     * chunk (one 16-byte load, prefetched two chunks ahead), the path state
+     * moves by one shuffle per step, lane u keeps step t0 + u for the store */
+    const int nb = (Tp + kLBack - 1) / kLBack;
+    const int wmax = Tb / kLBack - 1; /* last 16-byte chunk of the row */
+    auto load = [&](int c) -> uint4 {
+        const int cc = min(max(c, 0), wmax);
+        return *reinterpret_cast<const uint4 *>(bp + (int64_t)cc * kLBack);
+    };
+    uint4 q0 = load(nb - 1), q1 = load(nb - 2);
+    for (int c = nb - 1; c >= 0; --c) {
+        const uint4 q2 = load(c - 2);
+        const uint32_t wd[4] = {q0.x, q0.y, q0.z, q0.w};
+        int mine = 0;
+#pragma unroll
+        for (int u = kLBack - 1; u >= 0; --u) {
+            const int t = c * kLBack + u;
+            if (t < Tp) {
+                if ((ln.j & (kLBack - 1)) == u)
+                    mine = z + 1;
+                if (t > 0)
+                    z = __shfl((int)((wd[u >> 2] >> (8 * (u & 3))) & 0xffu), z, kLG);
+            }
+        }
+        const int t = c * kLBack + (ln.j & (kLBack - 1));
+        if (ln.j < kLBack && t < Tp)
+            a.zstar[ln.p + a.P * (int64_t)t] = mine;
+        q0 = q1;
+        q1 = q2;
+    }
+}
+
+/* LDS bytes of a launch with `threads` lanes: exchange slots + tables. */
+static inline size_t lk_lds(const DevArgs &a, int threads, bool discrete)
+{
+    const size_t groups = (size_t)threads / kLG;
+    return groups * 2 * kLG * sizeof(double) + (discrete ? groups * (size_t)a.L * kLG * sizeof(double) : 0);
+}
+
+template <int MODEL>
+static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
+{
+    constexpr bool discrete = !LkTraits<MODEL>::kGauss;
+    const uint32_t out = a.outputs;
+    const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
+    const uint32_t vit = HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+    if (out & ~(fb | vit)) {
+        set_error("K = %d > %d: this build evaluates loglik, alpha, beta, ungamma, gamma, zstar and logp_zstar "
+                  "(no log-scale unalpha / unbeta, no FFBS)", a.K, kMaxK);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    int threads = kBlock;
+    while (threads > kLG && lk_lds(a, threads, discrete) > kLdsLimit)
+        threads /= 2;
+    if (lk_lds(a, threads, discrete) > kLdsLimit) {
+        set_error("emission table of L = %d symbols does not fit in LDS", a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const int gpb = threads / kLG;
+    const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
+    /* checkpoints use the [rows][K][P] layout of the lane kernels */
+    if (out & fb)
+        hipLaunchKernelGGL((lk_fb_kernel<MODEL>), grid, dim3(threads), lk_lds(a, threads, discrete), st, a);
+    if (out & vit)
+        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL>), grid, dim3(threads), lk_lds(a, threads, discrete), st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("large-K kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+} // namespace hhmm

@@ -33,6 +33,7 @@ MODELS = {
 
 PAIR_GRID = 0
 PAIR_ZIP = 1
+PAIR_BLOCK = 2
 
 # hhmm_request.flags
 FLAG_SCAN_AUTO = 0

@@ -95,7 +95,7 @@ class PreparedRequest:
         req = _abi.Request()
         req.abi_version = _abi.ABI_VERSION
         req.model = _abi.MODELS[model]
-        req.pairing = {"grid": _abi.PAIR_GRID, "zip": _abi.PAIR_ZIP}[pairing]
+        req.pairing = {"grid": _abi.PAIR_GRID, "zip": _abi.PAIR_ZIP, "block": _abi.PAIR_BLOCK}[pairing]
         req.device = device
         req.flags = int(flags)
 
@@ -151,7 +151,9 @@ class PreparedRequest:
         req.draws.n_draws = S
         self.N, self.S, self.Tmax, self.K = N, S, Tmax, d.K
         self.T_oos_max = d.T_oos_max
-        self.P = N * S if pairing == "grid" else N
+        if pairing == "block" and S % N:
+            raise ValueError(f"block pairing needs n_draws ({S}) to be a multiple of n_series ({N})")
+        self.P = N * S if pairing == "grid" else (S if pairing == "block" else N)
 
         if pars is None:
             pars = ["loglik", "alpha_tk", "gamma_tk", "zstar_t", "logp_zstar"]

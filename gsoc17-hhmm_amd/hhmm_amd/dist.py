@@ -62,7 +62,8 @@ def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=No
 
     Returns (local, summed_loglik, paths):
       local          this rank's outputs (pairs of its series block, ABI order)
-      summed_loglik  [S] per-draw log-likelihood summed over ALL series (all-reduce)
+      summed_loglik  [S] per-draw log-likelihood summed over ALL series (all-reduce;
+                     zip / block pairing: each draw's own series)
       paths          on rank 0: zstar_t of every pair in global ABI order, else None
     """
     import torch
@@ -78,20 +79,21 @@ def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=No
     S = next(np.asarray(v).shape[0] for v in draws.values())
     b, e = shard_range(N, world, rank)
     ldata = slice_series(data, b, e)
-    ldraws = draws if pairing == "grid" else slice_draws(draws, b, e)
+    B = S // N if pairing == "block" else 1  # draws per series (block pairing: one fit per series)
+    ldraws = draws if pairing == "grid" else slice_draws(draws, b * B, e * B)
     local = compute(model, ldata, ldraws, pars=pars, pairing=pairing) if e > b else {}
 
     dev = device if device is not None else default_device(group)
     summed = None
     if "loglik" in pars:
-        s_len = S if pairing == "grid" else N
+        s_len = S if pairing in ("grid", "block") else N
         acc = torch.zeros(s_len, dtype=torch.float64, device=dev)
         if e > b:
             ll = np.asarray(local["loglik"])
             if pairing == "grid":  # pair p = s + S*n -> (S, n_local)
                 acc += torch.from_numpy(ll.reshape((S, e - b), order="F").sum(axis=1)).to(dev)
-            else:
-                acc[b:e] += torch.from_numpy(ll).to(dev)
+            else:  # zip: pair = series = draw; block: pair = draw, this rank's draws [b*B, e*B)
+                acc[b * B:e * B] += torch.from_numpy(ll).to(dev)
         dist.all_reduce(acc, group=group)
         summed = acc.cpu().numpy()
 

@@ -36,6 +36,10 @@
  * Pairing: HHMM_PAIR_GRID evaluates every series under every draw,
  * P = N*S, pair p = s + S*n (draw fastest: a batch of draws of one series is
  * rstan's [S, ...] slab).  HHMM_PAIR_ZIP pairs series n with draw n (N == S).
+ * HHMM_PAIR_BLOCK gives every series its own block of B = S / N draws (one
+ * fit per series, as the reference's walk-forward runs one stan() per window,
+ * tayal2009/R/wf-trade.R:30-100): P = S pairs, pair p = b + B*n evaluates
+ * series n under draw p.
  *
  * Errors: every entry point returns hhmm_status; the message of the last
  * failure on the calling thread is hhmm_last_error().  No C++ exception or
@@ -90,7 +94,8 @@ typedef enum hhmm_model {
 
 typedef enum hhmm_pairing {
     HHMM_PAIR_GRID = 0,
-    HHMM_PAIR_ZIP = 1
+    HHMM_PAIR_ZIP = 1,
+    HHMM_PAIR_BLOCK = 2
 } hhmm_pairing;
 
 /* Output selection bitmask (hhmm_request.outputs).  Names are the Stan names. */

@@ -1103,10 +1103,28 @@ static int64_t num_pairs(const hhmm_request *r)
 {
     if (r->pairing == HHMM_PAIR_ZIP)
         return r->data.n_series == r->draws.n_draws ? r->data.n_series : -1;
+    if (r->pairing == HHMM_PAIR_BLOCK)
+        return r->draws.n_draws % r->data.n_series == 0 ? r->draws.n_draws : -1;
     return r->data.n_series * r->draws.n_draws;
 }
 
-static void gather(pair_ctx *c, const hhmm_request *r, int64_t n, int64_t s)
+/* pair p -> (series n, draw s), include/hhmm.h pairing modes */
+static void pair_of(const hhmm_request *r, int64_t p, int64_t *n, int64_t *s)
+{
+    const int64_t N = r->data.n_series, S = r->draws.n_draws;
+    if (r->pairing == HHMM_PAIR_ZIP) {
+        *n = p;
+        *s = p;
+    } else if (r->pairing == HHMM_PAIR_BLOCK) {
+        *n = p / (S / N);
+        *s = p;
+    } else {
+        *n = p / S;
+        *s = p % S;
+    }
+}
+
+static void gather(pair_ctx *c, const hhmm_request *r, int64_t p, int64_t n, int64_t s)
 {
     const hhmm_data *d = &r->data;
     const hhmm_draws *w = &r->draws;
@@ -1124,12 +1142,12 @@ static void gather(pair_ctx *c, const hhmm_request *r, int64_t n, int64_t s)
                 c->u[(size_t)t * M + m] = d->u[(size_t)n + (size_t)N * ((size_t)t + (size_t)Tm * m)];
     }
     if (r->ffbs_u) {
-        const size_t P = (size_t)num_pairs(r), pp = (size_t)(r->pairing == HHMM_PAIR_ZIP ? n : s + S * n);
+        const size_t P = (size_t)num_pairs(r), pp = (size_t)p;
         for (int t = 0; t < c->T; ++t)
             c->ffbs_u[t] = r->ffbs_u[pp + P * (size_t)t];
     }
     if (r->hat_rand) {
-        const size_t P = (size_t)num_pairs(r), pp = (size_t)(r->pairing == HHMM_PAIR_ZIP ? n : s + S * n);
+        const size_t P = (size_t)num_pairs(r), pp = (size_t)p;
         for (int t = 0; t < c->T; ++t)
             for (int q = 0; q < 3; ++q)
                 c->hat_rand[(size_t)t * 3 + q] = r->hat_rand[pp + P * ((size_t)t + (size_t)Tm * q)];
@@ -1269,9 +1287,8 @@ int hhmm_oracle_run_range(const hhmm_request *r, hhmm_result *o, int64_t p0, int
 #pragma omp for schedule(dynamic, 1)
 #endif
         for (int64_t p = p0; p < p1; ++p) {
-            const int64_t S = r->draws.n_draws;
-            const int64_t n = (r->pairing == HHMM_PAIR_ZIP) ? p : p / S;
-            const int64_t s = (r->pairing == HHMM_PAIR_ZIP) ? p : p % S;
+            int64_t n, s;
+            pair_of(r, p, &n, &s);
             c.K = K;
             c.L = L;
             c.M = M;
@@ -1281,7 +1298,7 @@ int hhmm_oracle_run_range(const hhmm_request *r, hhmm_result *o, int64_t p0, int
             c.status = 0;
             c.loglik = NAN;
             c.logp_zstar = NAN;
-            gather(&c, r, n, s);
+            gather(&c, r, p, n, s);
             run_pair(&c, r);
             if (c.status)
                 failures += 1;

@@ -32,7 +32,7 @@ def _worker(rank, world, port, model, pairing, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         n = 5
-        data, draws = synth.GENERATORS[model](N=n, S=(n if pairing == "zip" else 4), T=30)
+        data, draws = synth.GENERATORS[model](N=n, S={"zip": n, "grid": 4, "block": 3 * n}[pairing], T=30)
         pars = ["loglik", "gamma_tk", "zstar_t"] if model != "hhmm-tayal2009-lite" else ["loglik", "zstar_t"]
 
         def compute(m, d, w, pars, pairing):
@@ -45,7 +45,8 @@ def _worker(rank, world, port, model, pairing, q):
 
 
 @pytest.mark.parametrize("model,pairing", [("hmm-multinom", "grid"), ("hmm-multinom", "zip"),
-                                           ("hhmm-tayal2009-lite", "grid"), ("iohmm-hmix", "grid")])
+                                           ("hmm-multinom", "block"), ("hhmm-tayal2009-lite", "grid"),
+                                           ("iohmm-hmix", "grid")])
 def test_two_rank_sharding_matches_single_process(oracle, model, pairing):
     from hhmm_amd import synth
     world = 2
@@ -63,9 +64,9 @@ def test_two_rank_sharding_matches_single_process(oracle, model, pairing):
         p.join(timeout=60)
         assert p.exitcode == 0
     n = 5
-    data, draws = synth.GENERATORS[model](N=n, S=(n if pairing == "zip" else 4), T=30)
+    data, draws = synth.GENERATORS[model](N=n, S={"zip": n, "grid": 4, "block": 3 * n}[pairing], T=30)
     ref = oracle.gqs(model, data, draws, pars=["loglik", "zstar_t"], pairing=pairing)
-    S = 4 if pairing == "grid" else n
+    S = {"zip": n, "grid": 4, "block": 3 * n}[pairing]
     if pairing == "grid":
         want = ref["loglik"].reshape((S, n), order="F").sum(axis=1)
     else:

@@ -264,3 +264,19 @@ def test_viterbi_layouts_agree_long(engine, model):
     b = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=_abi.FLAG_VIT_STATES)
     assert np.array_equal(a["zstar_t"], b["zstar_t"])
     assert np.array_equal(a["logp_zstar"].view(np.int64), b["logp_zstar"].view(np.int64))
+
+
+@pytest.mark.parametrize("model", DEVICE_MODELS)
+def test_parity_block_pairing(engine, oracle, model):
+    """HHMM_PAIR_BLOCK: every series under its own block of draws (one fit per
+    series, the walk-forward layout), ragged T."""
+    N, B, T = 3, 20, 57
+    data, draws = synth.GENERATORS[model](N=N, S=N * B, T=T)
+    data["T"] = np.array([57, 1, 30], dtype=np.int32)
+    if "x_oos" in data:
+        data["T_oos"] = np.array([2, 48, 19], dtype=np.int32)
+    pars = synth.PARS[model]
+    import hhmm_amd
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, pairing="block", lib=engine, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, pairing="block", return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])

@@ -173,3 +173,15 @@ def test_kat_iohmm_backward_is_state_independent(oracle):
     out = oracle.gqs("iohmm-reg", data, draws, pars=["beta_tk", "unbeta_tk"])
     assert np.allclose(out["beta_tk"], 1 / 3, rtol=1e-14)
     assert np.all(out["unbeta_tk"] == out["unbeta_tk"][:, :, :1])
+
+
+@pytest.mark.parametrize("model", ["hmm", "hmm-multinom"])
+@pytest.mark.parametrize("K", [12, 23])
+def test_oracle_large_K_matches_transcription(oracle, model, K):
+    """The oracle at the large K of SURVEY §8 N1 (free `int<lower=1> K`,
+    hmm-multinom.stan:9; 23 flattened states, log.md:657)."""
+    data, draws = synth.GENERATORS[model](N=2, S=2, T=17, K=K)
+    pars = synth.PARS[model]
+    ref = oracle.gqs(model, data, draws, pars=pars, variant="libm", return_status=True)
+    rows = onp.run(model, data, draws)
+    _compare_exact(model, ref, rows, pars)
