@@ -40,6 +40,13 @@ def main():
     fres = _abi.Result.from_buffer_copy(res)
     fres.gamma_tk = None
     run.reqs["fwd"] = (fwd, fres, ws)
+    # Viterbi forward only: logp_zstar without the path (no backtrack)
+    r, res, ws = run.reqs["viterbi"]
+    vf = _abi.Request.from_buffer_copy(r)
+    vf.outputs = _abi.OUT["logp_zstar"]
+    vres = _abi.Result.from_buffer_copy(res)
+    vres.zstar_t = None
+    run.reqs["vit_fwd"] = (vf, vres, ws)
     s0 = torch.cuda.current_stream()
     s1 = torch.cuda.Stream()
 
@@ -64,7 +71,8 @@ def main():
         s0.wait_event(join)
 
     cases = {"fb": lambda: run.launch("fb"), "fwd_only": lambda: run.launch("fwd"),
-             "viterbi": lambda: run.launch("viterbi"), "concurrent": concurrent,
+             "viterbi": lambda: run.launch("viterbi"), "vit_fwd": lambda: run.launch("vit_fwd"),
+             "concurrent": concurrent, "library_step": lambda: run.launch("step"),
              "sequential": lambda: (run.launch("fb"), run.launch("viterbi"))}
     t = {k: [] for k in cases}
     for i in range(a.rounds + 1):
