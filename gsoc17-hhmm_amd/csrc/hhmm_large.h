@@ -15,8 +15,9 @@
  * j reads its own state's column for the step's symbol.
  *
  * Arithmetic is the lane-per-pair kernels' (hhmm_hmm.h) with the K-vector
- * spread over lanes: the same linear-space scaled filter (K FMAs in the same
- * i order, an exact power-of-two renormalisation per step), the same
+ * spread over lanes: the same linear-space scaled filter (K FMAs per state,
+ * as four interleaved chains; an exact power-of-two renormalisation per
+ * step), the same
  * checkpoint-and-recompute backward sweep, and for the Viterbi the same
  * candidate order (delta + log A) + emission with strict '>' and the Q3 NaN
  * row -- so paths and logp_zstar are bit-identical to the oracle.
@@ -204,9 +205,12 @@ __device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, doubl
 {
     double *s = xch + slot * kLG;
     s[j] = v;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    /* The group is inside one wave, and a wave's LDS instructions execute in
+     * order, so its reads see its own write: only the compiler must keep them
+     * in order (a fence here would also wait for every outstanding global
+     * load and store, i.e. an HBM round trip per step). */
+    __asm__ __volatile__("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int i = 0; i < kLG; i += 2) {
         if (i < K) {
@@ -229,28 +233,31 @@ __device__ __forceinline__ double grp_renorm(double v, int &ex)
     return ldexp(v, -e);
 }
 
-/* alpha_t(j) = e_t(j) * sum_i alpha_{t-1}(i) A(i, j): the fma chain of fwd_step_raw. */
+/* sum_i w_i c_i over the K entries as four interleaved fma chains (a
+ * quarter of the dependent-latency of one chain; the posteriors are
+ * tolerance outputs, 1e-9 relative, so the association is free) */
+__device__ __forceinline__ double lk_dot(const double (&w)[kLG], const double (&c)[kLG], int K)
+{
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < kLG; ++i)
+        if (i < K)
+            acc[i & 3] = fma(w[i], c[i], acc[i & 3]);
+    return (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
+/* alpha_t(j) = e_t(j) * sum_i alpha_{t-1}(i) A(i, j) (fwd_step_raw) */
 template <int MODEL>
 __device__ __forceinline__ double lk_fwd(const LkLane<MODEL> &ln, const double (&w)[kLG], double e)
 {
-    double acc = w[0] * ln.col[0];
-#pragma unroll
-    for (int i = 1; i < kLG; ++i)
-        if (i < ln.K)
-            acc = fma(w[i], ln.col[i], acc);
-    return ln.on ? acc * e : 0.0;
+    return ln.on ? lk_dot(w, ln.col, ln.K) * e : 0.0;
 }
 
-/* beta_{t-1}(j) = sum_i A(j, i) b_i, b_i = e_t(i) beta_t(i) (bwd_step). */
+/* beta_{t-1}(j) = sum_i A(j, i) b_i, b_i = e_t(i) beta_t(i) (bwd_step) */
 template <int MODEL>
 __device__ __forceinline__ double lk_bwd(const LkLane<MODEL> &ln, const double (&w)[kLG])
 {
-    double acc = ln.row[0] * w[0];
-#pragma unroll
-    for (int i = 1; i < kLG; ++i)
-        if (i < ln.K)
-            acc = fma(ln.row[i], w[i], acc);
-    return ln.on ? acc : 0.0;
+    return ln.on ? lk_dot(w, ln.row, ln.K) : 0.0;
 }
 
 template <int MODEL>
