@@ -4,13 +4,16 @@
  * (hmm-multinom.stan:9), e.g. the 23-state flattened HHMMs the reference
  * discusses (log.md:657, tayal2009/main.Rmd:310-346).
  *
- * Layout: a GROUP of G = 32 lanes owns one (series, draw) pair, lane j state
- * j (lanes j >= K idle), two pairs per wave.  The K x K transition matrix is
+ * Layout: a GROUP of G lanes owns one (series, draw) pair, lane j state j
+ * (lanes j >= K idle): G = 16 for K <= 16 (four pairs per wave), G = 32 above
+ * (two).  Idle lanes hold the neutral entry (0 in the filters, -inf in the
+ * max-plus recursion), so every loop over states runs a compile-time G.  The K x K transition matrix is
  * split by column and row over the group: lane j keeps column j (forward,
  * Viterbi) and row j (backward) in registers.  Each step the group exchanges
  * its state vector through a per-pair LDS slot -- every lane writes its
  * entry, then reads all K back as broadcast ds_read_b128 -- and reduces
- * across the group with 32-lane shuffles (renormalisation max, gamma sum).
+ * across the group with DPP / ds_swizzle butterflies (renormalisation max,
+ * gamma sums).
  * The emission table (multinomial: phi[l][j] per pair) sits in LDS so lane
  * j reads its own state's column for the step's symbol.
  *
@@ -38,7 +41,6 @@
 
 namespace hhmm {
 
-constexpr int kLG = 32;     /* lanes per pair */
 constexpr int kLChunk = 8;  /* steps per forward checkpoint */
 constexpr int kLBack = 16;  /* backtrack steps per back-pointer chunk */
 
@@ -50,45 +52,79 @@ struct LkTraits {
     static constexpr bool kGauss = (MODEL == HHMM_MODEL_HMM_GAUSS);
 };
 
-/* group reductions over the 32 lanes of a pair (the pair's lanes are one
- * aligned 32-lane half of the wave) */
+/* Group reductions over the 32 lanes of a pair (one aligned half of the
+ * wave): a butterfly of DPP moves inside each 16-lane row (quad xor 1, quad
+ * xor 2, half-row mirror, row mirror) and one ds_swizzle xor 16 across the
+ * two rows -- a few cycles per level instead of the LDS crossbar round trip
+ * of a ds_bpermute shuffle.  Every level combines two mirror-image partial
+ * results, and IEEE addition is commutative, so all lanes end with the same
+ * bits. */
+template <int CTRL>
+__device__ __forceinline__ double lk_dpp(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double lk_xor16(double v)
+{
+    constexpr int kXor16 = 0x1F | (0x10 << 10); /* ds_swizzle bit mode: and 0x1F, or 0, xor 0x10 */
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)b, kXor16);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), kXor16);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+constexpr int kDppXor1 = 0xB1;       /* quad_perm [1,0,3,2] */
+constexpr int kDppXor2 = 0x4E;       /* quad_perm [2,3,0,1] */
+constexpr int kDppHalfMirror = 0x141;
+constexpr int kDppMirror = 0x140;
+
+template <int G>
 __device__ __forceinline__ double grp_max(double v)
 {
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1)
-        v = fmax(v, __shfl_xor(v, off, kLG));
+    v = fmax(v, lk_dpp<kDppXor1>(v));
+    v = fmax(v, lk_dpp<kDppXor2>(v));
+    v = fmax(v, lk_dpp<kDppHalfMirror>(v));
+    v = fmax(v, lk_dpp<kDppMirror>(v));
+    if constexpr (G == 32)
+        v = fmax(v, lk_xor16(v));
     return v;
 }
+template <int G>
 __device__ __forceinline__ double grp_sum(double v)
 {
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1)
-        v += __shfl_xor(v, off, kLG);
+    v = v + lk_dpp<kDppXor1>(v);
+    v = v + lk_dpp<kDppXor2>(v);
+    v = v + lk_dpp<kDppHalfMirror>(v);
+    v = v + lk_dpp<kDppMirror>(v);
+    if constexpr (G == 32)
+        v = v + lk_xor16(v);
     return v;
 }
 
 /* Per-lane state of one pair's group. */
-template <int MODEL>
+template <int MODEL, int G>
 struct LkLane {
     int j;          /* this lane's state (>= K: idle) */
     bool on;        /* j < K */
     int64_t p, n, d;
     int Tp, K, L;
-    double col[kLG]; /* A[i][j] (probabilities; Viterbi: log) */
-    double row[kLG]; /* A[j][i] (backward) */
+    double col[G]; /* A[i][j] (probabilities; Viterbi: log) */
+    double row[G]; /* A[j][i] (backward) */
     double pj;       /* p_1k[j] */
     double mu, isig, c0, lsig; /* gauss, state j */
-    double *xch;     /* this pair's LDS exchange slots: 2 x kLG doubles */
-    const double *tab; /* multinomial: this pair's [L][kLG] emission table */
+    double *xch;     /* this pair's LDS exchange slots: 2 x G doubles */
+    const double *tab; /* multinomial: this pair's [L][G] emission table */
 };
 
-template <int MODEL>
-__device__ __forceinline__ void lk_setup(LkLane<MODEL> &ln, const DevArgs &a, double *lds, bool LOG)
+template <int MODEL, int G>
+__device__ __forceinline__ void lk_setup(LkLane<MODEL, G> &ln, const DevArgs &a, double *lds, bool LOG)
 {
     const int tid = threadIdx.x;
-    const int g = tid / kLG;                 /* group in the workgroup */
-    const int gpb = blockDim.x / kLG;        /* groups per workgroup */
-    ln.j = tid % kLG;
+    const int g = tid / G;                 /* group in the workgroup */
+    const int gpb = blockDim.x / G;        /* groups per workgroup */
+    ln.j = tid % G;
     ln.K = a.K;
     ln.L = a.L;
     ln.on = ln.j < a.K;
@@ -97,9 +133,9 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL> &ln, const DevArgs &a, do
     ln.Tp = pair_len(a, ln.n);
     const int jj = ln.on ? ln.j : 0;
     const int64_t S = a.S, d = ln.d;
-    double rawc[kLG], rawr[kLG];
+    double rawc[G], rawr[G];
 #pragma unroll
-    for (int i = 0; i < kLG; ++i) {
+    for (int i = 0; i < G; ++i) {
         rawc[i] = 0.0;
         rawr[i] = 0.0;
         if (i < a.K) {
@@ -108,7 +144,7 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL> &ln, const DevArgs &a, do
         }
     }
 #pragma unroll
-    for (int i = 0; i < kLG; ++i) {
+    for (int i = 0; i < G; ++i) {
         ln.col[i] = (LOG && i < a.K) ? hhmm_cr_log(rawc[i]) : rawc[i];
         ln.row[i] = rawr[i];
     }
@@ -120,9 +156,9 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL> &ln, const DevArgs &a, do
         ln.lsig = hhmm_cr_log(sg);
         ln.c0 = HHMM_NEG_LOG_SQRT_TWO_PI - ln.lsig;
     }
-    /* LDS: [groups][2][kLG] exchange, then [groups][L][kLG] tables */
-    ln.xch = lds + (size_t)g * 2 * kLG;
-    double *tab = lds + (size_t)gpb * 2 * kLG + (size_t)g * a.L * kLG;
+    /* LDS: [groups][2][G] exchange, then [groups][L][G] tables */
+    ln.xch = lds + (size_t)g * 2 * G;
+    double *tab = lds + (size_t)gpb * 2 * G + (size_t)g * a.L * G;
     ln.tab = tab;
     if constexpr (!LkTraits<MODEL>::kGauss) {
         for (int l0 = 0; l0 < a.L; l0 += 8) {
@@ -133,27 +169,27 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL> &ln, const DevArgs &a, do
 #pragma unroll
             for (int r = 0; r < 8; ++r)
                 if (l0 + r < a.L)
-                    tab[(l0 + r) * kLG + ln.j] = (LOG && ln.on) ? hhmm_cr_log(v[r]) : v[r];
+                    tab[(l0 + r) * G + ln.j] = (LOG && ln.on) ? hhmm_cr_log(v[r]) : v[r];
         }
     }
     __syncthreads();
 }
 
-/* Observations come a block of kLG steps at a time: lane j of the group
+/* Observations come a block of G steps at a time: lane j of the group
  * loads step 32b + j (clamped, unconditional), one load instruction per 32
  * steps, issued a block ahead; step t's symbol is then one shuffle from lane
  * t % 32 of the group. */
-template <int MODEL>
+template <int MODEL, int G>
 struct LkObs {
     int x;
     double xr;
 };
 
-template <int MODEL>
-__device__ __forceinline__ LkObs<MODEL> lk_block(const LkLane<MODEL> &ln, const DevArgs &a, int b)
+template <int MODEL, int G>
+__device__ __forceinline__ LkObs<MODEL, G> lk_block(const LkLane<MODEL, G> &ln, const DevArgs &a, int b)
 {
-    const int tc = min(max(b * kLG + ln.j, 0), a.Tmax - 1);
-    LkObs<MODEL> o;
+    const int tc = min(max(b * G + ln.j, 0), a.Tmax - 1);
+    LkObs<MODEL, G> o;
     o.x = 1;
     o.xr = 0.0;
     if constexpr (LkTraits<MODEL>::kGauss)
@@ -163,20 +199,53 @@ __device__ __forceinline__ LkObs<MODEL> lk_block(const LkLane<MODEL> &ln, const 
     return o;
 }
 
-template <int MODEL>
-__device__ __forceinline__ void lk_get(const LkObs<MODEL> &blk, int u, int &x, double &xr)
+/* step u of the block: lane u of the group; u is wave-uniform, so two scalar
+ * reads (one per group of the wave) and a select replace a shuffle */
+template <int G>
+__device__ __forceinline__ int lk_pick(int v, int u)
+{
+    const int a = __builtin_amdgcn_readlane(v, u), b = __builtin_amdgcn_readlane(v, u + G);
+    if constexpr (G == 32) {
+        return (threadIdx.x & 32) ? b : a;
+    } else {
+        const int c = __builtin_amdgcn_readlane(v, u + 32), d = __builtin_amdgcn_readlane(v, u + 48);
+        const int q = (threadIdx.x >> 4) & 3;
+        return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
+    }
+}
+
+/* step u of the block when u may differ between the wave's two groups (the
+ * backward sweep's chunks of pairs with different T): a shuffle */
+template <int MODEL, int G>
+__device__ __forceinline__ void lk_get_var(const LkObs<MODEL, G> &blk, int u, int &x, double &xr)
 {
     x = 1;
     xr = 0.0;
     if constexpr (LkTraits<MODEL>::kGauss)
-        xr = __shfl(blk.xr, u, kLG);
+        xr = __shfl(blk.xr, u, G);
     else
-        x = __shfl(blk.x, u, kLG);
+        x = __shfl(blk.x, u, G);
+}
+
+/* step u of the block, u the same for the whole wave (the forward sweeps run
+ * both groups in lockstep over t) */
+template <int MODEL, int G>
+__device__ __forceinline__ void lk_get(const LkObs<MODEL, G> &blk, int u, int &x, double &xr)
+{
+    x = 1;
+    xr = 0.0;
+    if constexpr (LkTraits<MODEL>::kGauss) {
+        const long long b = __double_as_longlong(blk.xr);
+        const int lo = lk_pick<G>((int)b, u), hi = lk_pick<G>((int)(b >> 32), u);
+        xr = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    } else {
+        x = lk_pick<G>(blk.x, u);
+    }
 }
 
 /* Stan's normal_lpdf(y | mu_j, sigma_j), as gauss_lpdf. */
-template <int MODEL>
-__device__ __forceinline__ double lk_lpdf(const LkLane<MODEL> &ln, double y)
+template <int MODEL, int G>
+__device__ __forceinline__ double lk_lpdf(const LkLane<MODEL, G> &ln, double y)
 {
     const double z = (y - ln.mu) * ln.isig;
     const double z2 = z * z;
@@ -185,25 +254,26 @@ __device__ __forceinline__ double lk_lpdf(const LkLane<MODEL> &ln, double y)
 
 /* Linear-space emission e_t(j) and its log scale m (gauss: densities over
  * their group max, as emit_prob); idle lanes 0. */
-template <int MODEL>
-__device__ __forceinline__ double lk_emit(const LkLane<MODEL> &ln, int x, double xr, double &m)
+template <int MODEL, int G>
+__device__ __forceinline__ double lk_emit(const LkLane<MODEL, G> &ln, int x, double xr, double &m)
 {
     if constexpr (LkTraits<MODEL>::kGauss) {
-        const double lp = ln.on ? lk_lpdf(ln, xr) : dev_ninf();
-        m = grp_max(lp);
+        const double lp = ln.on ? lk_lpdf<MODEL, G>(ln, xr) : dev_ninf();
+        m = grp_max<G>(lp);
         return ln.on ? exp(lp - m) : 0.0;
     } else {
         m = 0.0;
         const int xc = min(max(x, 1), ln.L);
-        return ln.on ? ln.tab[(xc - 1) * kLG + ln.j] : 0.0;
+        return ln.on ? ln.tab[(xc - 1) * G + ln.j] : 0.0;
     }
 }
 
-/* The group's K-vector v (this lane's entry) through LDS slot `slot`: w[i] =
- * v of state i for i < K (0 beyond). */
-__device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, double v, double (&w)[kLG], int K)
+/* The group's vector v (this lane's entry) through LDS slot `slot`: w[i] = v
+ * of lane i for all G lanes (idle lanes carry the neutral entry). */
+template <int G>
+__device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, double v, double (&w)[G])
 {
-    double *s = xch + slot * kLG;
+    double *s = xch + slot * G;
     s[j] = v;
     /* The group is inside one wave, and a wave's LDS instructions execute in
      * order, so its reads see its own write: only the compiler must keep them
@@ -212,125 +282,121 @@ __device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, doubl
     __asm__ __volatile__("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < kLG; i += 2) {
-        if (i < K) {
-            const double2 q = *reinterpret_cast<const double2 *>(s + i);
-            w[i] = q.x;
-            w[i + 1] = (i + 1 < K) ? q.y : 0.0;
-        } else {
-            w[i] = 0.0;
-            w[i + 1] = 0.0;
-        }
+    for (int i = 0; i < G; i += 2) {
+        const double2 q = *reinterpret_cast<const double2 *>(s + i);
+        w[i] = q.x;
+        w[i + 1] = q.y;
     }
 }
 
 /* Power-of-two renormalisation over the group (renorm<K>). */
+template <int G>
 __device__ __forceinline__ double grp_renorm(double v, int &ex)
 {
-    const double mx = grp_max(v);
+    const double mx = grp_max<G>(v);
     const int e = __builtin_amdgcn_frexp_exp(mx);
     ex += e;
     return ldexp(v, -e);
 }
 
-/* sum_i w_i c_i over the K entries as four interleaved fma chains (a
- * quarter of the dependent-latency of one chain; the posteriors are
+/* sum_i w_i c_i over the G entries (idle ones 0 x 0) as four interleaved fma
+ * chains (a quarter of the dependent latency of one chain; the posteriors are
  * tolerance outputs, 1e-9 relative, so the association is free) */
-__device__ __forceinline__ double lk_dot(const double (&w)[kLG], const double (&c)[kLG], int K)
+template <int G>
+__device__ __forceinline__ double lk_dot(const double (&w)[G], const double (&c)[G])
 {
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int i = 0; i < kLG; ++i)
-        if (i < K)
-            acc[i & 3] = fma(w[i], c[i], acc[i & 3]);
+    for (int i = 0; i < G; ++i)
+        acc[i & 3] = fma(w[i], c[i], acc[i & 3]);
     return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 /* alpha_t(j) = e_t(j) * sum_i alpha_{t-1}(i) A(i, j) (fwd_step_raw) */
-template <int MODEL>
-__device__ __forceinline__ double lk_fwd(const LkLane<MODEL> &ln, const double (&w)[kLG], double e)
+template <int MODEL, int G>
+__device__ __forceinline__ double lk_fwd(const LkLane<MODEL, G> &ln, const double (&w)[G], double e)
 {
-    return ln.on ? lk_dot(w, ln.col, ln.K) * e : 0.0;
+    return ln.on ? lk_dot<G>(w, ln.col) * e : 0.0;
 }
 
 /* beta_{t-1}(j) = sum_i A(j, i) b_i, b_i = e_t(i) beta_t(i) (bwd_step) */
-template <int MODEL>
-__device__ __forceinline__ double lk_bwd(const LkLane<MODEL> &ln, const double (&w)[kLG])
+template <int MODEL, int G>
+__device__ __forceinline__ double lk_bwd(const LkLane<MODEL, G> &ln, const double (&w)[G])
 {
-    return ln.on ? lk_dot(w, ln.row, ln.K) : 0.0;
+    return ln.on ? lk_dot<G>(w, ln.row) : 0.0;
 }
 
-template <int MODEL>
-__device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLane<MODEL> &ln, int t, double v)
+template <int MODEL, int G>
+__device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLane<MODEL, G> &ln, int t, double v)
 {
     if (ln.on && out)
         out[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
 }
 
 /* Forward-backward: loglik, alpha, beta, ungamma, gamma. */
-template <int MODEL>
+template <int MODEL, int G>
 __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
-    LkLane<MODEL> ln;
-    lk_setup<MODEL>(ln, a, lds, false);
+    LkLane<MODEL, G> ln;
+    lk_setup<MODEL, G>(ln, a, lds, false);
     const uint32_t out = a.outputs;
     const bool need_bwd = (out & (HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
     const int Tp = ln.Tp; /* per pair: uniform over the group (the wave's two groups may differ) */
     const int K = ln.K;
-    double w[kLG];
+    double w[G];
     int slot = 0;
     auto ckpt = [&](int c) -> double & { return a.ckpt[ln.p + a.P * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
 
     /* ---- forward: alpha_1 (hmm.stan:30 Q2 / hmm-multinom.stan:31), then the recursion ---- */
-    LkObs<MODEL> bcur = lk_block<MODEL>(ln, a, 0), bnxt = lk_block<MODEL>(ln, a, 1);
+    LkObs<MODEL, G> bcur = lk_block<MODEL, G>(ln, a, 0), bnxt = lk_block<MODEL, G>(ln, a, 1);
     double al, lsc = 0.0;
     int ex = 0;
     {
         int x;
         double xr, m;
-        lk_get<MODEL>(bcur, 0, x, xr);
+        lk_get<MODEL, G>(bcur, 0, x, xr);
         if constexpr (LkTraits<MODEL>::kGauss) {
             /* log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k): alpha_1 = p_1k */
             const double z = (xr - ln.mu) * ln.isig;
             const double tk = ln.on ? (HHMM_NEG_LOG_SQRT_TWO_PI - ln.lsig) + (-0.5 * (z * z)) : 0.0;
-            lsc += grp_sum(tk);
+            lsc += grp_sum<G>(tk);
             al = ln.on ? ln.pj : 0.0;
         } else {
-            const double e = lk_emit<MODEL>(ln, x, xr, m);
+            const double e = lk_emit<MODEL, G>(ln, x, xr, m);
             al = ln.on ? ln.pj * e : 0.0;
         }
-        al = grp_renorm(al, ex);
+        al = grp_renorm<G>(al, ex);
     }
     if (need_bwd) {
         if (ln.on)
             ckpt(0) = al;
     } else if ((out & HHMM_OUT_ALPHA) && a.alpha) {
-        lk_put<MODEL>(a.alpha, a, ln, 0, al / grp_sum(al));
+        lk_put<MODEL, G>(a.alpha, a, ln, 0, al / grp_sum<G>(al));
     }
     for (int t = 1; t < Tp; ++t) {
-        const int u = t % kLG;
+        const int u = t % G;
         if (u == 0) { /* group-uniform: next block of observations, prefetch the one after */
             bcur = bnxt;
-            bnxt = lk_block<MODEL>(ln, a, t / kLG + 1);
+            bnxt = lk_block<MODEL, G>(ln, a, t / G + 1);
         }
         int x;
         double xr, m;
-        lk_get<MODEL>(bcur, u, x, xr);
-        const double e = lk_emit<MODEL>(ln, x, xr, m);
-        grp_exchange(ln.xch, slot, ln.j, al, w, K);
+        lk_get<MODEL, G>(bcur, u, x, xr);
+        const double e = lk_emit<MODEL, G>(ln, x, xr, m);
+        grp_exchange<G>(ln.xch, slot, ln.j, al, w);
         slot ^= 1;
         lsc += m;
-        al = grp_renorm(lk_fwd<MODEL>(ln, w, e), ex);
+        al = grp_renorm<G>(lk_fwd<MODEL, G>(ln, w, e), ex);
         if (!need_bwd) {
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
-                lk_put<MODEL>(a.alpha, a, ln, t, al / grp_sum(al));
+                lk_put<MODEL, G>(a.alpha, a, ln, t, al / grp_sum<G>(al));
         } else if (t % kLChunk == 0 && ln.on) {
             ckpt(t / kLChunk) = al;
         }
     }
     {
-        const double sa = grp_sum(al); /* every lane takes part in the shuffle */
+        const double sa = grp_sum<G>(al); /* every lane takes part in the shuffle */
         if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0)
             a.loglik[ln.p] = log(sa) + (lsc + kLn2 * ex);
     }
@@ -342,26 +408,26 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
      * backwards emitting the posteriors and stepping beta (bwd_chunk) ---- */
     double be = ln.on ? 1.0 : 0.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
     int bex = 0;
-    constexpr int CPB = kLG / kLChunk; /* chunks per observation block */
+    constexpr int CPB = G / kLChunk; /* chunks per observation block */
     const int nck = (Tp + kLChunk - 1) / kLChunk;
     int cb = (nck - 1) / CPB;
-    LkObs<MODEL> ob = lk_block<MODEL>(ln, a, cb), obp = lk_block<MODEL>(ln, a, cb - 1);
+    LkObs<MODEL, G> ob = lk_block<MODEL, G>(ln, a, cb), obp = lk_block<MODEL, G>(ln, a, cb - 1);
     double ck = ckpt(nck - 1), ckn = ckpt(max(nck - 2, 0));
     for (int c = nck - 1; c >= 0; --c) {
         if (c / CPB != cb) { /* group-uniform: step back one observation block */
             cb = c / CPB;
             ob = obp;
-            obp = lk_block<MODEL>(ln, a, cb - 1);
+            obp = lk_block<MODEL, G>(ln, a, cb - 1);
         }
         const int t0 = c * kLChunk;
-        const int ub = t0 % kLG; /* the chunk's first step inside the block */
+        const int ub = t0 % G; /* the chunk's first step inside the block */
         double es[kLChunk];
 #pragma unroll
         for (int u = 0; u < kLChunk; ++u) {
             int x;
             double xr, m;
-            lk_get<MODEL>(ob, ub + u, x, xr);
-            es[u] = lk_emit<MODEL>(ln, x, xr, m);
+            lk_get_var<MODEL, G>(ob, ub + u, x, xr);
+            es[u] = lk_emit<MODEL, G>(ln, x, xr, m);
         }
         double abuf[kLChunk];
         abuf[0] = ln.on ? ck : 0.0;
@@ -372,9 +438,9 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         for (int u = 1; u < kLChunk; ++u) {
             abuf[u] = 0.0;
             if (t0 + u < Tp) { /* group-uniform */
-                grp_exchange(ln.xch, slot, ln.j, abuf[u - 1], w, K);
+                grp_exchange<G>(ln.xch, slot, ln.j, abuf[u - 1], w);
                 slot ^= 1;
-                abuf[u] = grp_renorm(lk_fwd<MODEL>(ln, w, es[u]), exb);
+                abuf[u] = grp_renorm<G>(lk_fwd<MODEL, G>(ln, w, es[u]), exb);
             }
         }
 #pragma unroll
@@ -383,25 +449,25 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             if (t >= Tp)
                 continue;
             const double av = abuf[u];
-            const double sa = grp_sum(av), sb = grp_sum(be);
+            const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
-                lk_put<MODEL>(a.alpha, a, ln, t, av / sa);
+                lk_put<MODEL, G>(a.alpha, a, ln, t, av / sa);
             if ((out & HHMM_OUT_BETA) && a.beta)
-                lk_put<MODEL>(a.beta, a, ln, t, be / sb);
+                lk_put<MODEL, G>(a.beta, a, ln, t, be / sb);
             if (out & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
                 /* gamma = normalize(alpha .* beta) from the normalised vectors (hmm.stan:89-96) */
                 const double ug = (av / sa) * (be / sb);
                 if ((out & HHMM_OUT_UNGAMMA) && a.ungamma)
-                    lk_put<MODEL>(a.ungamma, a, ln, t, ug);
+                    lk_put<MODEL, G>(a.ungamma, a, ln, t, ug);
                 if ((out & HHMM_OUT_GAMMA) && a.gamma) {
-                    const double sg = grp_sum(ug);
-                    lk_put<MODEL>(a.gamma, a, ln, t, ug / sg);
+                    const double sg = grp_sum<G>(ug);
+                    lk_put<MODEL, G>(a.gamma, a, ln, t, ug / sg);
                 }
             }
             if (t > 0) {
-                grp_exchange(ln.xch, slot, ln.j, es[u] * be, w, K);
+                grp_exchange<G>(ln.xch, slot, ln.j, es[u] * be, w);
                 slot ^= 1;
-                be = grp_renorm(lk_bwd<MODEL>(ln, w), bex);
+                be = grp_renorm<G>(lk_bwd<MODEL, G>(ln, w), bex);
             }
         }
     }
@@ -410,7 +476,8 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
 /* ---- Viterbi (hmm.stan:98-130; hmm-multinom.stan:100-132) ---- */
 
 /* SSE2 maxCoeff order of stan_max_vec for a runtime K (oracle stan_max_vec). */
-__device__ __forceinline__ double stan_max_rt(const double (&d)[kLG], int n)
+template <int G>
+__device__ __forceinline__ double stan_max_rt(const double (&d)[G], int n)
 {
     if (n < 2)
         return d[0];
@@ -419,7 +486,7 @@ __device__ __forceinline__ double stan_max_rt(const double (&d)[kLG], int n)
     if (aligned > 2) {
         double r1a = d[2], r1b = d[3];
 #pragma unroll
-        for (int i = 4; i + 4 <= kLG; i += 4) {
+        for (int i = 4; i + 4 <= G; i += 4) {
             if (i < aligned2) {
                 r0a = sse_max(r0a, d[i]);
                 r0b = sse_max(r0b, d[i + 1]);
@@ -431,7 +498,7 @@ __device__ __forceinline__ double stan_max_rt(const double (&d)[kLG], int n)
         r0b = sse_max(r0b, r1b);
         if (aligned > aligned2) {
 #pragma unroll
-            for (int q = 4; q + 2 <= kLG; q += 4)
+            for (int q = 4; q + 2 <= G; q += 4)
                 if (q == aligned2) {
                     r0a = sse_max(r0a, d[q]);
                     r0b = sse_max(r0b, d[q + 1]);
@@ -440,27 +507,27 @@ __device__ __forceinline__ double stan_max_rt(const double (&d)[kLG], int n)
     }
     double res = sse_max(r0a, r0b);
 #pragma unroll
-    for (int i = 2; i < kLG; ++i)
+    for (int i = 2; i < G; ++i)
         if (i >= aligned && i < n)
             res = std_max(res, d[i]);
     return res;
 }
 
-template <int MODEL>
+template <int MODEL, int G>
 __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
-    LkLane<MODEL> ln;
-    lk_setup<MODEL>(ln, a, lds, true);
+    LkLane<MODEL, G> ln;
+    lk_setup<MODEL, G>(ln, a, lds, true);
     const int Tp = ln.Tp;
     const int K = ln.K;
-    double w[kLG];
+    double w[G];
     int slot = 0;
     auto emit_log = [&](int x, double xr) -> double {
         if constexpr (LkTraits<MODEL>::kGauss)
-            return ln.on ? lk_lpdf(ln, xr) : 0.0;
+            return ln.on ? lk_lpdf<MODEL, G>(ln, xr) : 0.0;
         else
-            return ln.on ? ln.tab[(min(max(x, 1), ln.L) - 1) * kLG + ln.j] : 0.0;
+            return ln.on ? ln.tab[(min(max(x, 1), ln.L) - 1) * G + ln.j] : 0.0;
     };
     /* back-pointers [P][K][Tb] bytes, Tb = T_max rounded up to 16: a state's
      * bytes are contiguous in t and its row 16-byte aligned */
@@ -468,45 +535,43 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
     uint8_t *bp = reinterpret_cast<uint8_t *>(a.bp) + ((int64_t)ln.p * K + (ln.on ? ln.j : 0)) * Tb;
 
     /* delta_tk[1, K] = emission of state K only (Q3: the others keep NaN) */
-    LkObs<MODEL> bcur = lk_block<MODEL>(ln, a, 0), bnxt = lk_block<MODEL>(ln, a, 1);
+    LkObs<MODEL, G> bcur = lk_block<MODEL, G>(ln, a, 0), bnxt = lk_block<MODEL, G>(ln, a, 1);
     int x;
     double xr;
-    lk_get<MODEL>(bcur, 0, x, xr);
+    lk_get<MODEL, G>(bcur, 0, x, xr);
     const double le0 = emit_log(x, xr);
-    double dl = (ln.j == K - 1) ? le0 : dev_nan();
+    double dl = !ln.on ? dev_ninf() : ((ln.j == K - 1) ? le0 : dev_nan());
     for (int t = 1; t < Tp; ++t) {
-        const int u = t % kLG;
+        const int u = t % G;
         if (u == 0) {
             bcur = bnxt;
-            bnxt = lk_block<MODEL>(ln, a, t / kLG + 1);
+            bnxt = lk_block<MODEL, G>(ln, a, t / G + 1);
         }
-        lk_get<MODEL>(bcur, u, x, xr);
+        lk_get<MODEL, G>(bcur, u, x, xr);
         const double le = emit_log(x, xr);
-        grp_exchange(ln.xch, slot, ln.j, dl, w, K);
+        grp_exchange<G>(ln.xch, slot, ln.j, dl, w);
         slot ^= 1;
         /* candidate (delta + log A) + emission, strict '>' from -inf; the
          * running max as fmax (vit_step): NaN never wins, first i on ties */
         double best = dev_ninf();
         int arg = 0;
 #pragma unroll
-        for (int i = 0; i < kLG; ++i) {
-            if (i < K) {
-                const double cand = (w[i] + ln.col[i]) + le;
-                const bool gt = cand > best;
-                best = fmax(best, cand);
-                arg = gt ? i : arg;
-            }
+        for (int i = 0; i < G; ++i) { /* idle i: delta -inf, never greater */
+            const double cand = (w[i] + ln.col[i]) + le;
+            const bool gt = cand > best;
+            best = fmax(best, cand);
+            arg = gt ? i : arg;
         }
         dl = ln.on ? best : dev_ninf();
         if (ln.on)
             bp[t] = (uint8_t)arg;
     }
     /* logp_zstar = max(delta_T) (SSE2 order); zstar_T = LAST j attaining it */
-    grp_exchange(ln.xch, slot, ln.j, dl, w, K);
-    const double lp = stan_max_rt(w, K);
+    grp_exchange<G>(ln.xch, slot, ln.j, dl, w);
+    const double lp = stan_max_rt<G>(w, K);
     int z = -1;
 #pragma unroll
-    for (int j = 0; j < kLG; ++j)
+    for (int j = 0; j < G; ++j)
         if (j < K && w[j] == lp)
             z = j;
     const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
@@ -519,7 +584,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
     if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
         return;
     if (invalid) {
-        for (int t = ln.j; t < Tp; t += kLG)
+        for (int t = ln.j; t < Tp; t += G)
             a.zstar[ln.p + a.P * (int64_t)t] = 0;
         return;
     }
@@ -544,7 +609,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
                 if ((ln.j & (kLBack - 1)) == u)
                     mine = z + 1;
                 if (t > 0)
-                    z = __shfl((int)((wd[u >> 2] >> (8 * (u & 3))) & 0xffu), z, kLG);
+                    z = __shfl((int)((wd[u >> 2] >> (8 * (u & 3))) & 0xffu), z, G);
             }
         }
         const int t = c * kLBack + (ln.j & (kLBack - 1));
@@ -556,13 +621,14 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
 }
 
 /* LDS bytes of a launch with `threads` lanes: exchange slots + tables. */
+template <int G>
 static inline size_t lk_lds(const DevArgs &a, int threads, bool discrete)
 {
-    const size_t groups = (size_t)threads / kLG;
-    return groups * 2 * kLG * sizeof(double) + (discrete ? groups * (size_t)a.L * kLG * sizeof(double) : 0);
+    const size_t groups = (size_t)threads / G;
+    return groups * 2 * G * sizeof(double) + (discrete ? groups * (size_t)a.L * G * sizeof(double) : 0);
 }
 
-template <int MODEL>
+template <int MODEL, int G>
 static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
 {
     constexpr bool discrete = !LkTraits<MODEL>::kGauss;
@@ -575,19 +641,19 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_UNSUPPORTED;
     }
     int threads = kBlock;
-    while (threads > kLG && lk_lds(a, threads, discrete) > kLdsLimit)
+    while (threads > G && lk_lds<G>(a, threads, discrete) > kLdsLimit)
         threads /= 2;
-    if (lk_lds(a, threads, discrete) > kLdsLimit) {
+    if (lk_lds<G>(a, threads, discrete) > kLdsLimit) {
         set_error("emission table of L = %d symbols does not fit in LDS", a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
-    const int gpb = threads / kLG;
+    const int gpb = threads / G;
     const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
     /* checkpoints use the [rows][K][P] layout of the lane kernels */
     if (out & fb)
-        hipLaunchKernelGGL((lk_fb_kernel<MODEL>), grid, dim3(threads), lk_lds(a, threads, discrete), st, a);
+        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
     if (out & vit)
-        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL>), grid, dim3(threads), lk_lds(a, threads, discrete), st, a);
+        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("large-K kernel launch: %s", hipGetErrorString(e));

@@ -1,0 +1,12 @@
+#!/bin/bash
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/pmc_n1
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+i=0
+for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+            "SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM"; do
+  i=$((i+1))
+  timeout -s KILL 200 rocprofv3 --pmc $CTRS --kernel-include-regex "lk_" --output-format csv -d $OUT/p$i -o p$i -- python $R/bench.py --workload n1 --no-cpu-baseline --steps 1 --warmup 0 --pars loglik > $OUT/p$i.log 2>&1
+  echo "pass $i rc=$?" >> $OUT/passes.txt
+done
