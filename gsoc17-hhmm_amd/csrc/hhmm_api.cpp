@@ -676,6 +676,22 @@ hhmm_status hhmm_selftest_cr_exp(const double *in, double *out, int64_t n)
     return selftest_cr_math(in, out, n, 1);
 }
 
+hhmm_status hhmm_selftest_det_log(const double *in, double *out, int64_t n)
+{
+    hhmm_status s = check_device();
+    if (s != HHMM_OK)
+        return s;
+    return selftest_cr_math(in, out, n, 2);
+}
+
+hhmm_status hhmm_selftest_det_exp(const double *in, double *out, int64_t n)
+{
+    hhmm_status s = check_device();
+    if (s != HHMM_OK)
+        return s;
+    return selftest_cr_math(in, out, n, 3);
+}
+
 } /* extern "C" */
 
 /* ------------------------------------------------------------------ */

@@ -1,0 +1,113 @@
+/*
+ * hhmm_detmath.h -- deterministic exp / log, shared verbatim by the CPU oracle
+ * (gcc, oracle/hhmm_oracle.c) and the gfx950 kernels (hipcc).
+ *
+ * Why: the FFBS draws (the contract of DESIGN.md §5) are
+ * compared index-for-index with the oracle, so every transcendental the
+ * contract consumes must be the same double on both sides.  It does NOT have
+ * to be Stan's (the reference's draws come from Stan's RNG and are not
+ * reproducible at all), so instead of the correctly rounded hhmm_cr_exp /
+ * hhmm_cr_log (table lookups, a rounding test, a rarely taken accurate phase)
+ * the contract uses these: a fixed sequence of IEEE-754 operations -- +, -, *,
+ * /, explicit fma, rint, bit moves -- each exactly rounded in round-to-nearest
+ * on both sides, so the result is bit-identical wherever it is evaluated.  No
+ * table, no branch (selects only), about 25 (exp) / 35 (log) instructions.
+ * Accuracy: a few ulp (well inside the 1e-9 tolerance of the float outputs
+ * computed from them).
+ *
+ *   hhmm_det_exp: x = k ln2 + r (Cody-Waite, ln2 in two parts, k*LN2_HI exact
+ *     for |k| < 2^11), |r| <= ln2/2, exp(r) by the degree-13 Taylor sum in
+ *     Horner form (truncation < 2^-57), times 2^k as two exact power-of-two
+ *     factors (one rounding, also for subnormal results).
+ *   hhmm_det_log: x = 2^e m, m in [sqrt(1/2), sqrt(2)); s = (m - 1) / (m + 1),
+ *     log m = 2 s + s^3 (2/3 + 2/5 s^2 + ... + 2/21 s^18) (truncation < 2^-60),
+ *     + e ln2 (two parts).
+ *
+ * The includer defines HHMM_MATH_FN (see hhmm_crmath.h).  Both sides compile
+ * with -ffp-contract=off, so no multiply-add is fused behind our back.
+ */
+#pragma once
+#include <stdint.h>
+
+#define HHMM_DET_INV_LN2 0x1.71547652b82fep+0
+#define HHMM_DET_LN2_HI 0x1.62e42feep-1 /* 32 significant bits */
+#define HHMM_DET_LN2_LO 0x1.a39ef35793c76p-33
+#define HHMM_DET_SQRT2 0x1.6a09e667f3bcdp+0
+
+HHMM_MATH_FN double hhmm_det_bits(uint64_t u)
+{
+    union { uint64_t u; double d; } v;
+    v.u = u;
+    return v.d;
+}
+
+HHMM_MATH_FN uint64_t hhmm_det_ubits(double d)
+{
+    union { uint64_t u; double d; } v;
+    v.d = d;
+    return v.u;
+}
+
+/* 2^k for k in [-1022, 1023]. */
+HHMM_MATH_FN double hhmm_det_pow2(int k)
+{
+    return hhmm_det_bits((uint64_t)(k + 1023) << 52);
+}
+
+HHMM_MATH_FN double hhmm_det_exp(double x)
+{
+    /* clamp into [-746, 710]: below, exp rounds to 0; above, to +inf -- the
+     * clamped argument still gives exactly that (NaN is selected at the end) */
+    const double xc = x < -746.0 ? -746.0 : (x > 710.0 ? 710.0 : x);
+    const double kd = __builtin_rint(xc * HHMM_DET_INV_LN2);
+    double r = __builtin_fma(-kd, HHMM_DET_LN2_HI, xc);
+    r = __builtin_fma(-kd, HHMM_DET_LN2_LO, r);
+    double p = 0x1.6124613a86d09p-33;
+    p = __builtin_fma(p, r, 0x1.1eed8eff8d898p-29);
+    p = __builtin_fma(p, r, 0x1.ae64567f544e4p-26);
+    p = __builtin_fma(p, r, 0x1.27e4fb7789f5cp-22);
+    p = __builtin_fma(p, r, 0x1.71de3a556c734p-19);
+    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-16);
+    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-13);
+    p = __builtin_fma(p, r, 0x1.6c16c16c16c17p-10);
+    p = __builtin_fma(p, r, 0x1.1111111111111p-7);
+    p = __builtin_fma(p, r, 0x1.5555555555555p-5);
+    p = __builtin_fma(p, r, 0x1.5555555555555p-3);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    /* k in [-1077, 1025]: 2^k = 2^k1 2^k2 with both factors normal */
+    const int k = (int)kd;
+    const int k1 = k / 2;
+    const int k2 = k - k1;
+    const double y = (p * hhmm_det_pow2(k1)) * hhmm_det_pow2(k2);
+    return x != x ? x + x : y;
+}
+
+HHMM_MATH_FN double hhmm_det_log(double x)
+{
+    const int sub = x < 0x1p-1022;
+    const uint64_t u = hhmm_det_ubits(sub ? x * 0x1p54 : x);
+    const double m0 = hhmm_det_bits((u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL); /* [1, 2) */
+    const int hi = m0 > HHMM_DET_SQRT2;
+    const double m = hi ? m0 * 0.5 : m0; /* [sqrt(1/2), sqrt(2)), exact */
+    const int e = (int)((u >> 52) & 0x7ff) - 1023 - (sub ? 54 : 0) + hi;
+    const double s = (m - 1.0) / (m + 1.0); /* m - 1 exact */
+    const double s2 = s * s;
+    double q = 0x1.8618618618618p-4;
+    q = __builtin_fma(q, s2, 0x1.af286bca1af28p-4);
+    q = __builtin_fma(q, s2, 0x1.e1e1e1e1e1e1ep-4);
+    q = __builtin_fma(q, s2, 0x1.1111111111111p-3);
+    q = __builtin_fma(q, s2, 0x1.3b13b13b13b14p-3);
+    q = __builtin_fma(q, s2, 0x1.745d1745d1746p-3);
+    q = __builtin_fma(q, s2, 0x1.c71c71c71c71cp-3);
+    q = __builtin_fma(q, s2, 0x1.2492492492492p-2);
+    q = __builtin_fma(q, s2, 0x1.999999999999ap-2);
+    q = __builtin_fma(q, s2, 0x1.5555555555555p-1);
+    const double lm = __builtin_fma(s * s2, q, 2.0 * s);
+    const double E = (double)e;
+    const double y = __builtin_fma(E, HHMM_DET_LN2_HI, __builtin_fma(E, HHMM_DET_LN2_LO, lm));
+    /* log(+0) = -inf, log(x < 0) = log(NaN) = NaN, log(+inf) = +inf */
+    const double special = x == 0.0 ? -__builtin_inf() : (x == __builtin_inf() ? x : hhmm_det_bits(0x7ff8000000000000ULL));
+    return (x > 0.0 && x < __builtin_inf()) ? y : special;
+}

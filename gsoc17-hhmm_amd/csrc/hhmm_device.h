@@ -15,10 +15,58 @@
 #define HHMM_MATH_TABLE static __constant__
 #endif
 #include "hhmm_crmath.h"
+#include "hhmm_detmath.h"
 
 namespace hhmm {
 
 constexpr double kLn2 = 0x1.62e42fefa39efp-1;
+
+/* ------------------------------------------------------------------ */
+/* Correctly rounded exp / log for hot loops                            */
+/* ------------------------------------------------------------------ */
+
+/* hhmm_cr_exp / hhmm_cr_log as a kernel's inner loop wants them: the quick
+ * phase runs on every lane unconditionally (special arguments replaced by a
+ * harmless one, the rounding test as selects), and ONE divergent branch sends
+ * the lanes whose argument is special or whose rounding test fails (~2^-15 of
+ * arguments) to the full function.  The same double as hhmm_cr_exp /
+ * hhmm_cr_log for every argument: the full functions take exactly this quick
+ * branch when its conditions hold.  Written out as nested branches, the full
+ * functions cost ~4 exec-mask regions per call in every loop iteration. */
+__device__ __attribute__((noinline)) static double cr_exp_cold(double x) { return hhmm_cr_exp(x); }
+__device__ __attribute__((noinline)) static double cr_log_cold(double x) { return hhmm_cr_log(x); }
+
+__device__ __forceinline__ bool cr_round_safe(double v, double w, double err)
+{
+    const uint64_t b = hhmm_double_to_bits(v);
+    const uint64_t eb = b & 0x7ff0000000000000ULL;
+    const double hu0 = hhmm_bits_to_double(eb) * 0x1p-53;
+    const double hu = (b & 0x000fffffffffffffULL) == 0 ? hu0 * 0.5 : hu0;
+    return (eb != 0) & (eb != 0x7ff0000000000000ULL) & (__builtin_fabs(w) + err < hu);
+}
+
+__device__ __forceinline__ double dev_cr_exp(double x)
+{
+    const bool in = (x > -707.0) & (x < 693.0); /* NaN: false */
+    int e;
+    const hhmm_dd f = hhmm_cr_exp_quick_dd(in ? x : 0.0, &e);
+    const bool ok = in & cr_round_safe(f.hi, f.lo, f.hi * 0x1p-72);
+    double r = f.hi * hhmm_bits_to_double((uint64_t)(e + 1023) << 52);
+    if (!ok)
+        r = cr_exp_cold(x);
+    return r;
+}
+
+__device__ __forceinline__ double dev_cr_log(double x)
+{
+    const bool in = (x >= 0x1p-1022) & (x < __builtin_inf()) & (x != 1.0); /* NaN: false */
+    const hhmm_dd f = hhmm_cr_log_quick_dd(in ? x : 2.0);
+    const bool ok = in & cr_round_safe(f.hi, f.lo, __builtin_fabs(f.hi) * 0x1p-68);
+    double r = f.hi;
+    if (!ok)
+        r = cr_log_cold(x);
+    return r;
+}
 
 /* ------------------------------------------------------------------ */
 /* Small device helpers                                                  */

@@ -162,7 +162,7 @@ __device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevA
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                pp.A[i][j] = LOG ? hhmm_cr_log(A[i][j]) : A[i][j];
+                pp.A[i][j] = LOG ? dev_cr_log(A[i][j]) : A[i][j];
     } else {
         double raw[K][K];
 #pragma unroll
@@ -185,13 +185,13 @@ __device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevA
         for (int i = 0; i < K; ++i)
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                pp.A[i][j] = LOG ? hhmm_cr_log(raw[i][j]) : raw[i][j];
+                pp.A[i][j] = LOG ? dev_cr_log(raw[i][j]) : raw[i][j];
         if constexpr (ModelTraits<MODEL>::kGauss) {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 pp.mu[k] = mu[k];
                 pp.isig[k] = 1.0 / sg[k];
-                pp.lsig[k] = hhmm_cr_log(sg[k]);
+                pp.lsig[k] = dev_cr_log(sg[k]);
                 pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - pp.lsig[k];
             }
         }
@@ -222,8 +222,8 @@ __device__ __forceinline__ void fill_table(double2 *slab, const DevArgs &a, int6
                 for (int kp = 0; kp < KP; ++kp) {
                     double v0 = v[r][2 * kp], v1 = v[r][2 * kp + 1];
                     if (LOG) {
-                        v0 = hhmm_cr_log(v0);
-                        v1 = hhmm_cr_log(v1);
+                        v0 = dev_cr_log(v0);
+                        v1 = dev_cr_log(v1);
                     }
                     slab[((l0 + r) * KP + kp) * 64] = make_double2(v0, v1);
                 }
@@ -267,9 +267,9 @@ struct Em {
     double m;
 };
 
-/* CREXP: the Gaussian exp is the correctly rounded one (FFBS contract: the
+/* DETEXP: the Gaussian exp is hhmm_det_exp (FFBS contract, DESIGN.md §5: the
  * filter the draws come from is bit-reproducible by the oracle). */
-template <int MODEL, int K, bool CREXP = false>
+template <int MODEL, int K, bool DETEXP = false>
 __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const double2 *slab, int L,
                                           const Obs &o, Em<K> &em)
 {
@@ -283,7 +283,7 @@ __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const 
         }
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            em.e[j] = CREXP ? hhmm_cr_exp(lp[j] - m) : exp(lp[j] - m);
+            em.e[j] = DETEXP ? hhmm_det_exp(lp[j] - m) : exp(lp[j] - m);
         em.m = m;
     } else {
         read_table<K>(slab, o.x, L, em.e);
@@ -651,7 +651,7 @@ __device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, 
                                           int &bex, const double (&uu)[fb_ffbs(MODE) ? C : 1], const Obs &onext,
                                           int &z)
 {
-    constexpr bool CREXP = fb_ffbs(MODE);
+    constexpr bool DETEXP = fb_ffbs(MODE);
     const int t0 = c * C;
     double abuf[C][K];
     double lsbuf[fb_base(MODE) == FB_FULL ? C : 1];
@@ -663,11 +663,11 @@ __device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, 
         double lsacc = 0.0;
         int exb = 0;
         Em<K> ecur;
-        emit_prob<MODEL, K, CREXP>(ln.pp, ln.slab, ln.L, cur[1 < C ? 1 : 0], ecur);
+        emit_prob<MODEL, K, DETEXP>(ln.pp, ln.slab, ln.L, cur[1 < C ? 1 : 0], ecur);
 #pragma unroll
         for (int u = 1; u < C; ++u) {
             Em<K> enx;
-            emit_prob<MODEL, K, CREXP>(ln.pp, ln.slab, ln.L, cur[u + 1 < C ? u + 1 : u], enx);
+            emit_prob<MODEL, K, DETEXP>(ln.pp, ln.slab, ln.L, cur[u + 1 < C ? u + 1 : u], enx);
             if (FULLC || t0 + u < ln.Tp) {
                 lsacc += ecur.m;
                 fwd_step_to<MODEL, K>(abuf[u - 1], abuf[u], ln.pp, ecur.e, cur[u], exb);
@@ -1615,7 +1615,7 @@ __global__ void __launch_bounds__(64) viterbi_sp_kernel(const DevArgs a)
     if constexpr (ModelTraits<MODEL>::kDiscrete) {
         double *col = ldsd + lane;
         for (int l = 0; l < a.L; ++l)
-            col[l * 64] = hhmm_cr_log(draw2<K>(a.phi_k, a, d, ln.js, l, K));
+            col[l * 64] = dev_cr_log(draw2<K>(a.phi_k, a, d, ln.js, l, K));
     }
     if constexpr (ModelTraits<MODEL>::kTayal) {
         double *rows = ldsd + (size_t)a.L * 64 + lane;

@@ -29,13 +29,23 @@
  * broadcast loads.  w_km (and b_km) live in registers; the mixture tables
  * (log lambda, mu, 1/s, NEG_LOG_SQRT_TWO_PI - log s) in a per-lane LDS slab.
  *
- * Exactness: Viterbi paths are bit-exact with the oracle, so whenever zstar /
- * logp_zstar / FFBS draws are requested (EXACT), every transcendental the
- * Viterbi or FFBS consumes -- the softmax exps, log A, the mixture LSE, the
- * log(sigma) of normal_lpdf -- is the shared correctly rounded hhmm_cr_exp /
- * hhmm_cr_log, in the reference's operation order (Eigen SSE2 dot order,
- * sequential softmax sum, Stan's log_sum_exp).  Otherwise the device libm
- * (within the 1e-9 tolerance of the float outputs) is used.
+ * Arithmetic modes (template MATH, chosen per request by launch_io3):
+ *   IO_LIBM  no bit-exact output: device libm everywhere (within the 1e-9
+ *            tolerance of the float outputs);
+ *   IO_CR    zstar / logp_zstar requested: every transcendental the Viterbi
+ *            consumes -- the softmax exps, log A, the mixture LSE, the
+ *            log(sigma) of normal_lpdf -- is the shared correctly rounded
+ *            exp / log (dev_cr_exp / dev_cr_log = hhmm_cr_exp / hhmm_cr_log),
+ *            in the reference's operation order (Eigen SSE2 dot order,
+ *            sequential softmax sum, Stan's log_sum_exp), so paths are
+ *            bit-exact with the oracle; the filter's e_t stays libm;
+ *   IO_DET   FFBS draws requested: the same transcendentals, plus the
+ *            filter's e_t, are the deterministic hhmm_det_exp / hhmm_det_log
+ *            of the FFBS contract (cheap, table-free, and
+ *            bit-identical in the oracle).
+ * A request with both Viterbi and FFBS outputs runs an IO_CR sweep and an
+ * IO_DET sweep (FFBS only).  log A_t is evaluated only when the Viterbi or the
+ * logA_ij output consumes it.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -50,19 +60,25 @@ constexpr int kIoLmax = 8; /* mixture components per state on the device path */
 
 enum IoFam { IO_REG = 0, IO_MIX = 1 };
 
-template <bool EXACT>
+enum IoMath { IO_LIBM = 0, IO_CR = 1, IO_DET = 2 };
+
+template <int MATH>
 __device__ __forceinline__ double io_exp(double x)
 {
-    if constexpr (EXACT)
-        return hhmm_cr_exp(x);
+    if constexpr (MATH == IO_CR)
+        return dev_cr_exp(x);
+    else if constexpr (MATH == IO_DET)
+        return hhmm_det_exp(x);
     else
         return exp(x);
 }
-template <bool EXACT>
+template <int MATH>
 __device__ __forceinline__ double io_log(double x)
 {
-    if constexpr (EXACT)
-        return hhmm_cr_log(x);
+    if constexpr (MATH == IO_CR)
+        return dev_cr_log(x);
+    else if constexpr (MATH == IO_DET)
+        return hhmm_det_log(x);
     else
         return log(x);
 }
@@ -110,7 +126,7 @@ __device__ __forceinline__ double sse_dot(const double (&a)[MMAX], const double 
 }
 
 /* Stan Math softmax(v): theta = exp(v - max v); theta / sequential sum. */
-template <int K, bool EXACT>
+template <int K, int MATH>
 __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K])
 {
     double mx = v[0];
@@ -121,7 +137,7 @@ __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[
     double sum = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        th[i] = io_exp<EXACT>(v[i] - mx);
+        th[i] = io_exp<MATH>(v[i] - mx);
         sum += th[i];
     }
 #pragma unroll
@@ -160,7 +176,7 @@ struct IoStep {
  * normal_lpdf = ((NEG_LOG_SQRT_TWO_PI - log s) + (-0.5 * z^2)), z = (x - mu) * (1/s);
  * log_sum_exp(std::vector): max by '>', sum of exp(x - max) over x != -inf
  * in order, max + log(sum). */
-template <int FAM, int K, int MMAX, bool EXACT>
+template <int FAM, int K, int MMAX, int MATH>
 __device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, const double2 *slab, int L, int M,
                                             double x, const double (&u)[MMAX], double (&o)[K])
 {
@@ -193,26 +209,28 @@ __device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, co
 #pragma unroll
             for (int l = 0; l < kIoLmax; ++l)
                 if (l < L && acc[l] != dev_ninf())
-                    sum += io_exp<EXACT>(acc[l] - mx);
-            o[j] = mx + io_log<EXACT>(sum);
+                    sum += io_exp<MATH>(acc[l] - mx);
+            o[j] = mx + io_log<MATH>(sum);
         }
     }
 }
 
 /* Transition vector of step t >= 1: A_t = softmax(u_t' w_j), log A_t
  * (iohmm-reg.stan:40-49; iohmm-mix.stan:42-51, :69; iohmm-hmix.stan:36-48). */
-template <int FAM, int K, int MMAX, bool EXACT>
+template <int FAM, int K, int MMAX, int MATH>
 __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, int M, const double (&u)[MMAX],
-                                              IoStep<K> &st)
+                                              IoStep<K> &st, bool need_lA)
 {
     double v[K];
 #pragma unroll
     for (int j = 0; j < K; ++j)
         v[j] = sse_dot<MMAX>(u, pp.w[j], M);
-    stan_softmax<K, EXACT>(v, st.A);
+    stan_softmax<K, MATH>(v, st.A);
+    if (need_lA) {
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-        st.lA[j] = io_log<EXACT>(st.A[j]);
+        for (int j = 0; j < K; ++j)
+            st.lA[j] = io_log<MATH>(st.A[j]);
+    }
 }
 
 /* Loads x_t and u_t[0..M) of one series (clamped, unconditional). */
@@ -229,7 +247,7 @@ __device__ __forceinline__ void io_load(const DevArgs &a, uint32_t n, int t, dou
     }
 }
 
-template <int FAM, int K, int MMAX, bool EXACT>
+template <int FAM, int K, int MMAX, int MATH>
 __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 {
     HIP_DYNAMIC_SHARED(double2, lds)
@@ -244,10 +262,11 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
     const int Tp = pair_len(a, n);
     const int M = a.M, L = a.L;
     const uint32_t out = a.outputs;
-    const bool want_vit = EXACT && (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR));
-    const bool want_ffbs = EXACT && (out & HHMM_OUT_FFBS) && a.z_ffbs;
+    const bool want_vit = MATH == IO_CR && (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR));
+    const bool want_ffbs = MATH == IO_DET && (out & HHMM_OUT_FFBS) && a.z_ffbs;
     const bool fixed_init = (a.model == HHMM_MODEL_IOHMM_HMIX); /* iohmm-hmix.stan:166-167 */
     const bool log_A_out = (a.model == HHMM_MODEL_IOHMM_HMIX || a.model == HHMM_MODEL_IOHMM_HMIX_LITE);
+    const bool need_lA = want_vit || (log_A_out && (out & HHMM_OUT_LOGA) && a.logA);
 
     /* ---- per-pair parameters ---- */
     IoParams<FAM, K, MMAX> pp;
@@ -263,7 +282,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
         if constexpr (FAM == IO_REG) {
             const double s = a.s_k[d + a.S * k];
             pp.isig[k] = 1.0 / s;
-            pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - io_log<EXACT>(s);
+            pp.c0[k] = HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(s);
         }
     }
     double2 *slab = lds + (size_t)wave * K * L * 2 * 64 + lane;
@@ -275,7 +294,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                 const double s = a.s_kl[ix];
                 *const_cast<double2 *>(mix_row(slab, L, j, l, 0)) = make_double2(a.mu_kl[ix], 1.0 / s);
                 *const_cast<double2 *>(mix_row(slab, L, j, l, 1)) =
-                    make_double2(io_log<EXACT>(a.lambda_kl[ix]), HHMM_NEG_LOG_SQRT_TWO_PI - io_log<EXACT>(s));
+                    make_double2(io_log<MATH>(a.lambda_kl[ix]), HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(s));
             }
     }
     const int Tw_min = wave_min(Tp);
@@ -297,16 +316,16 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
         io_load<MMAX>(a, (uint32_t)n, t + 1, xn, un); /* one step ahead */
         if (t < Tp) {
             IoStep<K> st;
-            io_emission<FAM, K, MMAX, EXACT>(pp, slab, L, M, x, u, st.o);
+            io_emission<FAM, K, MMAX, MATH>(pp, slab, L, M, x, u, st.o);
             if (t == 0) {
                 /* A_ij[1] = p_1k (filler, iohmm-reg.stan:41-42); logA_ij[1] = log(p_1k) (iohmm-hmix.stan:40) */
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     st.A[k] = pp.p[k];
-                    st.lA[k] = log_A_out ? io_log<EXACT>(pp.p[k]) : 0.0;
+                    st.lA[k] = log_A_out ? io_log<MATH>(pp.p[k]) : 0.0;
                 }
             } else {
-                io_transition<FAM, K, MMAX, EXACT>(pp, M, u, st);
+                io_transition<FAM, K, MMAX, MATH>(pp, M, u, st, need_lA);
             }
             if ((out & HHMM_OUT_OBLIK_TK) && a.oblik)
                 store_tk<K>(a.oblik, a, p, t, st.o);
@@ -321,10 +340,10 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
             if (m == dev_ninf())
                 m = 0.0; /* every emission impossible: f_t = 0, alpha = NaN as in Stan */
             double e[K];
-            if (EXACT && want_ffbs) { /* the FFBS contract's e_t (correctly rounded exp) */
+            if constexpr (MATH == IO_DET) { /* the FFBS contract's e_t */
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    e[k] = hhmm_cr_exp(st.o[k] - m);
+                    e[k] = hhmm_det_exp(st.o[k] - m);
             } else {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -502,23 +521,23 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 #ifndef HHMM_IO_REG_WAVES
 #define HHMM_IO_REG_WAVES 2
 #endif
-template <int K, int MMAX, bool EXACT>
+template <int K, int MMAX, int MATH>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HHMM_IO_REG_WAVES))) iohmm_reg_kernel(const DevArgs a)
 {
-    iohmm_sweep<IO_REG, K, MMAX, EXACT>(a);
+    iohmm_sweep<IO_REG, K, MMAX, MATH>(a);
 }
 
-template <int K, int MMAX, bool EXACT>
+template <int K, int MMAX, int MATH>
 __global__ void __launch_bounds__(kBlock) iohmm_mix_kernel(const DevArgs a)
 {
-    iohmm_sweep<IO_MIX, K, MMAX, EXACT>(a);
+    iohmm_sweep<IO_MIX, K, MMAX, MATH>(a);
 }
 
 /* ------------------------------------------------------------------ */
 /* Host-side launch                                                      */
 /* ------------------------------------------------------------------ */
 
-template <int FAM, int K, int MMAX, bool EXACT>
+template <int FAM, int K, int MMAX, int MATH>
 static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
 {
     const size_t per_wave = (FAM == IO_MIX) ? (size_t)K * a.L * 2 * 64 * sizeof(double2) : 0;
@@ -532,9 +551,9 @@ static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
     const int threads = 64 * waves;
     const dim3 grid((unsigned)((a.P + threads - 1) / threads));
     if constexpr (FAM == IO_REG)
-        hipLaunchKernelGGL((iohmm_reg_kernel<K, MMAX, EXACT>), grid, dim3(threads), per_wave * waves, st, a);
+        hipLaunchKernelGGL((iohmm_reg_kernel<K, MMAX, MATH>), grid, dim3(threads), per_wave * waves, st, a);
     else
-        hipLaunchKernelGGL((iohmm_mix_kernel<K, MMAX, EXACT>), grid, dim3(threads), per_wave * waves, st, a);
+        hipLaunchKernelGGL((iohmm_mix_kernel<K, MMAX, MATH>), grid, dim3(threads), per_wave * waves, st, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("iohmm kernel launch: %s", hipGetErrorString(e));
@@ -543,13 +562,29 @@ static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
     return HHMM_OK;
 }
 
+template <int FAM, int K, int MATH>
+static hhmm_status launch_io_m(const DevArgs &a, hipStream_t st)
+{
+    return a.M <= 4 ? launch_io4<FAM, K, 4, MATH>(a, st) : launch_io4<FAM, K, 8, MATH>(a, st);
+}
+
+/* The arithmetic mode(s) of a request (see the header comment). */
 template <int FAM, int K>
 static hhmm_status launch_io3(const DevArgs &a, hipStream_t st)
 {
-    const bool exact = (a.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR | HHMM_OUT_FFBS)) != 0;
-    if (a.M <= 4)
-        return exact ? launch_io4<FAM, K, 4, true>(a, st) : launch_io4<FAM, K, 4, false>(a, st);
-    return exact ? launch_io4<FAM, K, 8, true>(a, st) : launch_io4<FAM, K, 8, false>(a, st);
+    const bool vit = (a.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) != 0;
+    const bool ffbs = (a.outputs & HHMM_OUT_FFBS) != 0 && a.z_ffbs;
+    if (!ffbs)
+        return vit ? launch_io_m<FAM, K, IO_CR>(a, st) : launch_io_m<FAM, K, IO_LIBM>(a, st);
+    if (!vit)
+        return launch_io_m<FAM, K, IO_DET>(a, st);
+    DevArgs b = a;
+    b.outputs = a.outputs & ~(uint32_t)HHMM_OUT_FFBS;
+    const hhmm_status s = launch_io_m<FAM, K, IO_CR>(b, st);
+    if (s != HHMM_OK)
+        return s;
+    b.outputs = HHMM_OUT_FFBS;
+    return launch_io_m<FAM, K, IO_DET>(b, st);
 }
 
 /* Dispatch on K for the K values [KK, KHI] this translation unit instantiates. */

@@ -54,7 +54,10 @@ __global__ void cr_math_kernel(const double *in, double *out, int64_t n, int whi
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n)
-        out[i] = which ? hhmm_cr_exp(in[i]) : hhmm_cr_log(in[i]);
+        out[i] = which == 0 ? dev_cr_log(in[i])
+                 : which == 1 ? dev_cr_exp(in[i])
+                 : which == 2 ? hhmm_det_log(in[i])
+                              : hhmm_det_exp(in[i]);
 }
 
 

@@ -145,7 +145,7 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G> &ln, const DevArgs &a,
     }
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-        ln.col[i] = (LOG && i < a.K) ? hhmm_cr_log(rawc[i]) : rawc[i];
+        ln.col[i] = (LOG && i < a.K) ? dev_cr_log(rawc[i]) : rawc[i];
         ln.row[i] = rawr[i];
     }
     ln.pj = a.p_1k[d + S * jj];
@@ -153,7 +153,7 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G> &ln, const DevArgs &a,
         const double sg = a.sigma_k[d + S * jj];
         ln.mu = a.mu_k[d + S * jj];
         ln.isig = 1.0 / sg;
-        ln.lsig = hhmm_cr_log(sg);
+        ln.lsig = dev_cr_log(sg);
         ln.c0 = HHMM_NEG_LOG_SQRT_TWO_PI - ln.lsig;
     }
     /* LDS: [groups][2][G] exchange, then [groups][L][G] tables */
@@ -169,7 +169,7 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G> &ln, const DevArgs &a,
 #pragma unroll
             for (int r = 0; r < 8; ++r)
                 if (l0 + r < a.L)
-                    tab[(l0 + r) * G + ln.j] = (LOG && ln.on) ? hhmm_cr_log(v[r]) : v[r];
+                    tab[(l0 + r) * G + ln.j] = (LOG && ln.on) ? dev_cr_log(v[r]) : v[r];
         }
     }
     __syncthreads();

@@ -234,4 +234,8 @@ def declare(lib):
     lib.hhmm_selftest_cr_log.restype = C.c_int
     lib.hhmm_selftest_cr_exp.argtypes = [F64P, F64P, C.c_int64]
     lib.hhmm_selftest_cr_exp.restype = C.c_int
+    lib.hhmm_selftest_det_log.argtypes = [F64P, F64P, C.c_int64]
+    lib.hhmm_selftest_det_log.restype = C.c_int
+    lib.hhmm_selftest_det_exp.argtypes = [F64P, F64P, C.c_int64]
+    lib.hhmm_selftest_det_exp.restype = C.c_int
     return lib

@@ -268,9 +268,12 @@ hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res,
                             void *workspace, size_t workspace_bytes, void *stream);
 
 /* Self-test hooks: the device's correctly rounded log / exp over n host
- * doubles (the transcendentals every exact Viterbi / FFBS input goes through). */
+ * doubles (the transcendentals every exact Viterbi input goes through), and
+ * the deterministic log / exp of the FFBS contract (hhmm_detmath.h). */
 hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n);
 hhmm_status hhmm_selftest_cr_exp(const double *in, double *out, int64_t n);
+hhmm_status hhmm_selftest_det_log(const double *in, double *out, int64_t n);
+hhmm_status hhmm_selftest_det_exp(const double *in, double *out, int64_t n);
 
 #ifdef __cplusplus
 }

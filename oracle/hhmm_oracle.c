@@ -37,6 +37,7 @@
 #define HHMM_MATH_FN static inline
 #define HHMM_MATH_TABLE static
 #include "hhmm_crmath.h"
+#include "hhmm_detmath.h"
 
 #ifdef _OPENMP
 #include <omp.h>
@@ -311,7 +312,7 @@ static void ctx_alloc(pair_ctx *c, int K, int L, int M, int Tm, int Toos)
     c->logA = xmalloc(sizeof(double) * tk);
     c->delta = xmalloc(sizeof(double) * tk);
     c->acc = xmalloc(sizeof(double) * (K > KL ? K : KL));
-    c->tmp = xmalloc(sizeof(double) * (K > KL ? K : KL));
+    c->tmp = xmalloc(sizeof(double) * 2 * (K > KL ? K : KL)); /* FFBS: w and A_{t+1} */
     c->bp = xmalloc(sizeof(int32_t) * tk);
     c->zstar = xmalloc(sizeof(int32_t) * TT);
     c->oblik_t = xmalloc(sizeof(double) * TT);
@@ -899,8 +900,11 @@ static void model_tayal_lite(pair_ctx *c)
  *
  *   filter f_t (K-vector, linear space, renormalised each step):
  *     e_t(j) = emission: phi_k[j, x_t] (multinomial / semisup / Tayal);
- *              cr_exp(lpdf_j - m) with m = fmax over j (hmm.stan Gaussian);
- *              cr_exp(oblik_t(j) - m), m = fmax over j (0 if -inf) (IOHMM)
+ *              det_exp(lpdf_j - m) with m = fmax over j (hmm.stan Gaussian);
+ *              det_exp(ob_t(j) - m), m = fmax over j (0 if -inf) (IOHMM)
+ *     det_exp / det_log: the deterministic exp / log of hhmm_detmath.h (the
+ *     contract's own transcendentals: bit-identical on both sides, cheaper
+ *     than the correctly rounded ones the Viterbi needs)
  *     f_0(j) = p_j * e_0(j); hmm.stan: p_j (Q2, the summed emission cancels);
  *              Tayal: e_0(j) * p_j only where the init predicate holds, else e_0(j)
  *     f_t(j) = s_t(j) * e_t(j), s_t(j) = f(0) A(0,j), then fma(f(i), A(i,j), s) for i = 1..K-1;
@@ -917,6 +921,9 @@ static void model_tayal_lite(pair_ctx *c)
  *   IOHMM (Q5: the transition K-vector A_t does not depend on the next state,
  *     so f_t is proportional to e_t for t >= 1 and the draws decouple):
  *     v_0 = p .* e_0, v_t = e_t (t >= 1); z_t = cat(v_t .* A_{t+1}, u_t); z_{T-1} = cat(v_{T-1}, u_{T-1}).
+ *     ob_t and A_t are the model's emission and softmax transition in the
+ *     model's operation order (iohmm-reg.stan:40-57, iohmm-mix.stan:42-65,
+ *     iohmm-hmix.stan:36-62) with det_exp / det_log in place of exp / log.
  */
 static void ffbs_renorm(double *v, int K)
 {
@@ -957,7 +964,7 @@ static void ffbs_emission_hmm(const pair_ctx *c, int gauss, const int32_t *x, in
             m = fmax(m, e[j]);
         }
         for (int j = 0; j < K; ++j)
-            e[j] = OR_EXP(e[j] - m);
+            e[j] = hhmm_det_exp(e[j] - m);
     } else {
         for (int j = 0; j < K; ++j)
             e[j] = PHI(j, x[t] - 1);
@@ -973,6 +980,53 @@ static int ffbs_mask(int model, const pair_ctx *c, int t, int j1)
     return 1;
 }
 
+/* The IOHMM emission ob_t (K-vector) and softmax transition A_t (t >= 1) of
+ * the FFBS contract: the model's blocks (iohmm_mixture_oblik, model_iohmm_reg's
+ * emission, iohmm_transitions above) with det_exp / det_log. */
+static void ffbs_iohmm_oblik(const pair_ctx *c, int model, int t, double *ob)
+{
+    const int K = c->K, M = c->M, L = c->L;
+    double acc[L > 0 ? L : 1];
+    for (int j = 0; j < K; ++j) {
+        if (model == HHMM_MODEL_IOHMM_REG) { /* normal_lpdf(x_t | u_t' b_j, s_j) (iohmm-reg.stan:51-57) */
+            const double mu = stan_dot(&c->u[(size_t)t * M], &c->b[(size_t)j * M], M);
+            const double z = (c->xr[t] - mu) * (1.0 / c->sk[j]);
+            ob[j] = (HHMM_NEG_LOG_SQRT_TWO_PI - hhmm_det_log(c->sk[j])) + (-0.5 * (z * z));
+            continue;
+        }
+        /* LSE_l(log lambda_jl + normal_lpdf(x_t | mu_jl, s_jl)) (iohmm-mix.stan:53-65) */
+        double mx = NEG_INF, sum = 0.0;
+        for (int l = 0; l < L; ++l) {
+            const double s = c->skl[j * L + l];
+            const double z = (c->xr[t] - c->mukl[j * L + l]) * (1.0 / s);
+            acc[l] = hhmm_det_log(c->lambda[j * L + l]) + ((HHMM_NEG_LOG_SQRT_TWO_PI - hhmm_det_log(s)) + (-0.5 * (z * z)));
+            if (acc[l] > mx)
+                mx = acc[l];
+        }
+        for (int l = 0; l < L; ++l)
+            if (acc[l] != NEG_INF)
+                sum += hhmm_det_exp(acc[l] - mx);
+        ob[j] = mx + hhmm_det_log(sum);
+    }
+}
+
+static void ffbs_iohmm_transition(const pair_ctx *c, int t, double *A)
+{
+    const int K = c->K, M = c->M;
+    double mx = NEG_INF, sum = 0.0;
+    for (int j = 0; j < K; ++j) {
+        A[j] = stan_dot(&c->u[(size_t)t * M], &c->w[(size_t)j * M], M);
+        if (j == 0 || A[j] > mx)
+            mx = A[j];
+    }
+    for (int j = 0; j < K; ++j) {
+        A[j] = hhmm_det_exp(A[j] - mx);
+        sum += A[j];
+    }
+    for (int j = 0; j < K; ++j)
+        A[j] = A[j] / sum;
+}
+
 static void ffbs_contract(pair_ctx *c, int model)
 {
     const int K = c->K, T = c->T;
@@ -980,22 +1034,23 @@ static void ffbs_contract(pair_ctx *c, int model)
     const int iohmm = (model == HHMM_MODEL_IOHMM_REG || model == HHMM_MODEL_IOHMM_MIX ||
                        model == HHMM_MODEL_IOHMM_HMIX);
     if (iohmm) {
-        if (model == HHMM_MODEL_IOHMM_HMIX)
-            iohmm_transitions(c); /* the softmax values A_t (hmix keeps only their log) */
+        double *A1 = w + K; /* A_{t+1} */
         for (int t = 0; t < T; ++t) {
-            double m = TK(c->oblik, t, 0);
+            double m;
+            ffbs_iohmm_oblik(c, model, t, e);
+            m = e[0];
             for (int k = 1; k < K; ++k)
-                m = fmax(m, TK(c->oblik, t, k));
+                m = fmax(m, e[k]);
             if (m == NEG_INF)
                 m = 0.0;
             for (int k = 0; k < K; ++k) {
-                e[k] = OR_EXP(TK(c->oblik, t, k) - m);
+                e[k] = hhmm_det_exp(e[k] - m);
                 TK(c->ff, t, k) = (t == 0) ? c->p[k] * e[k] : e[k];
             }
-        }
-        for (int t = 0; t < T; ++t) {
+            if (t + 1 < T)
+                ffbs_iohmm_transition(c, t + 1, A1);
             for (int i = 0; i < K; ++i)
-                w[i] = (t + 1 < T) ? TK(c->ff, t, i) * TK(c->Arow, t + 1, i) : TK(c->ff, t, i);
+                w[i] = (t + 1 < T) ? TK(c->ff, t, i) * A1[i] : TK(c->ff, t, i);
             c->zf[t] = ffbs_cat(w, K, c->ffbs_u[t]);
         }
         return;
@@ -1325,6 +1380,19 @@ void hhmm_oracle_exp_array(const double *in, double *out, int64_t n)
 {
     for (int64_t i = 0; i < n; ++i)
         out[i] = OR_EXP(in[i]);
+}
+
+/* The FFBS contract's deterministic log / exp (hhmm_detmath.h; every build). */
+void hhmm_oracle_det_log_array(const double *in, double *out, int64_t n)
+{
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = hhmm_det_log(in[i]);
+}
+
+void hhmm_oracle_det_exp_array(const double *in, double *out, int64_t n)
+{
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = hhmm_det_exp(in[i]);
 }
 
 /* Self-check of hhmm_crmath.h's quick phases against its accurate phases

@@ -74,6 +74,17 @@ def exp_array(x, variant="cr"):
     return y
 
 
+def det_array(which, x):
+    """The FFBS contract's deterministic exp / log (which = "exp" / "log")."""
+    import numpy as np
+    lib = load("cr")
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    fn = lib.hhmm_oracle_det_exp_array if which == "exp" else lib.hhmm_oracle_det_log_array
+    fn(x.ctypes.data_as(C.POINTER(C.c_double)), y.ctypes.data_as(C.POINTER(C.c_double)), C.c_int64(x.size))
+    return y
+
+
 def crmath_quick_check(which, x):
     """(max relative quick-vs-accurate distance, rounding-test fallbacks,
     mismatches, arguments covered) of hhmm_crmath.h's quick phase; which is

@@ -30,7 +30,7 @@ def test_header_declares_entry_points():
     names = declared_functions()
     for n in ("hhmm_run", "hhmm_run_device", "hhmm_workspace_size", "hhmm_validate", "hhmm_version",
               "hhmm_last_error", "hhmm_init", "hhmm_shutdown", "hhmm_num_pairs", "hhmm_selftest_cr_log",
-              "hhmm_selftest_cr_exp", "hhmm_extract_features", "hhmm_extract_features_device",
+              "hhmm_selftest_cr_exp", "hhmm_selftest_det_log", "hhmm_selftest_det_exp", "hhmm_extract_features", "hhmm_extract_features_device",
               "hhmm_features_workspace_size", "hhmm_neighbouring_forecast",
               "hhmm_neighbouring_forecast_device", "hhmm_num_unconstrained", "hhmm_constrain_draws",
               "hhmm_constrain_draws_device"):

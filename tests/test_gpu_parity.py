@@ -68,6 +68,28 @@ def test_cr_exp_device_matches_oracle(engine, oracle):
     assert same.all(), f"{(~same).sum()} device exps differ from the oracle's"
 
 
+@pytest.mark.parametrize("which", ["log", "exp"])
+def test_det_math_device_matches_oracle(engine, oracle, which):
+    """The FFBS contract's deterministic exp / log (hhmm_detmath.h): the device
+    compilation bit-identical to the oracle's."""
+    import ctypes as C
+    from test_detmath import _args_exp, _args_log
+    g = np.random.Generator(np.random.Philox(9))
+    if which == "exp":
+        x = np.concatenate([_args_exp(), (g.random(300_000) - 0.5) * 1500.0, (g.random(100_000) - 0.5) * 40.0])
+        fn = engine.hhmm_selftest_det_exp
+    else:
+        x = np.concatenate([_args_log(), g.integers(1, 0x7FF0000000000000, size=300_000,
+                                                    dtype=np.int64).view(np.float64), g.random(100_000)])
+        fn = engine.hhmm_selftest_det_log
+    y = np.empty_like(x)
+    st = fn(x.ctypes.data_as(C.POINTER(C.c_double)), y.ctypes.data_as(C.POINTER(C.c_double)), x.size)
+    assert st == 0, engine.hhmm_last_error()
+    ref = oracle.det_array(which, x)
+    same = (y.view(np.int64) == ref.view(np.int64)) | (np.isnan(y) & np.isnan(ref))
+    assert same.all(), f"{(~same).sum()} device det_{which} differ from the oracle's"
+
+
 CASES = [
     ("hmm", dict(K=1)), ("hmm", dict(K=2)), ("hmm", dict(K=3)), ("hmm", dict(K=4)), ("hmm", dict(K=6)),
     ("hmm-multinom", dict(K=1, L=3)), ("hmm-multinom", dict(K=2, L=5)), ("hmm-multinom", dict(K=3, L=5)),
