@@ -1579,6 +1579,8 @@ __global__ void __launch_bounds__(64) viterbi_sp_kernel(const DevArgs a)
     const int lane = threadIdx.x & 63;
     const int64_t g = (int64_t)blockIdx.x * 64 + lane;
     const int64_t p = min(g >> 2, a.P - 1);
+    if (a.vs_redo && !a.vs_redo[p]) /* hhmm_vscan.h's fallback: only the pairs it flagged */
+        return;
     SpLane<MODEL, K> ln;
     ln.j = (int)(g & 3);
     ln.js = min(ln.j, K - 1);
@@ -1664,6 +1666,10 @@ __global__ void __launch_bounds__(64) viterbi_sp_kernel(const DevArgs a)
     quad_gather<K>(dl, dv);
     viterbi_epilogue<K, true>(a, p, Tp, Tw_min, Tw_max, dv, quad_or(bits));
 }
+
+} // namespace hhmm
+#include "hhmm_vscan.h"
+namespace hhmm {
 
 
 
@@ -2392,6 +2398,10 @@ static bool use_vit_states(const DevArgs &a)
 template <int MODEL, int K>
 static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
 {
+    if constexpr (K == 2 || K == 4) {
+        if (a.vs_nc > 0)
+            return launch_vscan<MODEL, K>(a, st);
+    }
     if constexpr (K >= 2 && K <= 4) {
         if (use_vit_states(a)) {
             const size_t lds = ((ModelTraits<MODEL>::kDiscrete ? (size_t)a.L : 0) +

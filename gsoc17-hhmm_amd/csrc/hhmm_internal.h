@@ -68,6 +68,15 @@ struct DevArgs {
     double *sc_sl;      /* [nc][P]       its log scale */
     double *sc_be;      /* [nc][K][P]    beta at each chunk's last step */
     double *sc_bl;      /* [nc][P]       its log scale */
+    /* T-parallel exact Viterbi (hhmm_vscan.h); vs_nc = 0: sequential decoders */
+    int32_t vs_nc;      /* V-chunks of kVsChunk steps per pair (of the Viterbi's T_max) */
+    double *vs_m;       /* [nc][K*K][P] chunk max-plus products (approximate, then on the grid) */
+    double *vs_d;       /* [nc+1][K][P] delta leaving chunk c - 1 (row c); row ncp: delta_T */
+    int32_t *vs_k;      /* [nc][P]      binary exponent of the chunk's grid (| kVsTie) */
+    uint32_t *vs_e;     /* [nc][P]      chunk backtrack map: byte s = entry state of exit state s */
+    int32_t *vs_z;      /* [nc][P]      path state at each chunk's last step (-1: no path) */
+    int32_t *vs_fail;   /* [P]          a replayed chunk disagreed: decode again sequentially */
+    const int32_t *vs_redo; /* state-parallel decoder: only pairs with vs_redo[p] != 0 (null: all) */
 };
 
 /* Phase-3 lanes of the T-scan per T-chunk: P rounded up to whole waves. */
@@ -79,6 +88,12 @@ struct ScanPlan {
     int nc;
 };
 ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint32_t flags);
+
+/* T-parallel exact Viterbi (hhmm_vscan.h): V-chunks of kVsChunk steps (a whole
+ * number of back-pointer words at K = 2 and 4); returns the chunk count per
+ * pair of a Viterbi over Tv steps, 0 when the sequential decoders run. */
+constexpr int kVsChunk = 512;
+int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t flags);
 
 /* Time steps between forward checkpoints kept for the backward sweep. */
 constexpr int fb_chunk(int K) { return K <= 4 ? 8 : 4; }

@@ -127,9 +127,27 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
     return sp;
 }
 
+int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t flags)
+{
+    const bool family = model == HHMM_MODEL_HMM_GAUSS || model == HHMM_MODEL_HMM_MULTINOM ||
+                        model == HHMM_MODEL_HMM_MULTINOM_SEMISUP || model == HHMM_MODEL_TAYAL ||
+                        model == HHMM_MODEL_TAYAL_LITE;
+    if (!family || !(K == 2 || K == 4) || !(outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) ||
+        (flags & (HHMM_FLAG_VIT_SCAN_OFF | HHMM_FLAG_VIT_LANES | HHMM_FLAG_VIT_STATES)))
+        return 0;
+    if (!(flags & HHMM_FLAG_VIT_SCAN) && (P >= 2048 || Tv < 16384))
+        return 0;
+    const int64_t nc = (Tv + kVsChunk - 1) / kVsChunk;
+    if (nc * P * K * K >= (int64_t(1) << 31)) /* 32-bit element offsets of the chunk products */
+        return 0;
+    return (int)nc;
+}
+
 /* Offsets of every workspace region (SIZE_MAX = unused) and the total. */
 struct WsLayout {
     size_t ckpt, ckpt_ls, xpk, bp, lam, mf, qb, mx, st, sl, be, bl, total;
+    size_t vm, vd, vk, ve, vz, vf;
+    int vnc;
     ScanPlan sp;
 };
 
@@ -138,6 +156,8 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     WsLayout w;
     const size_t NONE = SIZE_MAX;
     w.ckpt = w.ckpt_ls = w.xpk = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
+    w.vm = w.vd = w.vk = w.ve = w.vz = w.vf = NONE;
+    w.vnc = 0;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -180,6 +200,16 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
         const int Tv = (model == HHMM_MODEL_TAYAL_LITE) ? Toos : Tmax;
         w.bp = take((size_t)nword_of(K, Tv) * P * sizeof(uint32_t));
+        w.vnc = vscan_chunks(model, K, Tv, P, outputs, flags);
+        if (w.vnc > 0) {
+            const size_t nc = (size_t)w.vnc;
+            w.vm = take(nc * K * K * P * d);
+            w.vd = take((nc + 1) * K * P * d);
+            w.vk = take(nc * P * sizeof(int32_t));
+            w.ve = take(nc * P * sizeof(uint32_t));
+            w.vz = take(nc * P * sizeof(int32_t));
+            w.vf = take(P * sizeof(int32_t));
+        }
     }
     if (is_iohmm_model(model) && (outputs & HHMM_OUT_UNBETA))
         w.lam = take((size_t)Tmax * P * d);
@@ -211,6 +241,13 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
     a.sc_sl = (double *)at_off(w.sl);
     a.sc_be = (double *)at_off(w.be);
     a.sc_bl = (double *)at_off(w.bl);
+    a.vs_nc = w.vnc;
+    a.vs_m = (double *)at_off(w.vm);
+    a.vs_d = (double *)at_off(w.vd);
+    a.vs_k = (int32_t *)at_off(w.vk);
+    a.vs_e = (uint32_t *)at_off(w.ve);
+    a.vs_z = (int32_t *)at_off(w.vz);
+    a.vs_fail = (int32_t *)at_off(w.vf);
 }
 
 DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)

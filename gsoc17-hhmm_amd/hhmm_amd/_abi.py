@@ -43,6 +43,8 @@ FLAG_NO_FUSE = 1 << 2
 FLAG_VIT_LANES = 1 << 3
 FLAG_VIT_STATES = 1 << 4
 FLAG_FUSED = 1 << 5
+FLAG_VIT_SCAN = 1 << 6
+FLAG_VIT_SCAN_OFF = 1 << 7
 
 
 def flag_scan_chunk_log2(n):

@@ -197,6 +197,17 @@ typedef struct hhmm_draws {
  * emission tables in LDS hold the fused kernel at one wave per SIMD), so the
  * two-kernel schedule is the default. */
 #define HHMM_FLAG_FUSED (1u << 5)
+/* Viterbi over T in parallel (HMM family, K = 2 or 4): a batch
+ * of few pairs with long series decodes T-chunks in parallel and stays
+ * bit-identical to the sequential decoders -- inside a chunk whose values keep
+ * one binary exponent, Stan's rounded max-plus recursion is exact integer
+ * max-plus on that exponent's grid, so chunk products compose exactly; the
+ * chunks that cross an exponent are decoded sequentially, and every chunk is
+ * replayed from its exact entry vector and checked (a pair failing the check
+ * is decoded again by the sequential decoder).  AUTO picks it below 2048
+ * pairs with T >= 16384; VIT_SCAN forces it, VIT_SCAN_OFF forbids it. */
+#define HHMM_FLAG_VIT_SCAN (1u << 6)
+#define HHMM_FLAG_VIT_SCAN_OFF (1u << 7)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */
