@@ -40,6 +40,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <vector>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -2112,12 +2113,47 @@ __device__ __forceinline__ void load_mat(const double *base, const DevArgs &a, i
             M[i][j] = base[p + a.P * ((int64_t)(c * K + i) * K + j)];
 }
 
-/* Phase 2: one lane per pair scans its chunk products (matrices of the next
- * chunk prefetched while the current one is applied). */
+/* Phase 2: one wave per pair scans its chunk products.  The lanes fetch 64
+ * chunks' products and scale words at once (lane l: chunk block + l), stage
+ * them in LDS, and every lane walks the block with uniform-address LDS reads
+ * while the next block's loads are in flight (all lanes compute the same
+ * vectors in the same operation order; lane 0 stores).  One lane per pair
+ * walking its own chunks waited a memory round trip per chunk (C5: 2.5 ms). */
+template <int K>
+constexpr int scan_row() { return (K * K + 3 + 1) & ~1; }
+
+template <int K>
+__device__ __forceinline__ void scan_fetch(const double *base, const DevArgs &a, int64_t p, int c, double (&m)[K][K],
+                                           double (&x)[3])
+{
+    load_mat<K>(base, a, c, p, m);
+#pragma unroll
+    for (int f = 0; f < 3; ++f)
+        x[f] = a.sc_mx[p + a.P * (int64_t)(c * 3 + f)];
+}
+
+template <int K>
+__device__ __forceinline__ void scan_stage(double *blk, const double (&m)[K][K], const double (&x)[3])
+{
+    double *r = blk + (threadIdx.x & 63) * scan_row<K>();
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            r[i * K + j] = m[i][j];
+#pragma unroll
+    for (int f = 0; f < 3; ++f)
+        r[K * K + f] = x[f];
+}
+
 template <int MODEL, int K, bool BWD>
 __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
 {
-    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    HIP_DYNAMIC_SHARED(double, blk)
+    constexpr int RW = scan_row<K>();
+    const int64_t p = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool l0 = lane == 0;
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
@@ -2129,72 +2165,83 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
     for (int j = 0; j < K; ++j)
         f[j] = a.sc_mf[p + a.P * (int64_t)j];
     double sc = mx(0, 1) + kLn2 * mx(0, 0);
-    double M[K][K], Mn[K][K];
-    load_mat<K>(a.sc_mf, a, min(1, ncp - 1), p, M);
-    for (int c = 1; c < ncp; ++c) {
-        load_mat<K>(a.sc_mf, a, min(c + 1, ncp - 1), p, Mn);
+    double m[K][K], x3[3];
+    scan_fetch<K>(a.sc_mf, a, p, min(1 + lane, max(ncp - 1, 0)), m, x3);
+    for (int cb = 1; cb < ncp; cb += 64) {
+        scan_stage<K>(blk, m, x3);
+        __syncthreads();
+        scan_fetch<K>(a.sc_mf, a, p, min(cb + 64 + lane, ncp - 1), m, x3);
+        for (int i = 0; i < 64 && cb + i < ncp; ++i) {
+            const int c = cb + i;
+            const double *r = blk + i * RW;
+            if (l0) {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            a.sc_st[p + a.P * (int64_t)(c * K + k)] = f[k];
-        a.sc_sl[p + a.P * (int64_t)c] = sc;
-        double nf[K];
+                for (int k = 0; k < K; ++k)
+                    a.sc_st[p + a.P * (int64_t)(c * K + k)] = f[k];
+                a.sc_sl[p + a.P * (int64_t)c] = sc;
+            }
+            double nf[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            double acc = f[0] * M[0][j];
+            for (int j = 0; j < K; ++j) {
+                double acc = f[0] * r[j];
 #pragma unroll
-            for (int i = 1; i < K; ++i)
-                acc = fma(f[i], M[i][j], acc);
-            nf[j] = acc;
-        }
-        int e2 = 0;
-        renorm<K>(nf, e2);
-        sc += mx(c, 1) + kLn2 * (mx(c, 0) + e2);
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            f[j] = nf[j];
-#pragma unroll
-        for (int i = 0; i < K; ++i)
+                for (int ii = 1; ii < K; ++ii)
+                    acc = fma(f[ii], r[ii * K + j], acc);
+                nf[j] = acc;
+            }
+            int e2 = 0;
+            renorm<K>(nf, e2);
+            sc += r[K * K + 1] + kLn2 * (r[K * K + 0] + e2);
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                M[i][j] = Mn[i][j];
+                f[j] = nf[j];
+        }
+        __syncthreads();
     }
-    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+    if (l0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
         a.loglik[p] = log(vsum<K>(f)) + sc;
     if constexpr (BWD) {
         double b[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             b[k] = 1.0; /* unbeta_tk[T] = 1 (Q1) */
-            a.sc_be[p + a.P * (int64_t)((ncp - 1) * K + k)] = b[k];
+            if (l0)
+                a.sc_be[p + a.P * (int64_t)((ncp - 1) * K + k)] = b[k];
         }
-        a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = 0.0;
+        if (l0)
+            a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = 0.0;
         double bsc = 0.0;
-        load_mat<K>(a.sc_qb, a, ncp - 1, p, M);
-        for (int c = ncp - 1; c >= 1; --c) {
-            load_mat<K>(a.sc_qb, a, max(c - 1, 1), p, Mn);
-            double nb[K];
+        /* blocks of 64 chunks from the top down: lane l holds chunk top - l */
+        scan_fetch<K>(a.sc_qb, a, p, min(max(ncp - 1 - lane, 1), ncp - 1), m, x3);
+        for (int ct = ncp - 1; ct >= 1; ct -= 64) {
+            scan_stage<K>(blk, m, x3);
+            __syncthreads();
+            scan_fetch<K>(a.sc_qb, a, p, min(max(ct - 64 - lane, 1), ncp - 1), m, x3);
+            for (int i = 0; i < 64 && ct - i >= 1; ++i) {
+                const int c = ct - i;
+                const double *r = blk + i * RW;
+                double nb[K];
 #pragma unroll
-            for (int r = 0; r < K; ++r) {
-                double acc = M[r][0] * b[0];
+                for (int rr = 0; rr < K; ++rr) {
+                    double acc = r[rr * K + 0] * b[0];
 #pragma unroll
-                for (int i = 1; i < K; ++i)
-                    acc = fma(M[r][i], b[i], acc);
-                nb[r] = acc;
+                    for (int ii = 1; ii < K; ++ii)
+                        acc = fma(r[rr * K + ii], b[ii], acc);
+                    nb[rr] = acc;
+                }
+                int e2 = 0;
+                renorm<K>(nb, e2);
+                bsc += r[K * K + 1] + kLn2 * (r[K * K + 2] + e2);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    b[k] = nb[k];
+                    if (l0)
+                        a.sc_be[p + a.P * (int64_t)((c - 1) * K + k)] = b[k];
+                }
+                if (l0)
+                    a.sc_bl[p + a.P * (int64_t)(c - 1)] = bsc;
             }
-            int e2 = 0;
-            renorm<K>(nb, e2);
-            bsc += mx(c, 1) + kLn2 * (mx(c, 2) + e2);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                b[k] = nb[k];
-                a.sc_be[p + a.P * (int64_t)((c - 1) * K + k)] = b[k];
-            }
-            a.sc_bl[p + a.P * (int64_t)(c - 1)] = bsc;
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-                for (int j = 0; j < K; ++j)
-                    M[i][j] = Mn[i][j];
+            __syncthreads();
         }
     }
 }
@@ -2363,15 +2410,16 @@ static hhmm_status launch_fb_scan(const DevArgs &a, bool fwd_only, hipStream_t s
     const int64_t G3 = scan_lanes_per_chunk(a.P) * (int64_t)a.scan_nc; /* phase 3 lanes */
     const dim3 gridG((unsigned)((G + s.block.x - 1) / s.block.x));
     const dim3 gridG3((unsigned)((G3 + s.block.x - 1) / s.block.x));
-    const dim3 gridP((unsigned)((a.P + 63) / 64));
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     if (fwd_only) {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, false>), gridG, s.block, s.lds, st, a);
-        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), gridP, dim3(64), 0, st, a);
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64),
+                           64 * scan_row<K>() * sizeof(double), st, a);
         hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
     } else {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, true>), gridG, s.block, s.lds, st, a);
-        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), gridP, dim3(64), 0, st, a);
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64),
+                           64 * scan_row<K>() * sizeof(double), st, a);
         if (a.outputs & extra)
             hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
         else

@@ -71,6 +71,7 @@ struct DevArgs {
     /* T-parallel exact Viterbi (hhmm_vscan.h); vs_nc = 0: sequential decoders */
     int32_t vs_nc;      /* V-chunks of kVsChunk steps per pair (of the Viterbi's T_max) */
     double *vs_m;       /* [nc][K*K][P] chunk max-plus products (approximate, then on the grid) */
+    double *vs_m1;      /* [nc][K*K][P] chunks with a rounding tie: the products for odd entry values */
     double *vs_d;       /* [nc+1][K][P] delta leaving chunk c - 1 (row c); row ncp: delta_T */
     int32_t *vs_k;      /* [nc][P]      binary exponent of the chunk's grid (| kVsTie) */
     uint32_t *vs_e;     /* [nc][P]      chunk backtrack map: byte s = entry state of exit state s */

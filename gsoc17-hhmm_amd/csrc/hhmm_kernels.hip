@@ -146,7 +146,7 @@ int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t
 /* Offsets of every workspace region (SIZE_MAX = unused) and the total. */
 struct WsLayout {
     size_t ckpt, ckpt_ls, xpk, bp, lam, mf, qb, mx, st, sl, be, bl, total;
-    size_t vm, vd, vk, ve, vz, vf;
+    size_t vm, vm1, vd, vk, ve, vz, vf;
     int vnc;
     ScanPlan sp;
 };
@@ -156,7 +156,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     WsLayout w;
     const size_t NONE = SIZE_MAX;
     w.ckpt = w.ckpt_ls = w.xpk = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
-    w.vm = w.vd = w.vk = w.ve = w.vz = w.vf = NONE;
+    w.vm = w.vm1 = w.vd = w.vk = w.ve = w.vz = w.vf = NONE;
     w.vnc = 0;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -204,6 +204,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
         if (w.vnc > 0) {
             const size_t nc = (size_t)w.vnc;
             w.vm = take(nc * K * K * P * d);
+            w.vm1 = take(nc * K * K * P * d);
             w.vd = take((nc + 1) * K * P * d);
             w.vk = take(nc * P * sizeof(int32_t));
             w.ve = take(nc * P * sizeof(uint32_t));
@@ -243,6 +244,7 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
     a.sc_bl = (double *)at_off(w.bl);
     a.vs_nc = w.vnc;
     a.vs_m = (double *)at_off(w.vm);
+    a.vs_m1 = (double *)at_off(w.vm1);
     a.vs_d = (double *)at_off(w.vd);
     a.vs_k = (int32_t *)at_off(w.vk);
     a.vs_e = (uint32_t *)at_off(w.ve);

@@ -24,12 +24,14 @@
  *
  * Kernels, in stream order (lane = (pair, chunk) unless noted):
  *   vs_prod<GRID=false>  approximate chunk products (plain doubles)
- *   vs_scan0 (lane/pair) chunk 0 exactly (the model's t = 1 row, Q3 NaN step),
+ *   vs_scan0 (wave/pair) chunk 0 exactly (the model's t = 1 row, Q3 NaN step),
  *                        then the approximate scan: the binade k_c expected at
  *                        each chunk's entry
  *   vs_prod<GRID=true>   exact grid products on k_c's grid, tie flags
+ *   vs_prod_tie          chunks with a rounding tie: products for even and
+ *                        odd entry values (round-half-even depends on parity)
  *   vs_scan1 (wave/pair) the exact scan: delta_c (x) M_c where the checks hold
- *                        (entry max in binade k_c, no tie, every finite exit
+ *                        (entry max in binade k_c, every finite exit
  *                        value inside the binade), else that chunk decoded
  *                        step by step; one wave per pair, so a chunk crossing
  *                        a binade costs only its own pair
@@ -52,6 +54,7 @@ namespace hhmm {
 
 constexpr int32_t kVsTie = 1 << 30;     /* vs_k: a grid rounding tie inside the chunk */
 constexpr int32_t kVsNoGrid = -(1 << 20); /* vs_k: no finite magnitude estimate */
+constexpr int32_t kVsSeq = -(1 << 21);    /* vs_k after the exact scan: the chunk was decoded step by step */
 
 /* rho_u(a) = rint(a / u) u (exact: u a power of two); tie when a / u is a
  * half-integer.  -inf maps to -inf (never a tie). */
@@ -116,6 +119,166 @@ __device__ __forceinline__ void vs_steps(const SeriesPtrs &sp, int t0, int t1, F
     }
 }
 
+/* Rounding ties.  When a / u is a half-integer q + 1/2, fl(n u + a) rounds
+ * n + q + 1/2 to the even neighbour: m + (m & 1) with m = n + q, which
+ * depends on the parity of n.  Every step map x -> fl(x + a) is still
+ * monotone, and along a path the parity of the running value is fixed by the
+ * parity of the entry value, so a chunk holding a tie has two exact products:
+ * M0 for even entry values and M1 for odd ones (per entry state), and the
+ * exit is max_r (delta(r) + M^{parity(delta(r))}[r][j]).  vs_prod_tie_kernel
+ * computes both, in units of u (integer-valued doubles), for the chunks the
+ * grid pass flagged. */
+struct VsTerm {
+    double r, q;   /* rint(a/u), floor(a/u) */
+    double rp, qp; /* their parities (0 / 1) */
+    bool tie;
+};
+
+/* parity (0 or 1) of an integer-valued double */
+__device__ __forceinline__ double vs_parity(double x) { return x - 2.0 * floor(x * 0.5); }
+
+__device__ __forceinline__ VsTerm vs_term(double a, double iu)
+{
+    const double s = a * iu;
+    VsTerm t;
+    t.r = rint(s);
+    t.q = floor(s);
+    t.tie = __builtin_fabs(s - t.r) == 0.5;
+    t.rp = vs_parity(t.r);
+    t.qp = vs_parity(t.q);
+    return t;
+}
+
+/* o (+) a on the grid (o in units of u; ap = parity of the absolute value):
+ * returns the new offset and updates ap.  A tie rounds to the even
+ * neighbour: bump = parity(absolute + q), result even.  XOR of 0/1 doubles
+ * is |x - y|. */
+__device__ __forceinline__ double vs_add(double o, const VsTerm &t, double &ap)
+{
+    if (!(o > dev_ninf()))
+        return o;
+    if (t.tie) {
+        const double bump = __builtin_fabs(ap - t.qp);
+        ap = 0.0;
+        return (o + t.q) + bump;
+    }
+    ap = __builtin_fabs(ap - t.rp);
+    return o + t.r;
+}
+
+/* One parity product of a tie chunk (pi = parity of the entry values), into out. */
+template <int MODEL, int K>
+__device__ __forceinline__ void vs_tie_product(const DevArgs &a, const VsLane &v, const PairParams<MODEL, K> &pp,
+                                               const double2 *slab, const SeriesPtrs &sp, double iu, double u,
+                                               double pi, double *out)
+{
+    constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
+    VsTerm gA[K][K];
+    bool colTie[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        colTie[j] = false;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            gA[i][j] = vs_term(pp.A[i][j], iu);
+            colTie[j] = colTie[j] || gA[i][j].tie;
+        }
+    }
+    double M[K][K];
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            M[r][j] = (r == j) ? 0.0 : dev_ninf();
+    vs_steps<MODEL, VAUX>(sp, v.t0, v.t1, [&](int, const Obs &o) {
+        double le[K];
+        emit_log<MODEL, K>(pp, slab, a.L, o, le);
+        VsTerm gl[K];
+        bool on[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            gl[j] = vs_term(le[j], iu);
+            on[j] = true;
+            if constexpr (ModelTraits<MODEL>::kTayal)
+                on[j] = tayal_pred(o.aux, j);
+        }
+        double nm[K][K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+#pragma unroll
+            for (int r = 0; r < K; ++r) {
+                double best = dev_ninf();
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    double cand;
+                    const bool t2 = on[j] && gA[i][j].tie;
+                    if (!gl[j].tie && !t2) { /* no tie in this term: plain grid arithmetic */
+                        cand = M[r][i] + (ModelTraits<MODEL>::kTayal ? (on[j] ? gl[j].r + gA[i][j].r : gl[j].r)
+                                                                     : gA[i][j].r + gl[j].r);
+                    } else {
+                        double ap = vs_parity(M[r][i] + pi);
+                        if constexpr (ModelTraits<MODEL>::kTayal) {
+                            cand = vs_add(M[r][i], gl[j], ap);
+                            if (on[j])
+                                cand = vs_add(cand, gA[i][j], ap);
+                        } else {
+                            cand = vs_add(M[r][i], gA[i][j], ap);
+                            cand = vs_add(cand, gl[j], ap);
+                        }
+                    }
+                    best = fmax(best, cand);
+                }
+                nm[r][j] = best;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < K; ++r)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                M[r][j] = nm[r][j];
+    });
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            out[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = M[r][j] * u;
+}
+
+/* Gaussian emissions (continuous log densities: a tie shows up during the
+ * grid pass): the tie chunks' two parity products, one lane per parity. */
+template <int MODEL, int K>
+__global__ void __launch_bounds__(kBlock) vs_prod_tie_kernel(const DevArgs a)
+{
+    constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
+    constexpr int KP = (K + 1) / 2;
+    HIP_DYNAMIC_SHARED(double2, lds)
+    /* lanes [0, P*nc): even entry values; [P*nc, 2*P*nc): odd ones */
+    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int par = g0 >= a.P * (int64_t)a.vs_nc;
+    VsLane v;
+    v.p = (g0 - par * a.P * (int64_t)a.vs_nc) % a.P;
+    v.c = (int)((g0 - par * a.P * (int64_t)a.vs_nc) / a.P);
+    pair_coords(a, v.p, v.n, v.d);
+    v.Tp = pair_len(a, v.n);
+    v.t0 = v.c * kVsChunk;
+    v.t1 = min(v.t0 + kVsChunk, v.Tp);
+    if (v.c >= a.vs_nc || v.c == 0 || v.t0 >= v.Tp)
+        return;
+    const int32_t kw = a.vs_k[v.p + a.P * (int64_t)v.c];
+    if (kw == kVsNoGrid || !(kw & kVsTie) || kw < 0)
+        return;
+    const int32_t kc = kw & ~kVsTie;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+    PairParams<MODEL, K> pp;
+    load_params<MODEL, K, true>(pp, a, v.d);
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        fill_table<K, true>(slab, a, v.d);
+    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, v.n);
+    vs_tie_product<MODEL, K>(a, v, pp, slab, sp, ldexp(1.0, 52 - kc), ldexp(1.0, kc - 52), (double)par,
+                             par ? a.vs_m1 : a.vs_m);
+}
+
 /* Chunk max-plus product M = S_{t0} (x) ... (x) S_{t1-1}, M[r][j] = best path
  * sum from state r entering the chunk to state j at its last step.  GRID:
  * every term on the grid of the chunk's binade (vs_k), tie flag into vs_k. */
@@ -144,6 +307,29 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
     if constexpr (ModelTraits<MODEL>::kDiscrete)
         fill_table<K, true>(slab, a, v.d);
     bool tie = false;
+    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, v.n);
+    if constexpr (GRID && ModelTraits<MODEL>::kDiscrete) {
+        /* ties known up front (the log A and log phi tables): the chunk's two
+         * parity products right here, so no second pass waits for them */
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                any = any || vs_term(pp.A[i][j], iu).tie;
+        for (int l = 0; l < a.L; ++l)
+#pragma unroll
+            for (int kp = 0; kp < KP; ++kp) {
+                const double2 e = slab[(l * KP + kp) * 64];
+                any = any || vs_term(e.x, iu).tie || (2 * kp + 1 < K && vs_term(e.y, iu).tie);
+            }
+        if (any) {
+            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 0.0, a.vs_m);
+            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 1.0, a.vs_m1);
+            a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
+            return;
+        }
+    }
     if constexpr (GRID) {
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -157,7 +343,6 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
 #pragma unroll
         for (int j = 0; j < K; ++j)
             M[r][j] = (r == j) ? 0.0 : dev_ninf();
-    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, v.n);
     vs_steps<MODEL, VAUX>(sp, v.t0, v.t1, [&](int, const Obs &o) {
         double le[K];
         emit_log<MODEL, K>(pp, slab, a.L, o, le);
@@ -192,27 +377,7 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
         for (int j = 0; j < K; ++j)
             a.vs_m[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = M[r][j];
     if (GRID && tie)
-        a.vs_k[v.p + a.P * (int64_t)v.c] = kc | kVsTie;
-}
-
-/* delta (x) M for chunk c (rows of vs_m). */
-template <int K>
-__device__ __forceinline__ void vs_apply(const DevArgs &a, int64_t p, int c, const double (&D)[K], double (&out)[K])
-{
-    double M[K][K];
-#pragma unroll
-    for (int r = 0; r < K; ++r)
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            M[r][j] = a.vs_m[p + a.P * ((int64_t)c * K * K + r * K + j)];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        double best = D[0] + M[0][j];
-#pragma unroll
-        for (int r = 1; r < K; ++r)
-            best = fmax(best, D[r] + M[r][j]);
-        out[j] = best;
-    }
+        a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid; /* |delta| < 1: decode it */
 }
 
 template <int K>
@@ -324,87 +489,321 @@ __device__ __forceinline__ void vs_chunk(const DevArgs &a, const PairParams<MODE
     });
 }
 
-/* lane = pair: chunk 0 exactly (row 1 of vs_d), then the approximate scan
- * over the approximate chunk products: k_c = binade of the largest finite
- * delta entering chunk c. */
+/* The scans walk one pair's chunks in order, one wave per pair.  Lane l holds
+ * chunk (block + l)'s product and grid word, the next block's 64 chunks in
+ * flight while this one is walked; every lane walks the block with the values
+ * staged through LDS (uniform-address reads), so the walk neither waits on
+ * memory per chunk nor diverges (all lanes compute the same delta; lane 0
+ * stores).  A lane-per-pair walk waited one memory round trip per chunk. */
+template <int K>
+struct VsBlock {
+    double m[K][K];
+    double m1[K][K]; /* tie chunks: the products for odd entry values */
+    int32_t k;
+};
+
+template <int K>
+__device__ __forceinline__ void vs_fetch(const DevArgs &a, int64_t p, int c0, int ncp, VsBlock<K> &b)
+{
+    const int c = max(min(c0 + (int)(threadIdx.x & 63), ncp - 1), 0);
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            b.m[r][j] = a.vs_m[p + a.P * ((int64_t)c * K * K + r * K + j)];
+    b.k = a.vs_k[p + a.P * (int64_t)c];
+    const bool tie = b.k >= 0 && (b.k & kVsTie);
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            b.m1[r][j] = tie ? a.vs_m1[p + a.P * ((int64_t)c * K * K + r * K + j)] : 0.0;
+}
+
+/* The scans' series index as a VGPR value: with one pair per wave every
+ * observation address is uniform, and hipcc would fetch x_t / sign_t with
+ * scalar loads, which share lgkmcnt with the per-step LDS table reads -- each
+ * step's LDS wait then also waited for the prefetched observations. */
+__device__ __forceinline__ int64_t vs_vector_index(int64_t n)
+{
+    uint32_t v = (uint32_t)n;
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+/* The block in LDS, one row of 18 doubles per chunk (K*K products, the grid
+ * word): the walk then reads chunk i with uniform-address LDS loads instead
+ * of K*K*2 readlanes per chunk. */
+constexpr int kVsRow = 34; /* K*K products, K*K odd-entry products, the grid word */
+
+template <int K>
+__device__ __forceinline__ void vs_stage(const VsBlock<K> &b, double *blk)
+{
+    double *r = blk + (threadIdx.x & 63) * kVsRow;
+#pragma unroll
+    for (int rr = 0; rr < K; ++rr)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            r[rr * K + j] = b.m[rr][j];
+#pragma unroll
+    for (int rr = 0; rr < K; ++rr)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            r[16 + rr * K + j] = b.m1[rr][j];
+    r[32] = __longlong_as_double((long long)b.k);
+}
+
+template <int K>
+__device__ __forceinline__ int32_t vs_apply_lds(const double *blk, int i, const double (&D)[K], double (&out)[K])
+{
+    const double *r = blk + i * kVsRow;
+    const int32_t kw = (int32_t)__double_as_longlong(r[32]);
+    int off[K];
+#pragma unroll
+    for (int rr = 0; rr < K; ++rr)
+        off[rr] = rr * K;
+    if (kw >= 0 && (kw & kVsTie)) { /* M^{parity(delta(r))} per entry state */
+        const double iu = ldexp(1.0, 52 - (kw & ~kVsTie));
+#pragma unroll
+        for (int rr = 0; rr < K; ++rr)
+            off[rr] = (vs_parity(D[rr] * iu) == 1.0) ? 16 + rr * K : rr * K;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double best = D[0] + r[off[0] + j];
+#pragma unroll
+        for (int rr = 1; rr < K; ++rr)
+            best = fmax(best, D[rr] + r[off[rr] + j]);
+        out[j] = best;
+    }
+    return kw;
+}
+
+/* Step-by-step decoding inside the scans (chunk 0, and chunks that fail the
+ * grid checks), one lane per (state, quad) as viterbi_sp_kernel does: every
+ * quad of the wave runs the same pair, lane j of a quad holds delta(j) and
+ * forms its K candidates from the quad's delta by DPP broadcasts, with
+ * vit_step's arithmetic (the two decoders are bit-identical).  A lane walking
+ * all K states alone took ~1200 cycles per step on a wave with nothing else
+ * to hide its latency; the quad form has a K-times shorter chain per lane. */
+template <int MODEL, int K>
+__device__ __forceinline__ void vs_sp_setup(const DevArgs &a, int64_t d, double *ldsd, SpLane<MODEL, K> &ln)
+{
+    const int lane = threadIdx.x & 63;
+    ln.j = lane & 3;
+    ln.js = min(ln.j, K - 1);
+    PairParams<MODEL, K> pp;
+    load_params<MODEL, K, true>(pp, a, d);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double v = pp.A[i][0];
+#pragma unroll
+        for (int jj = 1; jj < K; ++jj)
+            v = (ln.js == jj) ? pp.A[i][jj] : v;
+        ln.colA[i] = v;
+    }
+    ln.mu = ln.isig = ln.c0 = 0.0;
+    if constexpr (ModelTraits<MODEL>::kGauss) {
+        ln.mu = pp.mu[0];
+        ln.isig = pp.isig[0];
+        ln.c0 = pp.c0[0];
+#pragma unroll
+        for (int jj = 1; jj < K; ++jj) {
+            ln.mu = (ln.js == jj) ? pp.mu[jj] : ln.mu;
+            ln.isig = (ln.js == jj) ? pp.isig[jj] : ln.isig;
+            ln.c0 = (ln.js == jj) ? pp.c0[jj] : ln.c0;
+        }
+    }
+    ln.slab = ldsd + lane;
+    ln.arow = ldsd + (size_t)a.L * 64 + lane;
+    if constexpr (ModelTraits<MODEL>::kDiscrete) {
+        double *col = ldsd + lane;
+        for (int l = 0; l < a.L; ++l)
+            col[l * 64] = dev_cr_log(draw2<K>(a.phi_k, a, d, ln.js, l, K));
+    }
+    if constexpr (ModelTraits<MODEL>::kTayal) {
+        double *rows = ldsd + (size_t)a.L * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                rows[(r * K + i) * 64] = tayal_pred(r + 1, ln.js) ? ln.colA[i] : -0.0;
+    }
+}
+
+/* Steps [t0, t1) from the quad's delta (FIRST: t0 = 0, the model's first row).
+ * The emission column entry and the masked log A row of step t+1 are read
+ * while step t computes, so the per-step chain is the DPP broadcast, two adds
+ * and the max. */
+template <int MODEL, int K, bool FIRST>
+__device__ __forceinline__ void vs_sp_steps(const DevArgs &a, const SpLane<MODEL, K> &ln, const SeriesPtrs &sp,
+                                            int t0, int t1, double (&D)[K])
+{
+    constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
+    constexpr int C = 16;
+    double dl = D[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k)
+        dl = (ln.js == k) ? D[k] : dl;
+    Obs cur[C], nxt[C];
+    load_chunk<MODEL, C, VAUX>(cur, sp, t0);
+    double le = sp_emit<MODEL, K>(ln, cur[0], a.L);
+    double ar[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        ar[i] = 0.0;
+    if constexpr (ModelTraits<MODEL>::kTayal)
+        sp_arow<MODEL, K>(ln, cur[0].aux, ar);
+    for (int tb = t0; tb < t1; tb += C) {
+        load_chunk<MODEL, C, VAUX>(nxt, sp, tb + C);
+#pragma unroll
+        for (int u = 0; u < C; ++u) {
+            const int t = tb + u;
+            const Obs &on1 = (u + 1 < C) ? cur[u + 1 < C ? u + 1 : 0] : nxt[0];
+            const double lnx = sp_emit<MODEL, K>(ln, on1, a.L);
+            double arx[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                arx[i] = 0.0;
+            if constexpr (ModelTraits<MODEL>::kTayal)
+                sp_arow<MODEL, K>(ln, on1.aux, arx);
+            if (t < t1) {
+                if (FIRST && t == 0) { /* Q3: only column K of delta_tk[1] is written */
+                    dl = (ln.js == K - 1) ? le : dev_nan();
+                } else {
+                    double d[K];
+                    quad_gather<K>(dl, d);
+                    double best = dev_ninf();
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        double cand;
+                        if constexpr (ModelTraits<MODEL>::kTayal)
+                            cand = (d[i] + le) + ar[i]; /* (delta + log phi) [+ log A] */
+                        else
+                            cand = (d[i] + ln.colA[i]) + le; /* (delta + log A) + emission */
+                        best = fmax(best, cand);
+                    }
+                    dl = best;
+                }
+            }
+            le = lnx;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                ar[i] = arx[i];
+        }
+#pragma unroll
+        for (int u = 0; u < C; ++u)
+            cur[u] = nxt[u];
+    }
+    quad_gather<K>(dl, D);
+}
+
+/* LDS of the scans: the state-parallel columns (log phi, Tayal masked log A rows). */
+template <int MODEL, int K>
+constexpr size_t vs_sp_lds(int L)
+{
+    return ((ModelTraits<MODEL>::kDiscrete ? (size_t)L : 0) + (ModelTraits<MODEL>::kTayal ? (size_t)3 * K : 0)) *
+           64 * sizeof(double);
+}
+
+/* One wave per pair: chunk 0 exactly (row 1 of vs_d), then the approximate
+ * scan over the approximate chunk products: k_c = binade of the largest
+ * finite delta entering chunk c. */
 template <int MODEL, int K>
 __global__ void __launch_bounds__(64) vs_scan0_kernel(const DevArgs a)
 {
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
-    HIP_DYNAMIC_SHARED(double2, lds)
-    const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (p >= a.P)
-        return;
+    HIP_DYNAMIC_SHARED(double, ldsd)
+    const int64_t p = blockIdx.x;
+    const bool l0 = threadIdx.x == 0;
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
     const int ncp = (Tp + kVsChunk - 1) / kVsChunk;
-    double2 *slab = lds + threadIdx.x;
-    PairParams<MODEL, K> pp;
-    load_params<MODEL, K, true>(pp, a, d);
-    if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, true>(slab, a, d);
-    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, n);
+    SpLane<MODEL, K> ln;
+    vs_sp_setup<MODEL, K>(a, d, ldsd, ln);
+    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, vs_vector_index(n));
+    double *blk = ldsd + vs_sp_lds<MODEL, K>(a.L) / sizeof(double);
+    VsBlock<K> nxt;
+    vs_fetch<K>(a, p, 1, ncp, nxt);
     double dl[K];
-    vs_chunk0<MODEL, K>(a, pp, slab, sp, min(kVsChunk, Tp), dl, [](int, const int (&)[K]) {});
-    vs_store_d<K>(a, p, 1, dl);
-    for (int c = 1; c < ncp; ++c) {
-        const double hi = vs_hi<K>(dl);
-        a.vs_k[p + a.P * (int64_t)c] = (hi > dev_ninf() && hi != 0.0) ? vs_binade(hi) : kVsNoGrid;
-        double nx[K];
-        vs_apply<K>(a, p, c, dl, nx);
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            dl[k] = nx[k];
+    for (int k = 0; k < K; ++k)
+        dl[k] = 0.0;
+    vs_sp_steps<MODEL, K, true>(a, ln, sp, 0, min(kVsChunk, Tp), dl);
+    if (l0)
+        vs_store_d<K>(a, p, 1, dl);
+    for (int cb = 1; cb < ncp; cb += 64) {
+        vs_stage<K>(nxt, blk);
+        __syncthreads();
+        vs_fetch<K>(a, p, cb + 64, ncp, nxt);
+        for (int i = 0; i < 64 && cb + i < ncp; ++i) {
+            const double hi = vs_hi<K>(dl);
+            if (l0)
+                a.vs_k[p + a.P * (int64_t)(cb + i)] = (hi > dev_ninf() && hi != 0.0) ? vs_binade(hi) : kVsNoGrid;
+            double nx[K];
+            (void)vs_apply_lds<K>(blk, i, dl, nx);
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                dl[k] = nx[k];
+        }
+        __syncthreads();
     }
 }
 
-/* One wave per pair (lane 0 works): the exact scan over the grid products,
- * chunks failing the checks decoded step by step.  Rows 2..ncp of vs_d. */
+/* One wave per pair: the exact scan over the grid products, chunks failing
+ * the checks decoded step by step.  Rows 2..ncp of vs_d. */
 template <int MODEL, int K>
 __global__ void __launch_bounds__(64) vs_scan1_kernel(const DevArgs a)
 {
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
-    HIP_DYNAMIC_SHARED(double2, lds)
-    if (threadIdx.x != 0)
-        return;
+    HIP_DYNAMIC_SHARED(double, ldsd)
     const int64_t p = blockIdx.x;
+    const bool l0 = threadIdx.x == 0;
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
     const int ncp = (Tp + kVsChunk - 1) / kVsChunk;
     if (ncp < 2)
         return;
-    double2 *slab = lds;
-    PairParams<MODEL, K> pp;
-    load_params<MODEL, K, true>(pp, a, d);
-    if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, true>(slab, a, d);
-    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, n);
+    SpLane<MODEL, K> ln;
+    vs_sp_setup<MODEL, K>(a, d, ldsd, ln);
+    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, vs_vector_index(n));
+    double *blk = ldsd + vs_sp_lds<MODEL, K>(a.L) / sizeof(double);
+    VsBlock<K> nxt;
+    vs_fetch<K>(a, p, 1, ncp, nxt);
     double dl[K];
     vs_load_d<K>(a, p, 1, dl);
-    for (int c = 1; c < ncp; ++c) {
-        const int32_t kc = a.vs_k[p + a.P * (int64_t)c];
-        const double hi = vs_hi<K>(dl);
-        bool ok = kc != kVsNoGrid && !(kc & kVsTie) && hi > dev_ninf() && hi != 0.0 && vs_binade(hi) == kc;
-        double nx[K];
-        if (ok) {
-            vs_apply<K>(a, p, c, dl, nx);
+    for (int cb = 1; cb < ncp; cb += 64) {
+        vs_stage<K>(nxt, blk);
+        __syncthreads();
+        vs_fetch<K>(a, p, cb + 64, ncp, nxt);
+        for (int i = 0; i < 64 && cb + i < ncp; ++i) {
+            const int c = cb + i;
+            const double hi = vs_hi<K>(dl);
+            double nx[K];
+            const int32_t kc = vs_apply_lds<K>(blk, i, dl, nx);
+            const int32_t kb = (kc >= 0) ? (kc & ~kVsTie) : kc; /* ties are exact through M0 / M1 */
+            bool ok = kc != kVsNoGrid && hi > dev_ninf() && hi != 0.0 && vs_binade(hi) == kb;
             /* every finite exit value inside the binade, 2^-40 of its width clear of the edge */
-            const double edge = -ldexp(1.0 - 0x1p-40, kc + 1);
+            const double edge = -ldexp(1.0 - 0x1p-40, kb + 1);
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 ok = ok && (nx[k] == dev_ninf() || nx[k] > edge);
-        }
-        if (ok) {
+            if (ok) {
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                dl[k] = nx[k];
-        } else {
-            const int t0 = c * kVsChunk;
-            vs_chunk<MODEL, K>(a, pp, slab, sp, t0, min(t0 + kVsChunk, Tp), dl, [](int, const int (&)[K]) {});
+                for (int k = 0; k < K; ++k)
+                    dl[k] = nx[k];
+            } else {
+                const int t0 = c * kVsChunk;
+                vs_sp_steps<MODEL, K, false>(a, ln, sp, t0, min(t0 + kVsChunk, Tp), dl);
+                if (l0)
+                    a.vs_k[p + a.P * (int64_t)c] = kVsSeq;
+            }
+            if (l0)
+                vs_store_d<K>(a, p, c + 1, dl);
         }
-        vs_store_d<K>(a, p, c + 1, dl);
+        __syncthreads();
     }
 }
 
@@ -581,13 +980,16 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
     const int64_t lanes = a.P * a.vs_nc;
     const dim3 gc((unsigned)((lanes + kBlock - 1) / kBlock)), bc(kBlock);
     const dim3 gp((unsigned)((a.P + 63) / 64)), b64(64);
-    const size_t lds_c = slab * (kBlock / 64), lds_p = slab;
+    const size_t lds_c = slab * (kBlock / 64), lds_s = vs_sp_lds<MODEL, K>(a.L) + 64 * kVsRow * sizeof(double);
     hipError_t e = hipMemsetAsync(a.vs_fail, 0, (size_t)a.P * sizeof(int32_t), st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, false>), gc, bc, lds_c, st, a);
-        hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K>), gp, b64, lds_p, st, a);
+        hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, true>), gc, bc, lds_c, st, a);
-        hipLaunchKernelGGL((vs_scan1_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_p, st, a);
+        if (ModelTraits<MODEL>::kGauss) /* discrete models resolve their ties inside the grid pass */
+            hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3((unsigned)((2 * lanes + kBlock - 1) / kBlock)), bc,
+                               lds_c, st, a);
+        hipLaunchKernelGGL((vs_scan1_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_replay_kernel<MODEL, K>), gc, bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_stitch_kernel<K>), gp, b64, 0, st, a);
         if ((a.outputs & HHMM_OUT_ZSTAR) && a.zstar)
@@ -599,6 +1001,51 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
                             (ModelTraits<MODEL>::kTayal ? (size_t)3 * K : 0)) * 64 * sizeof(double);
         hipLaunchKernelGGL((viterbi_sp_kernel<MODEL, K>), dim3((unsigned)((4 * a.P + 63) / 64)), dim3(64), lds, st, r);
         e = hipGetLastError();
+    }
+    if (e == hipSuccess && getenv("HHMM_PROBE_VS_STATS")) {
+        /* probe: chunks the exact scan decoded step by step, and replay failures */
+        std::vector<int32_t> k((size_t)a.P * a.vs_nc), f((size_t)a.P);
+        e = hipStreamSynchronize(st);
+        if (e == hipSuccess)
+            e = hipMemcpy(k.data(), a.vs_k, k.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess)
+            e = hipMemcpy(f.data(), a.vs_fail, f.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+        int64_t seq = 0, fail = 0, worst = 0, first = -1;
+        for (int64_t q = 0; q < a.P; ++q) {
+            int64_t n = 0;
+            for (int c = 1; c < a.vs_nc; ++c)
+                if (k[(size_t)q + (size_t)a.P * c] == kVsSeq) {
+                    ++n;
+                    if (q == 0 && first < 0)
+                        first = c;
+                }
+            seq += n;
+            worst = std::max(worst, n);
+        }
+        for (int32_t v : f)
+            fail += v != 0;
+        fprintf(stderr,
+                "[vscan] pairs %lld chunks/pair %d sequential chunks %lld (%.2f per pair, worst pair %lld) "
+                "replay failures %lld; pair 0:",
+                (long long)a.P, a.vs_nc, (long long)seq, (double)seq / (double)a.P, (long long)worst, (long long)fail);
+        for (int c = 1; c < a.vs_nc; ++c)
+            if (k[(size_t)a.P * c] == kVsSeq)
+                fprintf(stderr, " %d", c);
+        int64_t wq = 0, wn = -1;
+        for (int64_t q = 0; q < a.P; ++q) {
+            int64_t n = 0;
+            for (int c = 1; c < a.vs_nc; ++c)
+                n += k[(size_t)q + (size_t)a.P * c] == kVsSeq;
+            if (n > wn) {
+                wn = n;
+                wq = q;
+            }
+        }
+        fprintf(stderr, "; worst pair %lld:", (long long)wq);
+        for (int c = 1; c < a.vs_nc; ++c)
+            if (k[(size_t)wq + (size_t)a.P * c] == kVsSeq)
+                fprintf(stderr, " %d", c);
+        fprintf(stderr, "\n");
     }
     if (e != hipSuccess) {
         set_error("T-parallel Viterbi launch: %s", hipGetErrorString(e));

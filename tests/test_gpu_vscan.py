@@ -88,3 +88,39 @@ def test_vscan_agrees_with_sequential(engine):
     assert np.array_equal(a["zstar_t"], b["zstar_t"])
     assert np.array_equal(a["logp_zstar"].view(np.int64), b["logp_zstar"].view(np.int64))
     assert np.array_equal(a["pair_status"], b["pair_status"])
+
+
+def _tie_values(oracle, k, count, seed=5):
+    """Probabilities whose correctly rounded log is an odd multiple of 2^(k-53): a
+    rounding tie on the grid of binade k (the parity-dependent products of
+    hhmm_vscan.h's vs_prod_tie_kernel)."""
+    g = np.random.Generator(np.random.Philox(seed))
+    found = []
+    while len(found) < count:
+        x = g.uniform(0.05, 0.9, 400_000)
+        s = oracle.log_array(x, "cr") * 2.0 ** (53 - k)
+        ok = (s == np.round(s)) & (np.abs(np.fmod(s, 2.0)) == 1.0)
+        found.extend(x[ok][: count - len(found)])
+    return np.array(found)
+
+
+@pytest.mark.parametrize("model", ["hmm-multinom", "hhmm-tayal2009"])
+def test_vscan_rounding_ties(engine, oracle, model):
+    """Emission and transition log-probabilities that tie on the grid of the binades
+    |delta| crosses (k = 11, 12, 13): those chunks take the even / odd entry-value
+    products, still bit-exact."""
+    T = 20_000
+    if model == "hmm-multinom":
+        data, draws = synth.hmm_multinom(N=1, S=4, T=T, K=4, L=9)
+        phi = draws["phi_k"]
+        for s, k in enumerate((11, 12, 13, 13)):
+            v = _tie_values(oracle, k, 3, seed=5 + s)
+            phi[s, 0, :3] = v
+            draws["A_ij"][s, 1, 2] = v[0]
+    else:
+        data, draws = synth.tayal(N=1, S=4, T=T)
+        phi = draws["phi_k"]
+        for s, k in enumerate((11, 12, 13, 13)):
+            v = _tie_values(oracle, k, 4, seed=9 + s)
+            phi[s, :, 4] = v
+    run(engine, oracle, model, data, draws)
