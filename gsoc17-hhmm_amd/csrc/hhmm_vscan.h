@@ -69,16 +69,6 @@ __device__ __forceinline__ double vs_grid(double a, double iu, double u, bool &t
 /* Binade exponent k of a finite nonzero double: |x| in [2^k, 2^(k+1)). */
 __device__ __forceinline__ int vs_binade(double x) { return __builtin_amdgcn_frexp_exp(x) - 1; }
 
-/* Candidate of (i -> j) relative to delta_{t-1}(i), the model's two terms. */
-template <int MODEL>
-__device__ __forceinline__ double vs_rel(double la, double le, bool on)
-{
-    if constexpr (ModelTraits<MODEL>::kTayal)
-        return on ? le + la : le; /* (delta + log phi) [+ log A] (hhmm-tayal2009.stan:143-146) */
-    else
-        return la + le; /* (delta + log A) + emission (hmm.stan:111) */
-}
-
 /* lane = (pair, chunk): p fastest so a wave's lanes read one time row. */
 struct VsLane {
     int64_t p, n, d;
@@ -343,13 +333,25 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
 #pragma unroll
         for (int j = 0; j < K; ++j)
             M[r][j] = (r == j) ? 0.0 : dev_ninf();
+    if constexpr (GRID && ModelTraits<MODEL>::kDiscrete) {
+        /* the emission table on the grid, once (no tie: checked above) */
+        for (int l = 0; l < a.L; ++l)
+#pragma unroll
+            for (int kp = 0; kp < KP; ++kp) {
+                double2 &e = slab[(l * KP + kp) * 64];
+                e = make_double2(vs_grid(e.x, iu, u, tie), vs_grid(e.y, iu, u, tie));
+            }
+    }
+    /* M'[r][j] = max_i (M[r][i] + log A[i][j]) + log phi_j (the grid sums are
+     * exact, so the terms may be regrouped); Tayal steps whose mask is off for
+     * j take max_i M[r][i] + log phi_j, the row max shared by those columns */
     vs_steps<MODEL, VAUX>(sp, v.t0, v.t1, [&](int, const Obs &o) {
         double le[K];
         emit_log<MODEL, K>(pp, slab, a.L, o, le);
         bool on[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            if constexpr (GRID)
+            if constexpr (GRID && ModelTraits<MODEL>::kGauss)
                 le[j] = vs_grid(le[j], iu, u, tie);
             on[j] = true;
             if constexpr (ModelTraits<MODEL>::kTayal)
@@ -358,13 +360,24 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
 #pragma unroll
         for (int r = 0; r < K; ++r) {
             double nm[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                double best = M[r][0] + vs_rel<MODEL>(pp.A[0][j], le[j], on[j]);
+            double rm = M[r][0];
+            if constexpr (ModelTraits<MODEL>::kTayal) {
 #pragma unroll
                 for (int i = 1; i < K; ++i)
-                    best = fmax(best, M[r][i] + vs_rel<MODEL>(pp.A[i][j], le[j], on[j]));
-                nm[j] = best;
+                    rm = fmax(rm, M[r][i]);
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                double best;
+                if (ModelTraits<MODEL>::kTayal && !on[j]) {
+                    best = rm;
+                } else {
+                    best = M[r][0] + pp.A[0][j];
+#pragma unroll
+                    for (int i = 1; i < K; ++i)
+                        best = fmax(best, M[r][i] + pp.A[i][j]);
+                }
+                nm[j] = best + le[j];
             }
 #pragma unroll
             for (int j = 0; j < K; ++j)
