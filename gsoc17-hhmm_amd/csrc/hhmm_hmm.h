@@ -1427,36 +1427,6 @@ __global__ void __launch_bounds__(kBlock) fbv_kernel(const DevArgs a)
  * four lanes on the gathered delta_T; identical duplicate stores) and the
  * backtrack are shared. */
 
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-
-/* d[i] = v of lane i of this lane's quad. */
-template <int K>
-__device__ __forceinline__ void quad_gather(double v, double (&d)[K])
-{
-    d[0] = dpp_f64<0x00>(v);
-    if constexpr (K > 1)
-        d[1] = dpp_f64<0x55>(v);
-    if constexpr (K > 2)
-        d[2] = dpp_f64<0xAA>(v);
-    if constexpr (K > 3)
-        d[3] = dpp_f64<0xFF>(v);
-}
-
-/* OR of w over this lane's quad. */
-__device__ __forceinline__ uint32_t quad_or(uint32_t w)
-{
-    w |= (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false); /* quad_perm(1,0,3,2) */
-    w |= (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0x4E, 0xF, 0xF, false); /* quad_perm(2,3,0,1) */
-    return w;
-}
-
 /* Steps per prefetched observation chunk: a multiple of the word length, two
  * Viterbi chunks deep so the (latency-bound) loads run far ahead. */
 constexpr int vit_sp_chunk(int K) { return 2 * vit_chunk(K); }

@@ -247,7 +247,12 @@ __device__ __forceinline__ void io_load(const DevArgs &a, uint32_t n, int t, dou
     }
 }
 
-template <int FAM, int K, int MMAX, int MATH>
+/* HOT: the request asks for nothing outside kIoHot, so the other outputs'
+ * code (and their pointers, which would otherwise stay live in SGPRs through
+ * the loop and spill) is compiled out. */
+constexpr uint32_t kIoHot = HHMM_OUT_LOGLIK | HHMM_OUT_GAMMA | HHMM_OUT_ALPHA | HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+
+template <int FAM, int K, int MMAX, int MATH, bool HOT = false>
 __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 {
     HIP_DYNAMIC_SHARED(double2, lds)
@@ -261,7 +266,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
     const int M = a.M, L = a.L;
-    const uint32_t out = a.outputs;
+    const uint32_t out = HOT ? (a.outputs & kIoHot) : a.outputs;
     const bool want_vit = MATH == IO_CR && (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR));
     const bool want_ffbs = MATH == IO_DET && (out & HHMM_OUT_FFBS) && a.z_ffbs;
     const bool fixed_init = (a.model == HHMM_MODEL_IOHMM_HMIX); /* iohmm-hmix.stan:166-167 */
@@ -521,24 +526,239 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 #ifndef HHMM_IO_REG_WAVES
 #define HHMM_IO_REG_WAVES 2
 #endif
-template <int K, int MMAX, int MATH>
+template <int K, int MMAX, int MATH, bool HOT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HHMM_IO_REG_WAVES))) iohmm_reg_kernel(const DevArgs a)
 {
-    iohmm_sweep<IO_REG, K, MMAX, MATH>(a);
+    iohmm_sweep<IO_REG, K, MMAX, MATH, HOT>(a);
 }
 
-template <int K, int MMAX, int MATH>
+template <int K, int MMAX, int MATH, bool HOT>
 __global__ void __launch_bounds__(kBlock) iohmm_mix_kernel(const DevArgs a)
 {
-    iohmm_sweep<IO_MIX, K, MMAX, MATH>(a);
+    iohmm_sweep<IO_MIX, K, MMAX, MATH, HOT>(a);
+}
+
+/* ---- state-parallel sweep (few pairs; C4) ------------------------------ *
+ * One lane per (pair, state j), a pair's K <= 4 states in one lane quad.  A
+ * step's transcendentals are per state -- the mixture log_sum_exp of state j,
+ * its softmax exp, its filter exp -- so each lane evaluates only its own
+ * state's, and the quad exchanges the K-vectors it needs by DPP broadcasts:
+ * softmax max / sum, the emission max, A_t and e_t.  Everything that mixes
+ * states (the softmax sum, the forward dot, the FFBS category) is then
+ * evaluated by every lane of the quad from the gathered vectors in the lane
+ * sweep's order, so outputs and draws are bit-identical to iohmm_sweep.  At
+ * C4 (65,536 pairs) lane-per-pair runs one wave per SIMD, each step a
+ * latency-bound chain of ~24 exps; here it runs four with a quarter of the
+ * chain.  Profile: loglik, alpha / gamma (= alpha, Q5) and FFBS. */
+template <int FAM, int K, int MMAX, int MATH, int LM>
+__device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
+{
+    static_assert(K >= 2 && K <= 4, "one lane quad per pair");
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = (g >> 2) < a.P;
+    const int64_t p = min(g >> 2, a.P - 1);
+    const int j = (int)(g & 3);
+    const int js = min(j, K - 1);
+    const bool owns = live && j < K;
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int M = a.M, L = a.L;
+    const uint32_t out = a.outputs;
+    const bool want_ffbs = MATH == IO_DET && (out & HHMM_OUT_FFBS) && a.z_ffbs;
+
+    /* ---- parameters: p_1k whole, state js's rows and tables ---- */
+    double pk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        pk[k] = a.p_1k[d + a.S * k];
+    double w[MMAX], b[MMAX];
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) {
+        w[m] = (m < M) ? a.w_km[d + a.S * ((int64_t)js + (int64_t)K * m)] : 0.0;
+        b[m] = 0.0;
+        if constexpr (FAM == IO_REG)
+            b[m] = (m < M) ? a.b_km[d + a.S * ((int64_t)js + (int64_t)K * m)] : 0.0;
+    }
+    double isig = 0.0, c0 = 0.0;
+    double mu[LM], is[LM], ll[LM], lc[LM];
+    if constexpr (FAM == IO_REG) {
+        const double sg = a.s_k[d + a.S * js];
+        isig = 1.0 / sg;
+        c0 = HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(sg);
+    } else {
+#pragma unroll
+        for (int l = 0; l < LM; ++l) {
+            mu[l] = is[l] = ll[l] = lc[l] = 0.0;
+            if (l < L) {
+                const int64_t ix = d + a.S * ((int64_t)js + (int64_t)K * l);
+                const double sg = a.s_kl[ix];
+                mu[l] = a.mu_kl[ix];
+                is[l] = 1.0 / sg;
+                ll[l] = io_log<MATH>(a.lambda_kl[ix]);
+                lc[l] = HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(sg);
+            }
+        }
+    }
+    const int Tw_max = wave_max(Tp);
+
+    double f[K];
+    double lsc = 0.0;
+    int ex = 0;
+    double vprev[K];
+    double uprev = 0.5;
+    double x, xn;
+    double u[MMAX], un[MMAX];
+    io_load<MMAX>(a, (uint32_t)n, 0, x, u);
+    for (int t = 0; t < Tw_max; ++t) {
+        io_load<MMAX>(a, (uint32_t)n, t + 1, xn, un);
+        if (t < Tp) {
+            /* emission of state js (io_emission's arithmetic) */
+            double o;
+            if constexpr (FAM == IO_REG) {
+                const double mv = sse_dot<MMAX>(u, b, M);
+                const double z = (x - mv) * isig;
+                const double z2 = z * z;
+                o = c0 + (-0.5 * z2);
+            } else {
+                double acc[LM];
+                double mx = dev_ninf();
+#pragma unroll
+                for (int l = 0; l < LM; ++l) {
+                    if (l < L) {
+                        const double z = (x - mu[l]) * is[l];
+                        const double z2 = z * z;
+                        acc[l] = ll[l] + (lc[l] + (-0.5 * z2));
+                        if (acc[l] > mx)
+                            mx = acc[l];
+                    }
+                }
+                double sum = 0.0;
+#pragma unroll
+                for (int l = 0; l < LM; ++l)
+                    if (l < L && acc[l] != dev_ninf())
+                        sum += io_exp<MATH>(acc[l] - mx);
+                o = mx + io_log<MATH>(sum);
+            }
+            /* transition A_t = softmax(u_t' w) (stan_softmax's order); t = 0: p_1k */
+            double AA[K];
+            if (t == 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    AA[k] = pk[k];
+            } else {
+                const double v = sse_dot<MMAX>(u, w, M);
+                double vv[K];
+                quad_gather<K>(v, vv);
+                double mx = vv[0];
+#pragma unroll
+                for (int i = 1; i < K; ++i)
+                    if (vv[i] > mx)
+                        mx = vv[i];
+                const double th = io_exp<MATH>(v - mx);
+                double tt[K];
+                quad_gather<K>(th, tt);
+                double sum = 0.0;
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    sum += tt[i];
+                quad_gather<K>(th / sum, AA);
+            }
+            /* e_t = exp(o - max o) */
+            double oo[K];
+            quad_gather<K>(o, oo);
+            double m = oo[0];
+#pragma unroll
+            for (int k = 1; k < K; ++k)
+                m = fmax(m, oo[k]);
+            if (m == dev_ninf())
+                m = 0.0;
+            double ee[K];
+            quad_gather<K>(MATH == IO_DET ? hhmm_det_exp(o - m) : exp(o - m), ee);
+            if (want_ffbs) {
+                if (t > 0) {
+                    double wv[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        wv[k] = vprev[k] * AA[k];
+                    const int z = ffbs_cat<K>(wv, uprev) + 1;
+                    if (live && j == 0)
+                        at(a.z_ffbs + a.P * (int64_t)(t - 1), (uint32_t)p * 4u) = z;
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    vprev[k] = (t == 0) ? pk[k] * ee[k] : ee[k];
+                uprev = at(a.ffbs_u + a.P * (int64_t)t, (uint32_t)p * 8u);
+            }
+            /* forward: f_t = e_t * sum_i f_{t-1}(i) A_t(i) */
+            if (t == 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    f[k] = pk[k] * ee[k];
+            } else {
+                double sv = f[0] * AA[0];
+#pragma unroll
+                for (int i = 1; i < K; ++i)
+                    sv = fma(f[i], AA[i], sv);
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    f[k] = ee[k] * sv;
+            }
+            lsc += m;
+            renorm<K>(f, ex);
+            if ((out & (HHMM_OUT_ALPHA | HHMM_OUT_GAMMA)) && owns) {
+                double fj = f[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k)
+                    fj = (js == k) ? f[k] : fj;
+                const double v = fj * (1.0 / vsum<K>(f));
+                if ((out & HHMM_OUT_ALPHA) && a.alpha)
+                    put_out(a.alpha + a.P * ((int64_t)t + (int64_t)a.Tout * js), (uint32_t)p * 8u, v);
+                if ((out & HHMM_OUT_GAMMA) && a.gamma)
+                    put_out(a.gamma + a.P * ((int64_t)t + (int64_t)a.Tout * js), (uint32_t)p * 8u, v);
+            }
+        }
+        x = xn;
+#pragma unroll
+        for (int m2 = 0; m2 < MMAX; ++m2)
+            u[m2] = un[m2];
+    }
+    if (live && j == 0) {
+        if (want_ffbs)
+            at(a.z_ffbs + a.P * (int64_t)(Tp - 1), (uint32_t)p * 4u) = ffbs_cat<K>(vprev, uprev) + 1;
+        if ((out & HHMM_OUT_LOGLIK) && a.loglik)
+            a.loglik[p] = log(vsum<K>(f)) + (lsc + kLn2 * ex);
+    }
+}
+
+#ifndef HHMM_IO_SP_WAVES
+#define HHMM_IO_SP_WAVES 1
+#endif
+template <int FAM, int K, int MMAX, int MATH, int LM>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HHMM_IO_SP_WAVES)))
+iohmm_sp_kernel(const DevArgs a)
+{
+    if constexpr (K >= 2 && K <= 4)
+        iohmm_sp_sweep<FAM, K, MMAX, MATH, LM>(a);
+}
+
+/* The state-parallel sweep's profile and range: K = 2..4, outputs within
+ * loglik / alpha / gamma / FFBS, a batch that leaves lane-per-pair below two
+ * waves per SIMD (HHMM_FLAG_VIT_LANES / _VIT_STATES force one layout). */
+static bool io_states(const DevArgs &a)
+{
+    const uint32_t sp_out = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_GAMMA | HHMM_OUT_FFBS;
+    if (a.K < 2 || a.K > 4 || (a.outputs & ~sp_out) || (a.flags & HHMM_FLAG_VIT_LANES))
+        return false;
+    return (a.flags & HHMM_FLAG_VIT_STATES) || a.P < 131072;
 }
 
 /* ------------------------------------------------------------------ */
 /* Host-side launch                                                      */
 /* ------------------------------------------------------------------ */
 
-template <int FAM, int K, int MMAX, int MATH>
-static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
+template <int FAM, int K, int MMAX, int MATH, bool HOT>
+static hhmm_status launch_io5(const DevArgs &a, hipStream_t st)
 {
     const size_t per_wave = (FAM == IO_MIX) ? (size_t)K * a.L * 2 * 64 * sizeof(double2) : 0;
     int waves = 4;
@@ -551,9 +771,9 @@ static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
     const int threads = 64 * waves;
     const dim3 grid((unsigned)((a.P + threads - 1) / threads));
     if constexpr (FAM == IO_REG)
-        hipLaunchKernelGGL((iohmm_reg_kernel<K, MMAX, MATH>), grid, dim3(threads), per_wave * waves, st, a);
+        hipLaunchKernelGGL((iohmm_reg_kernel<K, MMAX, MATH, HOT>), grid, dim3(threads), per_wave * waves, st, a);
     else
-        hipLaunchKernelGGL((iohmm_mix_kernel<K, MMAX, MATH>), grid, dim3(threads), per_wave * waves, st, a);
+        hipLaunchKernelGGL((iohmm_mix_kernel<K, MMAX, MATH, HOT>), grid, dim3(threads), per_wave * waves, st, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("iohmm kernel launch: %s", hipGetErrorString(e));
@@ -562,9 +782,44 @@ static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
     return HHMM_OK;
 }
 
+/* The hot profile is instantiated for the Viterbi sweep at K <= 4 (C3's). */
+template <int FAM, int K, int MMAX, int MATH>
+static hhmm_status launch_io4(const DevArgs &a, hipStream_t st)
+{
+    if constexpr (MATH == IO_CR && K <= 4) {
+        if (!(a.outputs & ~kIoHot))
+            return launch_io5<FAM, K, MMAX, MATH, true>(a, st);
+    }
+    return launch_io5<FAM, K, MMAX, MATH, false>(a, st);
+}
+
+template <int FAM, int K, int MMAX, int MATH>
+static hhmm_status launch_io_sp(const DevArgs &a, hipStream_t st)
+{
+    const int64_t lanes = 4 * a.P;
+    const dim3 grid((unsigned)((lanes + kBlock - 1) / kBlock));
+    /* the mixture tables of a lane's state sit in registers: L <= 4 or <= 8 */
+    if (FAM == IO_REG)
+        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 1>), grid, dim3(kBlock), 0, st, a);
+    else if (a.L <= 4)
+        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 4>), grid, dim3(kBlock), 0, st, a);
+    else
+        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, kIoLmax>), grid, dim3(kBlock), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("iohmm state-parallel kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
 template <int FAM, int K, int MATH>
 static hhmm_status launch_io_m(const DevArgs &a, hipStream_t st)
 {
+    if constexpr (K >= 2 && K <= 4 && MATH != IO_CR) {
+        if (io_states(a))
+            return a.M <= 4 ? launch_io_sp<FAM, K, 4, MATH>(a, st) : launch_io_sp<FAM, K, 8, MATH>(a, st);
+    }
     return a.M <= 4 ? launch_io4<FAM, K, 4, MATH>(a, st) : launch_io4<FAM, K, 8, MATH>(a, st);
 }
 

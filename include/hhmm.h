@@ -185,9 +185,11 @@ typedef struct hhmm_draws {
  * joined back into it (the call's semantics are unchanged); this flag runs
  * both passes on the caller's stream, one after the other. */
 #define HHMM_FLAG_NO_FUSE (1u << 2)
-/* Viterbi decoding layout (HMM family, K = 2..4): by default batches below
- * 131072 pairs decode one lane per (pair, state), larger ones one lane per
- * pair; results are bit-identical either way.  These force one or the other. */
+/* Layout of the per-pair recursions at K = 2..4: by default batches below
+ * 131072 pairs run one lane per (pair, state), larger ones one lane per pair;
+ * results are bit-identical either way.  These force one or the other.  They
+ * apply to the HMM-family Viterbi and to the IOHMM sweep's loglik / alpha /
+ * gamma / FFBS profile. */
 #define HHMM_FLAG_VIT_LANES (1u << 3)
 #define HHMM_FLAG_VIT_STATES (1u << 4)
 /* hmm-multinom at K = 4 with gamma_tk (+ loglik) and zstar_t / logp_zstar in one
