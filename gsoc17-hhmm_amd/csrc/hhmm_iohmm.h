@@ -538,6 +538,36 @@ __global__ void __launch_bounds__(kBlock) iohmm_mix_kernel(const DevArgs a)
     iohmm_sweep<IO_MIX, K, MMAX, MATH, HOT>(a);
 }
 
+/* ffbs_cat with the quotients w_i / sum shared across the lane quad: lane
+ * js divides its own, the quad gathers them, and every lane runs the same
+ * cumulative comparison -- the same doubles as ffbs_cat's. */
+template <int K>
+__device__ __forceinline__ int ffbs_cat_quad(const double (&w)[K], int js, double u)
+{
+    double sum = w[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i)
+        sum = sum + w[i];
+    if (!(sum > 0.0) || !__builtin_isfinite(sum))
+        return -1;
+    double wj = w[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i)
+        wj = (js == i) ? w[i] : wj;
+    double q[K];
+    quad_gather<K>(wj / sum, q);
+    int b = 0;
+    double cum = q[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) {
+        if (b == i - 1 && u > cum) {
+            b = i;
+            cum = cum + q[i];
+        }
+    }
+    return b;
+}
+
 /* ---- state-parallel sweep (few pairs; C4) ------------------------------ *
  * One lane per (pair, state j), a pair's K <= 4 states in one lane quad.  A
  * step's transcendentals are per state -- the mixture log_sum_exp of state j,
@@ -549,7 +579,9 @@ __global__ void __launch_bounds__(kBlock) iohmm_mix_kernel(const DevArgs a)
  * sweep's order, so outputs and draws are bit-identical to iohmm_sweep.  At
  * C4 (65,536 pairs) lane-per-pair runs one wave per SIMD, each step a
  * latency-bound chain of ~24 exps; here it runs four with a quarter of the
- * chain.  Profile: loglik, alpha / gamma (= alpha, Q5) and FFBS. */
+ * chain.  The lane's mixture entries sit in its LDS column (registers held the
+ * kernel at three waves per SIMD).  Profile: loglik, alpha / gamma (= alpha,
+ * Q5) and FFBS. */
 template <int FAM, int K, int MMAX, int MATH, int LM>
 __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 {
@@ -581,7 +613,9 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
             b[m] = (m < M) ? a.b_km[d + a.S * ((int64_t)js + (int64_t)K * m)] : 0.0;
     }
     double isig = 0.0, c0 = 0.0;
-    double mu[LM], is[LM], ll[LM], lc[LM];
+    /* state js's mixture entries in the lane's LDS column: (mu, 1/s), (log lambda, C - log s) */
+    HIP_DYNAMIC_SHARED(double2, lds)
+    double2 *col = lds + (threadIdx.x >> 6) * (size_t)(2 * LM * 64) + (threadIdx.x & 63);
     if constexpr (FAM == IO_REG) {
         const double sg = a.s_k[d + a.S * js];
         isig = 1.0 / sg;
@@ -589,14 +623,12 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
     } else {
 #pragma unroll
         for (int l = 0; l < LM; ++l) {
-            mu[l] = is[l] = ll[l] = lc[l] = 0.0;
             if (l < L) {
                 const int64_t ix = d + a.S * ((int64_t)js + (int64_t)K * l);
                 const double sg = a.s_kl[ix];
-                mu[l] = a.mu_kl[ix];
-                is[l] = 1.0 / sg;
-                ll[l] = io_log<MATH>(a.lambda_kl[ix]);
-                lc[l] = HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(sg);
+                col[(2 * l) * 64] = make_double2(a.mu_kl[ix], 1.0 / sg);
+                col[(2 * l + 1) * 64] =
+                    make_double2(io_log<MATH>(a.lambda_kl[ix]), HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(sg));
             }
         }
     }
@@ -626,9 +658,11 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 #pragma unroll
                 for (int l = 0; l < LM; ++l) {
                     if (l < L) {
-                        const double z = (x - mu[l]) * is[l];
+                        const double2 ms = col[(2 * l) * 64];
+                        const double2 lg = col[(2 * l + 1) * 64];
+                        const double z = (x - ms.x) * ms.y;
                         const double z2 = z * z;
-                        acc[l] = ll[l] + (lc[l] + (-0.5 * z2));
+                        acc[l] = lg.x + (lg.y + (-0.5 * z2));
                         if (acc[l] > mx)
                             mx = acc[l];
                     }
@@ -681,7 +715,7 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 #pragma unroll
                     for (int k = 0; k < K; ++k)
                         wv[k] = vprev[k] * AA[k];
-                    const int z = ffbs_cat<K>(wv, uprev) + 1;
+                    const int z = ffbs_cat_quad<K>(wv, js, uprev) + 1;
                     if (live && j == 0)
                         at(a.z_ffbs + a.P * (int64_t)(t - 1), (uint32_t)p * 4u) = z;
                 }
@@ -731,8 +765,10 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
     }
 }
 
+/* Capped at four waves per SIMD (128 registers, a 12-register spill): C4 45.9
+ * against 47.5 ms uncapped (138 registers, three waves). */
 #ifndef HHMM_IO_SP_WAVES
-#define HHMM_IO_SP_WAVES 1
+#define HHMM_IO_SP_WAVES 4
 #endif
 template <int FAM, int K, int MMAX, int MATH, int LM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(HHMM_IO_SP_WAVES)))
@@ -799,12 +835,13 @@ static hhmm_status launch_io_sp(const DevArgs &a, hipStream_t st)
     const int64_t lanes = 4 * a.P;
     const dim3 grid((unsigned)((lanes + kBlock - 1) / kBlock));
     /* the mixture tables of a lane's state sit in registers: L <= 4 or <= 8 */
+    const size_t lds = (FAM == IO_MIX) ? (size_t)(kBlock / 64) * 2 * (a.L <= 4 ? 4 : kIoLmax) * 64 * sizeof(double2) : 0;
     if (FAM == IO_REG)
         hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 1>), grid, dim3(kBlock), 0, st, a);
     else if (a.L <= 4)
-        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 4>), grid, dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 4>), grid, dim3(kBlock), lds, st, a);
     else
-        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, kIoLmax>), grid, dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, kIoLmax>), grid, dim3(kBlock), lds, st, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("iohmm state-parallel kernel launch: %s", hipGetErrorString(e));
