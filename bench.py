@@ -133,6 +133,7 @@ class DeviceRun:
         self.reqs = {}
         self._ws = {}
         for name, outs, flags in (("step", hot, 0), ("fused", hot, _abi.FLAG_FUSED),
+                                  ("split", hot, _abi.FLAG_FB_SPLIT),
                                   ("fb", ["loglik", "gamma_tk"], 0), ("viterbi", ["zstar_t", "logp_zstar"], 0)):
             r = _abi.Request()
             r.abi_version = _abi.ABI_VERSION
@@ -408,9 +409,9 @@ WORKLOADS = {
 }
 
 
-def other_workload(a, lib, dev, world, rank):
-    """C3 / C4 / C5: one request per step through hhmm_run_device on resident
-    device buffers (synthetic inputs from hhmm_amd.synth, copied once)."""
+def prepare_other(a, lib, dev, rank):
+    """The request of workload a.workload on resident device buffers: returns
+    step() (one hhmm_run_device call on the current stream) and the shapes."""
     model, kw, pairing, pars, bps, desc = WORKLOADS[a.workload]
     kw = dict(kw)
     if a.pars:
@@ -448,12 +449,25 @@ def other_workload(a, lib, dev, world, rank):
     assert lib.hhmm_workspace_size(C.byref(req), C.byref(ws)) == 0
     wsbuf = torch.empty(max(int(ws.value), 256), dtype=torch.uint8, device=dev)
 
+    keep = (dmap, outs, status, wsbuf, host)
+
     def step():
         st = lib.hhmm_run_device(C.byref(req), C.byref(res), wsbuf.data_ptr(), wsbuf.numel(),
                                  torch.cuda.current_stream().cuda_stream)
         if st < 0:
             raise RuntimeError(lib.hhmm_last_error().decode())
+        return keep
 
+    return dict(step=step, model=model, kw=kw, pars=pars, bps=bps, desc=desc, data=data, draws=draws, P=P,
+                T=T, outs=outs, status=status)
+
+
+def other_workload(a, lib, dev, world, rank):
+    """C3 / C4 / C5: one request per step through hhmm_run_device on resident
+    device buffers (synthetic inputs from hhmm_amd.synth, copied once)."""
+    w = prepare_other(a, lib, dev, rank)
+    step, model, kw, pars, bps, desc = w["step"], w["model"], w["kw"], w["pars"], w["bps"], w["desc"]
+    data, draws, P, T, status = w["data"], w["draws"], w["P"], w["T"], w["status"]
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()

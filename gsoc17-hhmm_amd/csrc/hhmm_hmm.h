@@ -453,6 +453,11 @@ constexpr bool fb_big(int mode) { return (mode & FB_BIG) != 0; }
 constexpr int kFwdGroup = 4;  /* forward chunks per observation prefetch group */
 constexpr int kVitGroup = 2;  /* Viterbi chunks per observation prefetch group */
 constexpr int kBigChunk = 16; /* checkpoint interval of FB_BIG (a multiple of fb_chunk(K) = 8) */
+/* Phases of one forward-backward launch: both sweeps (the default), or the
+ * split schedule's two launches (HHMM_FLAG_FB_SPLIT): the forward sweep
+ * (loglik, checkpoints, packed symbols) and then the backward sweep, with the
+ * Viterbi decoding the packed symbols beside the latter. */
+enum FbPhase { FB_PH_BOTH = 0, FB_PH_FWD = 1, FB_PH_BWD = 2 };
 constexpr int kGroup = 2;     /* pass 1 keeps every kGroup-th state (32 steps / groups of 4 need
                                * ~300 VGPRs: occupancy 1) */
 
@@ -836,10 +841,11 @@ __device__ __forceinline__ void fb_backward_big(const DevArgs &a, const FbLane<M
  * A16), which enters with the boundary vectors the scan computed: al = the
  * forward state f_{t0-1} (ignored at t0 = 0, where the model's init runs),
  * be = beta at the chunk's last step, with their log scales. */
-template <int MODEL, int K, int MODE, bool SCAN>
+template <int MODEL, int K, int MODE, bool SCAN, int PH = FB_PH_BOTH>
 __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K> &ln, const SeriesPtrs &sp,
                                          double (&al)[K], double lsc, double (&be)[K], double blsc)
 {
+    static_assert(PH == FB_PH_BOTH || (fb_big(MODE) && !SCAN), "split sweeps: FB_BIG gamma profile only");
     constexpr int C = fb_chunk(K);
     constexpr bool AUX = ModelTraits<MODEL>::kAux;
     const int64_t p = ln.p;
@@ -849,6 +855,8 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     const int nchunk = (Tw_max + C - 1) / C;   /* chunks any lane needs */
     const int cb = ln.cb;
 
+    Obs cur[C];
+    if constexpr (PH != FB_PH_BWD) {
     /* ---- forward sweep ---- */
     int ex = 0;       /* sum of binary exponents removed */
     /* Full chunks go kFwdGroup at a time with the next group's observations
@@ -879,7 +887,6 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
             for (int u = 0; u < C; ++u)
                 grp[i][u] = nxt[i][u];
     }
-    Obs cur[C];
 #pragma unroll
     for (int u = 0; u < C; ++u)
         cur[u] = grp[0][u];
@@ -893,7 +900,8 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     }
     if (!SCAN && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
         a.loglik[p] = log(vsum<K>(al)) + (lsc + kLn2 * ex);
-    if constexpr (fb_base(MODE) == FB_FWD)
+    } /* forward sweep */
+    if constexpr (fb_base(MODE) == FB_FWD || PH == FB_PH_FWD)
         return;
 
     /* ---- backward sweep, chunk by chunk from the end ---- */
@@ -976,7 +984,7 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
 }
 
 /* One workgroup of the forward-backward: pairs [block * blockDim, +blockDim). */
-template <int MODEL, int K, int MODE>
+template <int MODEL, int K, int MODE, int PH>
 __device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
 {
     constexpr bool AUX = ModelTraits<MODEL>::kAux;
@@ -1009,13 +1017,13 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
         al[k] = 0.0;
         be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
     }
-    fb_sweep<MODEL, K, MODE, false>(a, ln, sp, al, 0.0, be, 0.0);
+    fb_sweep<MODEL, K, MODE, false, PH>(a, ln, sp, al, 0.0, be, 0.0);
 }
 
-template <int MODEL, int K, int MODE>
+template <int MODEL, int K, int MODE, int PH = FB_PH_BOTH>
 __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
 {
-    fb_block<MODEL, K, MODE>(a, blockIdx.x);
+    fb_block<MODEL, K, MODE, PH>(a, blockIdx.x);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1122,8 +1130,11 @@ __device__ __forceinline__ void vit_fwd_chunk(const DevArgs &a, int64_t p, const
     }
 }
 
-/* One workgroup of the Viterbi decoder: pairs [block * blockDim, +blockDim). */
-template <int MODEL, int K>
+/* One workgroup of the Viterbi decoder: pairs [block * blockDim, +blockDim).
+ * PK: the observations come from the packed symbol words the split
+ * schedule's forward launch wrote (a.xpk: one 4-bit symbol per step, one word
+ * per 8-step chunk; hmm-multinom, L <= 16), 0.5 instead of 4 bytes per step. */
+template <int MODEL, int K, bool PK = false>
 __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
 {
     constexpr int CV = vit_chunk(K);
@@ -1143,6 +1154,23 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
     if constexpr (ModelTraits<MODEL>::kDiscrete)
         fill_table<K, true>(slab, a, d);
     const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, n);
+    static_assert(!PK || (!VAUX && !ModelTraits<MODEL>::kGauss && CV == 8), "packed symbols: 8-step chunks, x only");
+    const int pkrows = (a.Tmax + CV - 1) / CV;
+    auto vload = [&](Obs (&dst)[CV], const SeriesPtrs &s, int t0) {
+        if constexpr (PK) {
+            /* rows past a lane's own length hold padding that is never consumed */
+            const int cc = min(max(t0 / CV, 0), pkrows - 1);
+            const uint32_t w = at(a.xpk + a.P * (int64_t)cc, (uint32_t)p * 4u);
+#pragma unroll
+            for (int v = 0; v < CV; ++v) {
+                dst[v].x = (int)((w >> (4 * v)) & 15u) + 1;
+                dst[v].aux = 0;
+                dst[v].xr = 0.0;
+            }
+        } else {
+            load_chunk<MODEL, CV, VAUX>(dst, s, t0);
+        }
+    };
     const int Tw_min = wave_min(Tp);
     const int Tw_max = wave_max(Tp);
     const int nfull = Tw_min / CV;
@@ -1152,14 +1180,14 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
      * the others keep stanc's NaN (Q3, e.g. hmm-multinom.stan:105-106). */
     double dl[K];
     Obs cur[CV];
-    load_chunk<MODEL, CV, VAUX>(cur, sp, 0);
+    vload(cur, sp, 0);
     /* chunks 1.. go kVitGroup at a time with the next group's observations in
      * flight (a one-chunk prefetch is shorter than an HBM round trip) */
     constexpr int D = kVitGroup;
     Obs grp[D][CV];
 #pragma unroll
     for (int i = 0; i < D; ++i)
-        load_chunk<MODEL, CV, VAUX>(grp[i], sp, (1 + i) * CV);
+        vload(grp[i], sp, (1 + i) * CV);
     double le[K];
     emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
 #pragma unroll
@@ -1174,7 +1202,7 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
         Obs nxt[D][CV];
 #pragma unroll
         for (int i = 0; i < D; ++i)
-            load_chunk<MODEL, CV, VAUX>(nxt[i], sp, (c + D + i) * CV);
+            vload(nxt[i], sp, (c + D + i) * CV);
 #pragma unroll
         for (int i = 0; i < D; ++i)
             vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c + i, grp[i],
@@ -1190,7 +1218,7 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
         cur[u] = grp[0][u];
     for (; c < nchunk; ++c) { /* < D full chunks, then the partial ones (one code copy) */
         Obs nxt[CV];
-        load_chunk<MODEL, CV, VAUX>(nxt, sp, (c + 1) * CV);
+        vload(nxt, sp, (c + 1) * CV);
         vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
 #pragma unroll
         for (int u = 0; u < CV; ++u)
@@ -1199,10 +1227,11 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
     viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dl, word);
 }
 
-template <int MODEL, int K>
+template <int MODEL, int K, bool PK = false>
 __global__ void __launch_bounds__(kBlock) viterbi_kernel(const DevArgs a)
 {
-    viterbi_block<MODEL, K>(a, blockIdx.x);
+    if constexpr (!PK || (fb_big_ok<MODEL, K>() && vit_chunk(K) == 8))
+        viterbi_block<MODEL, K, PK>(a, blockIdx.x);
 }
 
 /* ---- fused forward-backward + Viterbi (C2's profile) -------------------- *
@@ -2414,7 +2443,7 @@ static bool use_vit_states(const DevArgs &a)
 }
 
 template <int MODEL, int K>
-static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
+static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st, bool packed = false)
 {
     if constexpr (K == 2 || K == 4) {
         if (a.vs_nc > 0)
@@ -2445,7 +2474,10 @@ static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_UNSUPPORTED;
     }
     s.lds = std::max(s.lds, std::min(lds_floor("HHMM_PROBE_VIT_LDS_KB"), kLdsLimit));
-    hipLaunchKernelGGL((viterbi_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
+    if (packed && fbv_ok<MODEL, K>())
+        hipLaunchKernelGGL((viterbi_kernel<MODEL, K, fbv_ok<MODEL, K>()>), s.grid, s.block, s.lds, st, a);
+    else
+        hipLaunchKernelGGL((viterbi_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("viterbi_kernel launch: %s", hipGetErrorString(e));
@@ -2475,6 +2507,44 @@ static hhmm_status launch_fbv(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_HIP;
     }
     return HHMM_OK;
+}
+
+/* The split schedule (HHMM_FLAG_FB_SPLIT, C2's profile): the forward sweep
+ * alone (x read once: loglik, checkpoints, packed symbols), then the
+ * HBM-bound backward sweep on the caller's stream beside the VALU-bound
+ * Viterbi on the side stream, which decodes the packed symbols. */
+template <int MODEL, int K>
+static hhmm_status launch_split(const DevArgs &a, hipStream_t st)
+{
+    constexpr int MODE = FB_GAMMA | FB_PACK | FB_BIG;
+    LaunchShape s;
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
+        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL((fb_kernel<MODEL, K, MODE, FB_PH_FWD>), s.grid, s.block, s.lds, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("fb_kernel (forward) launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    hipStream_t vs = st;
+    hhmm_status r = fork_stream(st, &vs);
+    if (r != HHMM_OK)
+        return r;
+    r = launch_viterbi<MODEL, K>(a, vs, true);
+    if (r != HHMM_OK) {
+        join_stream(st, vs);
+        return r;
+    }
+    hipLaunchKernelGGL((fb_kernel<MODEL, K, MODE, FB_PH_BWD>), s.grid, s.block, s.lds, st, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) {
+        join_stream(st, vs);
+        set_error("fb_kernel (backward) launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return join_stream(st, vs);
 }
 
 template <int MODEL, int K>
@@ -2538,6 +2608,9 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
         if (vit && (out & HHMM_OUT_GAMMA) && !(out & extra) && a.xpk && a.scan_cl == 0 &&
             (a.flags & HHMM_FLAG_FUSED) && !use_vit_states(a))
             return launch_fbv<MODEL, K>(a, st);
+        if (vit && (out & HHMM_OUT_GAMMA) && !(out & extra) && a.xpk && a.scan_cl == 0 && a.vs_nc == 0 &&
+            (a.flags & HHMM_FLAG_FB_SPLIT) && !(a.flags & HHMM_FLAG_NO_FUSE) && !use_vit_states(a))
+            return launch_split<MODEL, K>(a, st);
     }
     hipStream_t vs = st;
     if (vit && any_fwd && !(a.flags & HHMM_FLAG_NO_FUSE)) {

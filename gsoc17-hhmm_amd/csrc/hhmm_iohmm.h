@@ -145,6 +145,83 @@ __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[
         th[i] = th[i] / sum;
 }
 
+/* stan_softmax<K, IO_CR> together with lA[i] = dev_cr_log(A[i]) -- the same
+ * doubles -- from ONE log per step instead of K:
+ *   log A_i = log th_i - log(sum) + log(A_i sum / th_i),
+ *   log th_i = y_i - log1p(rho_i), y_i = v_i - max v, rho_i = E.lo / E.hi where
+ *     the exp's quick phase gives exp(y_i) = (E.hi + E.lo) 2^e and th_i = E.hi 2^e;
+ *   A_i sum / th_i = 1 + rem_i / th_i, rem_i = fma(A_i, sum, -th_i) exact (the
+ *     remainder of a rounded quotient);
+ *   log(sum) as the log quick phase's double-double (relative error < 2^-72).
+ * Summed in double-double, the value is within
+ *   err = 2^-71 |log sum| + 2^-76 (the log and exp quick phases' bounds, the
+ *   dropped second-order terms < 2^-106, the reciprocal refinements)
+ * of log A_i, so where the rounding test passes the rounded head IS the
+ * correctly rounded log; elsewhere (the rounding test fails, the exp took its
+ * accurate phase, A_i within ~2^-18 of 1) the lane calls the full function. */
+/* Build knob, off by default: bit-identical (GPU parity green with it on),
+ * but measured SLOWER at C3 on one box (tools/ab_workload.py: 60.95 against
+ * 58.6 ms) -- the regression sweep is capped at 256 registers and the extra
+ * live doubles (y, th, rho per state) grow its spill from 144 to 224 bytes. */
+#ifndef HHMM_IO_ONELOG
+#define HHMM_IO_ONELOG 0
+#endif
+__device__ __forceinline__ double rcp_refined(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return r;
+}
+
+template <int K>
+__device__ __forceinline__ void softmax_cr_log(const double (&v)[K], double (&A)[K], double (&lA)[K])
+{
+    double mx = v[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i)
+        if (v[i] > mx)
+            mx = v[i];
+    double y[K], th[K], rho[K];
+    bool ok[K];
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        y[i] = v[i] - mx;
+        /* dev_cr_exp, keeping the quick phase's low part */
+        const bool in = (y[i] > -707.0) & (y[i] < 693.0); /* NaN: false */
+        int e;
+        const hhmm_dd f = hhmm_cr_exp_quick_dd(in ? y[i] : 0.0, &e);
+        ok[i] = in & cr_round_safe(f.hi, f.lo, f.hi * 0x1p-72);
+        double r = f.hi * hhmm_bits_to_double((uint64_t)(e + 1023) << 52);
+        rho[i] = f.lo * rcp_refined(f.hi);
+        if (!ok[i])
+            r = cr_exp_cold(y[i]);
+        th[i] = r;
+        sum += th[i];
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        A[i] = th[i] / sum;
+    /* sum >= 1 (the max term is exp(0) = 1): log(1) = 0 exactly */
+    const bool one = (sum == 1.0);
+    const bool sok = one | ((sum > 1.0) & (sum < 0x1p+1000));
+    hhmm_dd ls = hhmm_cr_log_quick_dd((sok & !one) ? sum : 2.0);
+    if (one)
+        ls = hhmm_dd_make(0.0, 0.0);
+    const double err = __builtin_fabs(ls.hi) * 0x1p-71 + 0x1p-76;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double rem = fma(A[i], sum, -th[i]);
+        const double corr = (rem * rcp_refined(th[i]) - rho[i]) - ls.lo;
+        const hhmm_dd s = hhmm_two_sum(y[i], -ls.hi);
+        const hhmm_dd r = hhmm_two_sum(s.hi, s.lo + corr);
+        double l = r.hi;
+        if (!(ok[i] & sok & cr_round_safe(r.hi, r.lo, err)))
+            l = cr_log_cold(A[i]);
+        lA[i] = l;
+    }
+}
+
 /* Per-lane mixture table entry (j, l): (mu, 1/s) and (log lambda, C - log s). */
 __device__ __forceinline__ const double2 *mix_row(const double2 *slab, int L, int j, int l, int f)
 {
@@ -215,6 +292,48 @@ __device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, co
     }
 }
 
+/* Mixture emission factor without the log (MATH != IO_CR: the FFBS
+ * contract's, or libm within tolerance): e(j) = sum_l exp(acc(j,l) - m) over
+ * the finite summands acc(j,l) = log lambda_jl + normal_lpdf of the model's
+ * log_sum_exp, m = fmax over j of max_l acc(j,l) (0 if -inf) -- exp(oblik(j) - m)
+ * with K*L exps and no log (oracle ffbs_iohmm_emission). */
+template <int K, int MATH>
+__device__ __forceinline__ void io_mix_factor(const double2 *slab, int L, double x, double (&e)[K], double &m)
+{
+    double acc[K][kIoLmax];
+    double mm = dev_ninf();
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double mx = dev_ninf();
+#pragma unroll
+        for (int l = 0; l < kIoLmax; ++l) {
+            acc[j][l] = dev_ninf();
+            if (l < L) {
+                const double2 ms = *mix_row(slab, L, j, l, 0);
+                const double2 lc = *mix_row(slab, L, j, l, 1);
+                const double z = (x - ms.x) * ms.y;
+                const double z2 = z * z;
+                acc[j][l] = lc.x + (lc.y + (-0.5 * z2));
+                if (acc[j][l] > mx)
+                    mx = acc[j][l];
+            }
+        }
+        mm = (j == 0) ? mx : fmax(mm, mx);
+    }
+    if (mm == dev_ninf())
+        mm = 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double sum = 0.0;
+#pragma unroll
+        for (int l = 0; l < kIoLmax; ++l)
+            if (l < L && acc[j][l] != dev_ninf())
+                sum += io_exp<MATH>(acc[j][l] - mm);
+        e[j] = sum;
+    }
+    m = mm;
+}
+
 /* Transition vector of step t >= 1: A_t = softmax(u_t' w_j), log A_t
  * (iohmm-reg.stan:40-49; iohmm-mix.stan:42-51, :69; iohmm-hmix.stan:36-48). */
 template <int FAM, int K, int MMAX, int MATH>
@@ -225,6 +344,12 @@ __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, 
 #pragma unroll
     for (int j = 0; j < K; ++j)
         v[j] = sse_dot<MMAX>(u, pp.w[j], M);
+    if constexpr (MATH == IO_CR && HHMM_IO_ONELOG) {
+        if (need_lA) { /* the Viterbi's log A from the softmax's own exps */
+            softmax_cr_log<K>(v, st.A, st.lA);
+            return;
+        }
+    }
     stan_softmax<K, MATH>(v, st.A);
     if (need_lA) {
 #pragma unroll
@@ -321,7 +446,12 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
         io_load<MMAX>(a, (uint32_t)n, t + 1, xn, un); /* one step ahead */
         if (t < Tp) {
             IoStep<K> st;
-            io_emission<FAM, K, MMAX, MATH>(pp, slab, L, M, x, u, st.o);
+            /* mixture without a bit-exact Viterbi: the filter's factor comes
+             * without the log-sum-exp's log (io_mix_factor); oblik itself only
+             * where an output reads it */
+            constexpr bool MIXF = (FAM == IO_MIX && MATH != IO_CR);
+            if (!MIXF || (out & (HHMM_OUT_OBLIK_TK | HHMM_OUT_UNALPHA)))
+                io_emission<FAM, K, MMAX, MATH>(pp, slab, L, M, x, u, st.o);
             if (t == 0) {
                 /* A_ij[1] = p_1k (filler, iohmm-reg.stan:41-42); logA_ij[1] = log(p_1k) (iohmm-hmix.stan:40) */
 #pragma unroll
@@ -338,13 +468,17 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                 store_tk<K>(a.logA, a, p, t, log_A_out ? st.lA : st.A);
 
             /* forward (iohmm-reg.stan:59-78): f_t = e_t * sum_i f_{t-1}(i) A_t(i) */
-            double m = st.o[0];
+            double m = 0.0;
+            double e[K];
+            if constexpr (MIXF) {
+                io_mix_factor<K, MATH>(slab, L, x, e, m);
+            } else {
+            m = st.o[0];
 #pragma unroll
             for (int k = 1; k < K; ++k)
                 m = fmax(m, st.o[k]);
             if (m == dev_ninf())
                 m = 0.0; /* every emission impossible: f_t = 0, alpha = NaN as in Stan */
-            double e[K];
             if constexpr (MATH == IO_DET) { /* the FFBS contract's e_t */
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -353,6 +487,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     e[k] = exp(st.o[k] - m);
+            }
             }
             /* FFBS: the K-vector transition does not depend on the
              * next state, so z_{t-1} = cat(v_{t-1} .* A_t, u_{t-1}) is drawn here */
@@ -403,7 +538,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 
             /* posteriors of step t */
             const double fs = vsum<K>(f);
-            const double rfs = 1.0 / fs;
+            const double rfs = fast_rcp(fs); /* renormalised: fs >= 1/2 (or 0 / NaN) */
             if ((out & HHMM_OUT_ALPHA) && a.alpha) {
                 double v[K];
 #pragma unroll
@@ -645,18 +780,20 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
     for (int t = 0; t < Tw_max; ++t) {
         io_load<MMAX>(a, (uint32_t)n, t + 1, xn, un);
         if (t < Tp) {
-            /* emission of state js (io_emission's arithmetic) */
-            double o;
+            /* emission of state js (io_emission's arithmetic); the mixture
+             * yields only its summands' max mx and the filter factor comes from
+             * them below (io_mix_factor's arithmetic: no log) */
+            double o = 0.0, acc[LM], mxs = 0.0;
             if constexpr (FAM == IO_REG) {
                 const double mv = sse_dot<MMAX>(u, b, M);
                 const double z = (x - mv) * isig;
                 const double z2 = z * z;
                 o = c0 + (-0.5 * z2);
             } else {
-                double acc[LM];
                 double mx = dev_ninf();
 #pragma unroll
                 for (int l = 0; l < LM; ++l) {
+                    acc[l] = dev_ninf();
                     if (l < L) {
                         const double2 ms = col[(2 * l) * 64];
                         const double2 lg = col[(2 * l + 1) * 64];
@@ -667,12 +804,7 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
                             mx = acc[l];
                     }
                 }
-                double sum = 0.0;
-#pragma unroll
-                for (int l = 0; l < LM; ++l)
-                    if (l < L && acc[l] != dev_ninf())
-                        sum += io_exp<MATH>(acc[l] - mx);
-                o = mx + io_log<MATH>(sum);
+                mxs = mx;
             }
             /* transition A_t = softmax(u_t' w) (stan_softmax's order); t = 0: p_1k */
             double AA[K];
@@ -698,17 +830,27 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
                     sum += tt[i];
                 quad_gather<K>(th / sum, AA);
             }
-            /* e_t = exp(o - max o) */
+            /* e_t = exp(o - max o); mixture: sum_l exp(acc_l - m) */
             double oo[K];
-            quad_gather<K>(o, oo);
+            quad_gather<K>(FAM == IO_REG ? o : mxs, oo);
             double m = oo[0];
 #pragma unroll
             for (int k = 1; k < K; ++k)
                 m = fmax(m, oo[k]);
             if (m == dev_ninf())
                 m = 0.0;
+            double ej;
+            if constexpr (FAM == IO_REG) {
+                ej = MATH == IO_DET ? hhmm_det_exp(o - m) : exp(o - m);
+            } else {
+                ej = 0.0;
+#pragma unroll
+                for (int l = 0; l < LM; ++l)
+                    if (l < L && acc[l] != dev_ninf())
+                        ej += io_exp<MATH>(acc[l] - m);
+            }
             double ee[K];
-            quad_gather<K>(MATH == IO_DET ? hhmm_det_exp(o - m) : exp(o - m), ee);
+            quad_gather<K>(ej, ee);
             if (want_ffbs) {
                 if (t > 0) {
                     double wv[K];
@@ -745,7 +887,7 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 1; k < K; ++k)
                     fj = (js == k) ? f[k] : fj;
-                const double v = fj * (1.0 / vsum<K>(f));
+                const double v = fj * fast_rcp(vsum<K>(f)); /* renormalised: the sum is >= 1/2 (or 0 / NaN) */
                 if ((out & HHMM_OUT_ALPHA) && a.alpha)
                     put_out(a.alpha + a.P * ((int64_t)t + (int64_t)a.Tout * js), (uint32_t)p * 8u, v);
                 if ((out & HHMM_OUT_GAMMA) && a.gamma)

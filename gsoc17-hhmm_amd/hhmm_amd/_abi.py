@@ -45,6 +45,7 @@ FLAG_VIT_STATES = 1 << 4
 FLAG_FUSED = 1 << 5
 FLAG_VIT_SCAN = 1 << 6
 FLAG_VIT_SCAN_OFF = 1 << 7
+FLAG_FB_SPLIT = 1 << 16
 
 
 def flag_scan_chunk_log2(n):

@@ -210,6 +210,11 @@ typedef struct hhmm_draws {
  * pairs with T >= 16384; VIT_SCAN forces it, VIT_SCAN_OFF forbids it. */
 #define HHMM_FLAG_VIT_SCAN (1u << 6)
 #define HHMM_FLAG_VIT_SCAN_OFF (1u << 7)
+/* The C2 profile (hmm-multinom, K = 4, gamma_tk (+ loglik) with zstar_t /
+ * logp_zstar, lane decoder) as three launches: the forward sweep, then the
+ * backward sweep beside a Viterbi that reads the forward sweep's packed
+ * symbols instead of x (identical results). */
+#define HHMM_FLAG_FB_SPLIT (1u << 16)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */

@@ -901,7 +901,12 @@ static void model_tayal_lite(pair_ctx *c)
  *   filter f_t (K-vector, linear space, renormalised each step):
  *     e_t(j) = emission: phi_k[j, x_t] (multinomial / semisup / Tayal);
  *              det_exp(lpdf_j - m) with m = fmax over j (hmm.stan Gaussian);
- *              det_exp(ob_t(j) - m), m = fmax over j (0 if -inf) (IOHMM)
+ *              IOHMM regression: det_exp(ob_t(j) - m), m = fmax over j (0 if -inf);
+ *              IOHMM mixture: sum_l det_exp(acc_t(j,l) - m) in l order over the
+ *              finite acc (acc = log lambda_jl + normal_lpdf, the summands of the
+ *              model's log_sum_exp), m = fmax over j of (max_l by '>') (0 if -inf):
+ *              exp(ob_t(j) - m) without forming ob_t, so a step takes K*L det_exp
+ *              and no det_log
  *     det_exp / det_log: the deterministic exp / log of hhmm_detmath.h (the
  *     contract's own transcendentals: bit-identical on both sides, cheaper
  *     than the correctly rounded ones the Viterbi needs)
@@ -980,33 +985,48 @@ static int ffbs_mask(int model, const pair_ctx *c, int t, int j1)
     return 1;
 }
 
-/* The IOHMM emission ob_t (K-vector) and softmax transition A_t (t >= 1) of
- * the FFBS contract: the model's blocks (iohmm_mixture_oblik, model_iohmm_reg's
- * emission, iohmm_transitions above) with det_exp / det_log. */
-static void ffbs_iohmm_oblik(const pair_ctx *c, int model, int t, double *ob)
+/* The IOHMM emission factor e_t (K-vector, scaled by exp(-m)) of the FFBS
+ * contract, from the model's emission (model_iohmm_reg's normal_lpdf,
+ * iohmm_mixture_oblik's summands) with det_exp / det_log. */
+static void ffbs_iohmm_emission(const pair_ctx *c, int model, int t, double *e)
 {
     const int K = c->K, M = c->M, L = c->L;
-    double acc[L > 0 ? L : 1];
-    for (int j = 0; j < K; ++j) {
-        if (model == HHMM_MODEL_IOHMM_REG) { /* normal_lpdf(x_t | u_t' b_j, s_j) (iohmm-reg.stan:51-57) */
+    double m = NEG_INF;
+    if (model == HHMM_MODEL_IOHMM_REG) {
+        for (int j = 0; j < K; ++j) { /* normal_lpdf(x_t | u_t' b_j, s_j) (iohmm-reg.stan:51-57) */
             const double mu = stan_dot(&c->u[(size_t)t * M], &c->b[(size_t)j * M], M);
             const double z = (c->xr[t] - mu) * (1.0 / c->sk[j]);
-            ob[j] = (HHMM_NEG_LOG_SQRT_TWO_PI - hhmm_det_log(c->sk[j])) + (-0.5 * (z * z));
-            continue;
+            e[j] = (HHMM_NEG_LOG_SQRT_TWO_PI - hhmm_det_log(c->sk[j])) + (-0.5 * (z * z));
+            m = (j == 0) ? e[j] : fmax(m, e[j]);
         }
-        /* LSE_l(log lambda_jl + normal_lpdf(x_t | mu_jl, s_jl)) (iohmm-mix.stan:53-65) */
-        double mx = NEG_INF, sum = 0.0;
+        if (m == NEG_INF)
+            m = 0.0;
+        for (int j = 0; j < K; ++j)
+            e[j] = hhmm_det_exp(e[j] - m);
+        return;
+    }
+    /* the summands of LSE_l(log lambda_jl + normal_lpdf(x_t | mu_jl, s_jl)) (iohmm-mix.stan:53-65) */
+    double acc[K * (L > 0 ? L : 1)];
+    for (int j = 0; j < K; ++j) {
+        double mx = NEG_INF;
         for (int l = 0; l < L; ++l) {
             const double s = c->skl[j * L + l];
             const double z = (c->xr[t] - c->mukl[j * L + l]) * (1.0 / s);
-            acc[l] = hhmm_det_log(c->lambda[j * L + l]) + ((HHMM_NEG_LOG_SQRT_TWO_PI - hhmm_det_log(s)) + (-0.5 * (z * z)));
-            if (acc[l] > mx)
-                mx = acc[l];
+            const double a = hhmm_det_log(c->lambda[j * L + l]) + ((HHMM_NEG_LOG_SQRT_TWO_PI - hhmm_det_log(s)) + (-0.5 * (z * z)));
+            acc[j * L + l] = a;
+            if (a > mx)
+                mx = a;
         }
+        m = (j == 0) ? mx : fmax(m, mx);
+    }
+    if (m == NEG_INF)
+        m = 0.0;
+    for (int j = 0; j < K; ++j) {
+        double sum = 0.0;
         for (int l = 0; l < L; ++l)
-            if (acc[l] != NEG_INF)
-                sum += hhmm_det_exp(acc[l] - mx);
-        ob[j] = mx + hhmm_det_log(sum);
+            if (acc[j * L + l] != NEG_INF)
+                sum += hhmm_det_exp(acc[j * L + l] - m);
+        e[j] = sum;
     }
 }
 
@@ -1036,17 +1056,9 @@ static void ffbs_contract(pair_ctx *c, int model)
     if (iohmm) {
         double *A1 = w + K; /* A_{t+1} */
         for (int t = 0; t < T; ++t) {
-            double m;
-            ffbs_iohmm_oblik(c, model, t, e);
-            m = e[0];
-            for (int k = 1; k < K; ++k)
-                m = fmax(m, e[k]);
-            if (m == NEG_INF)
-                m = 0.0;
-            for (int k = 0; k < K; ++k) {
-                e[k] = hhmm_det_exp(e[k] - m);
+            ffbs_iohmm_emission(c, model, t, e);
+            for (int k = 0; k < K; ++k)
                 TK(c->ff, t, k) = (t == 0) ? c->p[k] * e[k] : e[k];
-            }
             if (t + 1 < T)
                 ffbs_iohmm_transition(c, t + 1, A1);
             for (int i = 0; i < K; ++i)

@@ -180,16 +180,12 @@ def hmm_family(model, T, K, x, p, A, uu, phi=None, mu=None, sigma=None, aux=None
     return z
 
 
-def iohmm(T, K, p, oblik, Arows, uu):
-    """Draws for the IOHMM programs; oblik[t][k], Arows[t][k] 0-based (Arows[0] = p filler)."""
+def iohmm(T, K, p, E, Arows, uu):
+    """Draws for the IOHMM programs; E[t][k] the emission factor e_t(k),
+    Arows[t][k] 0-based (Arows[0] = p filler)."""
     v = []
     for t in range(T):
-        m = oblik[t][0]
-        for a in oblik[t][1:]:
-            m = fmax(m, a)
-        if m == NINF:
-            m = 0.0
-        e = [det_exp(a - m) for a in oblik[t]]
+        e = E[t]
         v.append([float(p[k]) * e[k] for k in range(K)] if t == 0 else e)
     z = []
     for t in range(T):
@@ -215,16 +211,27 @@ def iohmm_det_inputs(model, T, K, u, x, d):
             th.append(det_exp(a - mx))
             sm += th[-1]
         A.append([a / sm for a in th])
-    ob = []
+    E = []
     for t in range(T):
-        row = []
-        for j in range(K):
-            if model == "iohmm-reg":
+        if model == "iohmm-reg":
+            # e_t(j) = det_exp(ob_t(j) - m), m = fmax over j (0 if -inf)
+            ob = []
+            for j in range(K):
                 b = [float(v) for v in np.asarray(d["b_km"])[j]]
                 sg = float(d["s_k"][j])
                 z = (x[t] - onp.eigen_dot(u[t], b)) * (1.0 / sg)
-                row.append((NEG_LOG_SQRT_TWO_PI - det_log(sg)) + (-0.5 * (z * z)))
-                continue
+                ob.append((NEG_LOG_SQRT_TWO_PI - det_log(sg)) + (-0.5 * (z * z)))
+            m = ob[0]
+            for a in ob[1:]:
+                m = fmax(m, a)
+            if m == NINF:
+                m = 0.0
+            E.append([det_exp(a - m) for a in ob])
+            continue
+        # mixture: e_t(j) = sum_l det_exp(acc_jl - m) over the finite summands of the
+        # model's log_sum_exp, m = fmax over j of max_l acc_jl (0 if -inf): no det_log
+        accs, m = [], NINF
+        for j in range(K):
             lam, mu, sk = (np.asarray(d[k])[j] for k in ("lambda_kl", "mu_kl", "s_kl"))
             acc = []
             for l in range(len(lam)):
@@ -235,13 +242,19 @@ def iohmm_det_inputs(model, T, K, u, x, d):
             for a in acc:
                 if a > mx:
                     mx = a
+            m = mx if j == 0 else fmax(m, mx)
+            accs.append(acc)
+        if m == NINF:
+            m = 0.0
+        row = []
+        for acc in accs:
             sm = 0.0
             for a in acc:
                 if a != NINF:
-                    sm += det_exp(a - mx)
-            row.append(mx + det_log(sm))
-        ob.append(row)
-    return ob, A
+                    sm += det_exp(a - m)
+            row.append(sm)
+        E.append(row)
+    return E, A
 
 
 def run(model, data, draws, uniforms):
@@ -261,8 +274,8 @@ def run(model, data, draws, uniforms):
         if model.startswith("iohmm"):
             u = np.asarray(data["u_tm"]).reshape(N, Tm, -1)[n, :T]
             xt = [float(v) for v in np.asarray(data["x_t"]).reshape(N, Tm)[n, :T]]
-            ob, A = iohmm_det_inputs(model, T, K, [list(map(float, r)) for r in u], xt, d)
-            out.append(iohmm(T, K, d["p_1k"], ob, A, uu))
+            E, A = iohmm_det_inputs(model, T, K, [list(map(float, r)) for r in u], xt, d)
+            out.append(iohmm(T, K, d["p_1k"], E, A, uu))
         elif model == "hhmm-tayal2009":
             p1, A = onp.tayal_expand(float(d["p_11"]), d["A_row"])
             out.append(hmm_family(model, T, K, x[n], p1, A, uu, phi=d["phi_k"], aux=np.asarray(data["sign"])[n]))

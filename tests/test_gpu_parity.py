@@ -245,6 +245,73 @@ def test_viterbi_layouts_ragged(engine, oracle, model, layout):
     compare_all(got, ref, pars + ["pair_status"])
 
 
+@pytest.mark.parametrize("T", [1, 2, 9, 37, 130])
+def test_split_schedule(engine, oracle, T):
+    """HHMM_FLAG_FB_SPLIT (hmm-multinom K = 4, gamma + path in one request):
+    the forward launch packs the symbols, the Viterbi decodes them beside the
+    backward launch -- bit-exact paths, gamma / loglik within tolerance, at
+    series lengths around the 8-step chunk and 16-step block sizes."""
+    import hhmm_amd
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    data, draws = synth.hmm_multinom(N=70, S=70, T=T, K=4, L=9)
+    flags = _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=flags, pairing="zip",
+                       return_status=True)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+@pytest.mark.parametrize("scale", [1.0, 8.0, 40.0, 400.0])
+@pytest.mark.parametrize("model", ["iohmm-reg", "iohmm-hmix"])
+def test_viterbi_log_softmax_regimes(engine, oracle, model, scale):
+    """The Viterbi's log A_t(i) -- the correctly rounded log of each softmax
+    output (and, in a -DHHMM_IO_ONELOG=1 build, derived from the softmax's own
+    exps and one log of the sum: softmax_cr_log) -- bit-exact with the oracle
+    from mild transitions (scale 1) to saturated ones where one state takes
+    A = 1 - tiny (sum == 1, A within 2^-18 of 1) and the others underflow
+    toward the exp's accurate phase."""
+    import hhmm_amd
+    data, draws = synth.GENERATORS[model](N=3, S=50, T=120, K=4, M=4)
+    draws["w_km"] = draws["w_km"] * scale
+    pars = ["zstar_t", "logp_zstar", "loglik"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+def test_unsupported_shape_leaves_no_kernel_running(engine, oracle):
+    """hmm-multinom K = 4 with L = 100: the forward-backward's emission table
+    (L * 4 doubles per lane) does not fit in LDS while the state-parallel
+    decoder's would.  The request fails before either kernel is enqueued (no
+    decoder left writing into buffers the call hands back), and the next
+    request on the same device is still bit-exact with the oracle."""
+    import hhmm_amd
+    from hhmm_amd.api import HHMMError
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    data, draws = synth.hmm_multinom(N=3, S=40, T=200, K=4, L=100)
+    with pytest.raises(HHMMError, match="does not fit"):
+        hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine)
+    data, draws = synth.hmm_multinom(N=3, S=40, T=200, K=4, L=9)
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, return_status=True)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+def test_split_schedule_ragged(engine, oracle):
+    """Ragged lengths inside one wave: a lane's packed rows past its own end
+    are padding the decoder never consumes."""
+    import hhmm_amd
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    N = 130
+    data, draws = synth.hmm_multinom(N=N, S=N, T=300, K=4, L=9)
+    data["T"] = np.random.default_rng(5).integers(1, 301, N).astype(np.int32)
+    flags = _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=flags, pairing="zip",
+                       return_status=True)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
 @pytest.mark.parametrize("model", ["hmm-multinom", "hhmm-tayal2009"])
 def test_viterbi_states_backtrack_groups(engine, oracle, model):
     """The state-parallel decoder's backtrack reads its back-pointer words in

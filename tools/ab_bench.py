@@ -47,7 +47,7 @@ def main():
         libs[name] = hhmm_amd.load_library(path)
     x, draws = bench.make_batch(a.pairs, a.T, 9000, dev)
     runs = {n: bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev) for n, lib in libs.items()}
-    times = {n: {"fb": [], "vit": [], "pair": []} for n in runs}
+    times = {n: {"fb": [], "vit": [], "pair": [], "step": [], "split": []} for n in runs}
     s0 = torch.cuda.current_stream()
     s1 = torch.cuda.Stream()
 
@@ -95,6 +95,21 @@ def main():
             e1.record(s0)
             torch.cuda.synchronize()
             times[n]["pair"].append(e0.elapsed_time(e1))
+            for req in ("step", "split"):  # one library request each (side stream inside)
+                torch.cuda.synchronize()
+                e0.record(s0)
+                run.launch(req)
+                e1.record(s0)
+                torch.cuda.synchronize()
+                times[n][req].append(e0.elapsed_time(e1))
+                if r == 1 and req == "split":
+                    g = run.out["gamma_tk"][:, :, :4096].cpu()
+                    z = run.out["zstar_t"][:, :4096].cpu()
+                    run.launch("step")
+                    torch.cuda.synchronize()
+                    same_g = bool(torch.equal(g, run.out["gamma_tk"][:, :, :4096].cpu()))
+                    same_z = bool(torch.equal(z, run.out["zstar_t"][:, :4096].cpu()))
+                    print(f"{n}: split vs step outputs identical: gamma {same_g}, zstar {same_z}", flush=True)
     out = {}
     for n, t in times.items():
         out[n] = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for k, v in t.items()}

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of libhhmm variants on one bench.py workload (c3,
+c4, c5, n1), in ONE process on ONE device (cross-box numbers are not
+comparable):
+
+  python tools/ab_workload.py --workload c3 NAME=path/to/libhhmm.so [NAME=...] [--rounds 5] [--steps 3]
+
+Every variant gets the same synthetic request (bench.prepare_other); rounds
+run A B C A B C ..., each round `steps` back-to-back requests timed with HIP
+events.  After the warm-up the variants' outputs are compared with the first
+variant's (integer outputs bit for bit, float outputs to 1e-12 relative).
+"""
+import argparse
+import json
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "gsoc17-hhmm_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import hhmm_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5", "n1"])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--pars", default=None)
+    ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=bench.synth.SEED)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    runs = {}
+    for v in a.variants:
+        name, path = v.split("=", 1)
+        runs[name] = bench.prepare_other(a, hhmm_amd.load_library(path), dev, 0)
+    ref = None
+    for n, w in runs.items():
+        w["step"]()
+        torch.cuda.synchronize()
+        outs = {k: t.cpu() for k, t in w["outs"].items()}
+        if ref is None:
+            ref = outs
+            continue
+        for k, t in outs.items():
+            if t.dtype == torch.int32:
+                ok = bool(torch.equal(t, ref[k]))
+            else:
+                d = (t - ref[k]).abs() / ref[k].abs().clamp_min(1e-300)
+                ok = bool(torch.nan_to_num(d, nan=0.0).max() <= 1e-12)
+            print(f"{n}: {k} matches the first variant: {ok}", flush=True)
+    times = {n: [] for n in runs}
+    for _ in range(a.rounds):
+        for n, w in runs.items():
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            torch.cuda.synchronize()
+            ev[0].record()
+            for _ in range(a.steps):
+                w["step"]()
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[n].append(ev[0].elapsed_time(ev[1]) / a.steps)
+    out = {n: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))} for n, t in times.items()}
+    print(json.dumps({"workload": a.workload, "ms_per_request": out}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
