@@ -280,8 +280,10 @@ __device__ __forceinline__ double vsum(const double (&v)[K])
 
 /* cat(w, u): Stan's categorical_rng(w / sum(w)) with the caller's uniform u
  * (Stan Math: cumulative_sum of theta, `while (c > cum[b]) b++`), bounded to
- * K - 1; sequential sum, IEEE divisions.  Returns the 0-based state, or -1
- * when sum(w) is not a positive finite number.  FFBS contract, DESIGN.md §5. */
+ * K - 1, with the comparison scaled by the sum instead of dividing every
+ * weight: us = u * sum against the running sum of w.  Returns the 0-based
+ * state, or -1 when sum(w) is not a positive finite number.  FFBS contract,
+ * DESIGN.md §5 (oracle ffbs_cat). */
 template <int K>
 __device__ __forceinline__ int ffbs_cat(const double (&w)[K], double u)
 {
@@ -289,18 +291,16 @@ __device__ __forceinline__ int ffbs_cat(const double (&w)[K], double u)
 #pragma unroll
     for (int i = 1; i < K; ++i)
         sum = sum + w[i];
-    if (!(sum > 0.0) || !__builtin_isfinite(sum))
-        return -1;
+    const double us = u * sum;
     int b = 0;
-    double cum = w[0] / sum;
+    double cum = w[0];
 #pragma unroll
     for (int i = 1; i < K; ++i) {
-        if (b == i - 1 && u > cum) {
-            b = i;
-            cum = cum + w[i] / sum;
-        }
+        const bool step = (b == i - 1) & (us > cum);
+        b = step ? i : b;
+        cum = step ? cum + w[i] : cum;
     }
-    return b;
+    return ((sum > 0.0) & __builtin_isfinite(sum)) ? b : -1;
 }
 
 /* Viterbi chunk length: a multiple of the back-pointer steps per word so

@@ -125,9 +125,10 @@ __device__ __forceinline__ double sse_dot(const double (&a)[MMAX], const double 
     return res;
 }
 
-/* Stan Math softmax(v): theta = exp(v - max v); theta / sequential sum. */
+/* Stan Math softmax(v): theta = exp(v - max v); theta / sequential sum.
+ * num: the numerators exp(v - max v) (the FFBS contract's weights). */
 template <int K, int MATH>
-__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K])
+__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K], double (&num)[K])
 {
     double mx = v[0];
 #pragma unroll
@@ -137,12 +138,12 @@ __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[
     double sum = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        th[i] = io_exp<MATH>(v[i] - mx);
-        sum += th[i];
+        num[i] = io_exp<MATH>(v[i] - mx);
+        sum += num[i];
     }
 #pragma unroll
     for (int i = 0; i < K; ++i)
-        th[i] = th[i] / sum;
+        th[i] = num[i] / sum;
 }
 
 /* stan_softmax<K, IO_CR> together with lA[i] = dev_cr_log(A[i]) -- the same
@@ -222,6 +223,13 @@ __device__ __forceinline__ void softmax_cr_log(const double (&v)[K], double (&A)
     }
 }
 
+template <int K, int MATH>
+__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K])
+{
+    double num[K];
+    stan_softmax<K, MATH>(v, th, num);
+}
+
 /* Per-lane mixture table entry (j, l): (mu, 1/s) and (log lambda, C - log s). */
 __device__ __forceinline__ const double2 *mix_row(const double2 *slab, int L, int j, int l, int f)
 {
@@ -243,6 +251,7 @@ template <int K>
 struct IoStep {
     double o[K];  /* oblik_tk[t] */
     double A[K];  /* A_ij[t] (t = 0: p_1k filler) */
+    double th[K]; /* the softmax numerators of A_ij[t] (FFBS weights) */
     double lA[K]; /* log A_ij[t] (t = 0: log p_1k) */
 };
 
@@ -350,7 +359,7 @@ __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, 
             return;
         }
     }
-    stan_softmax<K, MATH>(v, st.A);
+    stan_softmax<K, MATH>(v, st.A, st.th);
     if (need_lA) {
 #pragma unroll
         for (int j = 0; j < K; ++j)
@@ -456,7 +465,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                 /* A_ij[1] = p_1k (filler, iohmm-reg.stan:41-42); logA_ij[1] = log(p_1k) (iohmm-hmix.stan:40) */
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    st.A[k] = pp.p[k];
+                    st.A[k] = st.th[k] = pp.p[k];
                     st.lA[k] = log_A_out ? io_log<MATH>(pp.p[k]) : 0.0;
                 }
             } else {
@@ -490,13 +499,14 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
             }
             }
             /* FFBS: the K-vector transition does not depend on the
-             * next state, so z_{t-1} = cat(v_{t-1} .* A_t, u_{t-1}) is drawn here */
+             * next state, so z_{t-1} = cat(v_{t-1} .* th_t, u_{t-1}) is drawn here
+             * (th_t = A_t's softmax numerators: cat normalises) */
             if (want_ffbs) {
                 if (t > 0) {
                     double w[K];
 #pragma unroll
                     for (int k = 0; k < K; ++k)
-                        w[k] = vprev[k] * st.A[k];
+                        w[k] = vprev[k] * st.th[k];
                     at(a.z_ffbs + a.P * (int64_t)(t - 1), (uint32_t)p * 4u) = ffbs_cat<K>(w, uprev) + 1;
                 }
 #pragma unroll
@@ -673,35 +683,6 @@ __global__ void __launch_bounds__(kBlock) iohmm_mix_kernel(const DevArgs a)
     iohmm_sweep<IO_MIX, K, MMAX, MATH, HOT>(a);
 }
 
-/* ffbs_cat with the quotients w_i / sum shared across the lane quad: lane
- * js divides its own, the quad gathers them, and every lane runs the same
- * cumulative comparison -- the same doubles as ffbs_cat's. */
-template <int K>
-__device__ __forceinline__ int ffbs_cat_quad(const double (&w)[K], int js, double u)
-{
-    double sum = w[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i)
-        sum = sum + w[i];
-    if (!(sum > 0.0) || !__builtin_isfinite(sum))
-        return -1;
-    double wj = w[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i)
-        wj = (js == i) ? w[i] : wj;
-    double q[K];
-    quad_gather<K>(wj / sum, q);
-    int b = 0;
-    double cum = q[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i) {
-        if (b == i - 1 && u > cum) {
-            b = i;
-            cum = cum + q[i];
-        }
-    }
-    return b;
-}
 
 /* ---- state-parallel sweep (few pairs; C4) ------------------------------ *
  * One lane per (pair, state j), a pair's K <= 4 states in one lane quad.  A
@@ -774,6 +755,8 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
     int ex = 0;
     double vprev[K];
     double uprev = 0.5;
+    double psum = 1.0; /* product of the softmax sums the filter did not divide by, */
+    int pex = 0;       /* as psum * 2^pex */
     double x, xn;
     double u[MMAX], un[MMAX];
     io_load<MMAX>(a, (uint32_t)n, 0, x, u);
@@ -821,14 +804,17 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
                 for (int i = 1; i < K; ++i)
                     if (vv[i] > mx)
                         mx = vv[i];
-                const double th = io_exp<MATH>(v - mx);
-                double tt[K];
-                quad_gather<K>(th, tt);
+                /* the numerators exp(v - max) only: the FFBS weights take them as
+                 * they are (cat normalises), and the filter carries the sum in a
+                 * separate log scale (psum, pex) instead of dividing */
+                quad_gather<K>(io_exp<MATH>(v - mx), AA);
                 double sum = 0.0;
 #pragma unroll
                 for (int i = 0; i < K; ++i)
-                    sum += tt[i];
-                quad_gather<K>(th / sum, AA);
+                    sum += AA[i];
+                int e;
+                psum = frexp(psum * sum, &e);
+                pex += e;
             }
             /* e_t = exp(o - max o); mixture: sum_l exp(acc_l - m) */
             double oo[K];
@@ -857,7 +843,7 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 #pragma unroll
                     for (int k = 0; k < K; ++k)
                         wv[k] = vprev[k] * AA[k];
-                    const int z = ffbs_cat_quad<K>(wv, js, uprev) + 1;
+                    const int z = ffbs_cat<K>(wv, uprev) + 1;
                     if (live && j == 0)
                         at(a.z_ffbs + a.P * (int64_t)(t - 1), (uint32_t)p * 4u) = z;
                 }
@@ -866,7 +852,7 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
                     vprev[k] = (t == 0) ? pk[k] * ee[k] : ee[k];
                 uprev = at(a.ffbs_u + a.P * (int64_t)t, (uint32_t)p * 8u);
             }
-            /* forward: f_t = e_t * sum_i f_{t-1}(i) A_t(i) */
+            /* forward: f_t = e_t * sum_i f_{t-1}(i) A_t(i) (times the softmax sum) */
             if (t == 0) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -903,7 +889,7 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
         if (want_ffbs)
             at(a.z_ffbs + a.P * (int64_t)(Tp - 1), (uint32_t)p * 4u) = ffbs_cat<K>(vprev, uprev) + 1;
         if ((out & HHMM_OUT_LOGLIK) && a.loglik)
-            a.loglik[p] = log(vsum<K>(f)) + (lsc + kLn2 * ex);
+            a.loglik[p] = (log(vsum<K>(f)) + (lsc + kLn2 * ex)) - (log(psum) + kLn2 * pex);
     }
 }
 

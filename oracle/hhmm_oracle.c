@@ -917,18 +917,20 @@ static void model_tayal_lite(pair_ctx *c)
  *              FORWARD pass) replaces s_t(j) by ((f(0) + f(1)) + ...) + f(K-1)
  *     renorm: f <- ldexp(f, -E), E = frexp exponent of fmax_j f(j) (0 if 0/inf/NaN)
  *   sampling, cat(w, u) = Stan's categorical_rng(w / sum w) with the caller's
- *     uniform: sum = ((w0 + w1) + ...); theta_i = w_i / sum; b = 0, c = theta_0;
- *     while (b < K-1 && u > c) c = c + theta_{++b};  draw b + 1
+ *     uniform, without the divisions: sum = ((w0 + w1) + ...); us = u * sum;
+ *     b = 0, c = w_0; while (b < K-1 && us > c) c = c + w_{++b};  draw b + 1
  *     (0 and every earlier draw 0 if sum is not a positive finite number)
  *     z_{T-1} = cat(f_{T-1}, u_{T-1});
  *     z_t     = cat(w, u_t), w_i = f_t(i) * A(i, z_{t+1}), or w_i = f_t(i) where the
  *               model's forward mask switches the transition off at (t+1, z_{t+1})
  *   IOHMM (Q5: the transition K-vector A_t does not depend on the next state,
  *     so f_t is proportional to e_t for t >= 1 and the draws decouple):
- *     v_0 = p .* e_0, v_t = e_t (t >= 1); z_t = cat(v_t .* A_{t+1}, u_t); z_{T-1} = cat(v_{T-1}, u_{T-1}).
- *     ob_t and A_t are the model's emission and softmax transition in the
- *     model's operation order (iohmm-reg.stan:40-57, iohmm-mix.stan:42-65,
- *     iohmm-hmix.stan:36-62) with det_exp / det_log in place of exp / log.
+ *     v_0 = p .* e_0, v_t = e_t (t >= 1); z_t = cat(v_t .* th_{t+1}, u_t); z_{T-1} = cat(v_{T-1}, u_{T-1}),
+ *     th_t = the softmax numerators det_exp(u_t' w_j - max_j) (A_t = th_t / sum: cat
+ *     normalises, so the division is left out).  ob_t and th_t follow the model's
+ *     emission and softmax transition in the model's operation order
+ *     (iohmm-reg.stan:40-57, iohmm-mix.stan:42-65, iohmm-hmix.stan:36-62) with
+ *     det_exp / det_log in place of exp / log.
  */
 static void ffbs_renorm(double *v, int K)
 {
@@ -949,11 +951,13 @@ static int ffbs_cat(const double *w, int K, double u)
         sum = sum + w[i];
     if (!(sum > 0.0) || !isfinite(sum))
         return 0;
+    /* u against the cumulative weights scaled by the sum: no division */
+    const double us = u * sum;
     int b = 0;
-    double cum = w[0] / sum;
-    while (b < K - 1 && u > cum) {
+    double cum = w[0];
+    while (b < K - 1 && us > cum) {
         ++b;
-        cum = cum + w[b] / sum;
+        cum = cum + w[b];
     }
     return b + 1;
 }
@@ -1030,21 +1034,18 @@ static void ffbs_iohmm_emission(const pair_ctx *c, int model, int t, double *e)
     }
 }
 
-static void ffbs_iohmm_transition(const pair_ctx *c, int t, double *A)
+/* The softmax numerators th_t(j) = det_exp(u_t' w_j - max) (t >= 1). */
+static void ffbs_iohmm_transition(const pair_ctx *c, int t, double *th)
 {
     const int K = c->K, M = c->M;
-    double mx = NEG_INF, sum = 0.0;
+    double mx = NEG_INF;
     for (int j = 0; j < K; ++j) {
-        A[j] = stan_dot(&c->u[(size_t)t * M], &c->w[(size_t)j * M], M);
-        if (j == 0 || A[j] > mx)
-            mx = A[j];
-    }
-    for (int j = 0; j < K; ++j) {
-        A[j] = hhmm_det_exp(A[j] - mx);
-        sum += A[j];
+        th[j] = stan_dot(&c->u[(size_t)t * M], &c->w[(size_t)j * M], M);
+        if (j == 0 || th[j] > mx)
+            mx = th[j];
     }
     for (int j = 0; j < K; ++j)
-        A[j] = A[j] / sum;
+        th[j] = hhmm_det_exp(th[j] - mx);
 }
 
 static void ffbs_contract(pair_ctx *c, int model)

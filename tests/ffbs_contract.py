@@ -109,11 +109,12 @@ def cat(w, u):
         s = s + a
     if not (s > 0.0) or not math.isfinite(s):
         return 0
+    us = u * s
     b = 0
-    c = w[0] / s
-    while b < len(w) - 1 and u > c:
+    c = w[0]
+    while b < len(w) - 1 and us > c:
         b += 1
-        c = c + w[b] / s
+        c = c + w[b]
     return b + 1
 
 
@@ -182,7 +183,7 @@ def hmm_family(model, T, K, x, p, A, uu, phi=None, mu=None, sigma=None, aux=None
 
 def iohmm(T, K, p, E, Arows, uu):
     """Draws for the IOHMM programs; E[t][k] the emission factor e_t(k),
-    Arows[t][k] 0-based (Arows[0] = p filler)."""
+    Arows[t][k] the softmax numerators th_t(k), 0-based (Arows[0] = p filler)."""
     v = []
     for t in range(T):
         e = E[t]
@@ -195,7 +196,7 @@ def iohmm(T, K, p, E, Arows, uu):
 
 
 def iohmm_det_inputs(model, T, K, u, x, d):
-    """The contract's ob_t and A_t (A[0] = p filler): the model's emission and
+    """The contract's e_t and th_t (th[0] = p filler): the model's emission and
     softmax transition (iohmm-reg.stan:40-57, iohmm-mix.stan:42-65) with
     det_exp / det_log."""
     w = [[float(v) for v in row] for row in np.asarray(d["w_km"])]
@@ -206,11 +207,8 @@ def iohmm_det_inputs(model, T, K, u, x, d):
         for a in v[1:]:
             if a > mx:
                 mx = a
-        th, sm = [], 0.0
-        for a in v:
-            th.append(det_exp(a - mx))
-            sm += th[-1]
-        A.append([a / sm for a in th])
+        # the softmax numerators (cat normalises the weights itself)
+        A.append([det_exp(a - mx) for a in v])
     E = []
     for t in range(T):
         if model == "iohmm-reg":
