@@ -128,7 +128,7 @@ __device__ __forceinline__ double sse_dot(const double (&a)[MMAX], const double 
 /* Stan Math softmax(v): theta = exp(v - max v); theta / sequential sum.
  * num: the numerators exp(v - max v) (the FFBS contract's weights). */
 template <int K, int MATH>
-__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K], double (&num)[K])
+__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K], double (&num)[K], double &den)
 {
     double mx = v[0];
 #pragma unroll
@@ -144,6 +144,7 @@ __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[
 #pragma unroll
     for (int i = 0; i < K; ++i)
         th[i] = num[i] / sum;
+    den = sum;
 }
 
 /* stan_softmax<K, IO_CR> together with lA[i] = dev_cr_log(A[i]) -- the same
@@ -226,8 +227,8 @@ __device__ __forceinline__ void softmax_cr_log(const double (&v)[K], double (&A)
 template <int K, int MATH>
 __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K])
 {
-    double num[K];
-    stan_softmax<K, MATH>(v, th, num);
+    double num[K], den;
+    stan_softmax<K, MATH>(v, th, num, den);
 }
 
 /* Per-lane mixture table entry (j, l): (mu, 1/s) and (log lambda, C - log s). */
@@ -252,6 +253,7 @@ struct IoStep {
     double o[K];  /* oblik_tk[t] */
     double A[K];  /* A_ij[t] (t = 0: p_1k filler) */
     double th[K]; /* the softmax numerators of A_ij[t] (FFBS weights) */
+    double den;   /* their sum */
     double lA[K]; /* log A_ij[t] (t = 0: log p_1k) */
 };
 
@@ -359,7 +361,7 @@ __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, 
             return;
         }
     }
-    stan_softmax<K, MATH>(v, st.A, st.th);
+    stan_softmax<K, MATH>(v, st.A, st.th, st.den);
     if (need_lA) {
 #pragma unroll
         for (int j = 0; j < K; ++j)
@@ -446,6 +448,11 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
     double lam = 0.0;    /* Lambda_t = sum_{2 <= tau <= t} log c_tau (unbeta pass) */
     double dl[K];        /* Viterbi delta */
     uint32_t word = 0;
+    /* the filter on the softmax numerators (no division; the sums in psum * 2^pex)
+     * wherever nothing reads the normalised s_t (unalpha) and no Viterbi shares A */
+    const bool num_filter = MATH != IO_CR && !(out & HHMM_OUT_UNALPHA);
+    double psum = 1.0;
+    int pex = 0;
     double vprev[K];     /* FFBS: v_{t-1} (p .* e_0 at t = 0, e_t after) */
     double uprev = 0.5;  /* FFBS: the uniform of step t - 1 */
     double x, xn;
@@ -468,6 +475,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                     st.A[k] = st.th[k] = pp.p[k];
                     st.lA[k] = log_A_out ? io_log<MATH>(pp.p[k]) : 0.0;
                 }
+                st.den = 1.0;
             } else {
                 io_transition<FAM, K, MMAX, MATH>(pp, M, u, st, need_lA);
             }
@@ -525,10 +533,17 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                 for (int k = 0; k < K; ++k)
                     f[k] = pp.p[k] * e[k];
             } else {
-                double s = f[0] * st.A[0];
+                /* num_filter: the softmax numerators, the sum in the log scale
+                 * (psum, pex) -- iohmm_sp_sweep's arithmetic, bit for bit */
+                double s = f[0] * (num_filter ? st.th[0] : st.A[0]);
 #pragma unroll
                 for (int i = 1; i < K; ++i)
-                    s = fma(f[i], st.A[i], s);
+                    s = fma(f[i], num_filter ? st.th[i] : st.A[i], s);
+                if (num_filter) {
+                    int pe;
+                    psum = frexp(psum * st.den, &pe);
+                    pex += pe;
+                }
                 ua_base = log(s) + (lsc + kLn2 * ex);
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -645,7 +660,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
     if (want_ffbs)
         at(a.z_ffbs + a.P * (int64_t)(Tp - 1), (uint32_t)p * 4u) = ffbs_cat<K>(vprev, uprev) + 1;
     if ((out & HHMM_OUT_LOGLIK) && a.loglik) /* target += log_sum_exp(unalpha_tk[T]) (iohmm-reg.stan:120) */
-        a.loglik[p] = log(vsum<K>(f)) + (lsc + kLn2 * ex);
+        a.loglik[p] = (log(vsum<K>(f)) + (lsc + kLn2 * ex)) - (log(psum) + kLn2 * pex);
 
     /* unbeta_tk: B_T = 1 (Q1); B_t = 1 + (Lambda_T - Lambda_t) (iohmm-reg.stan:80-98) */
     if ((out & HHMM_OUT_UNBETA) && a.unbeta) {
