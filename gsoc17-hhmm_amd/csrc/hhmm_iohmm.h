@@ -161,12 +161,13 @@ __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[
  * of log A_i, so where the rounding test passes the rounded head IS the
  * correctly rounded log; elsewhere (the rounding test fails, the exp took its
  * accurate phase, A_i within ~2^-18 of 1) the lane calls the full function. */
-/* Build knob, off by default: bit-identical (GPU parity green with it on),
- * but measured SLOWER at C3 on one box (tools/ab_workload.py: 60.95 against
- * 58.6 ms) -- the regression sweep is capped at 256 registers and the extra
- * live doubles (y, th, rho per state) grow its spill from 144 to 224 bytes. */
+/* Build knob (default on).  With w / b in registers it measured slower at C3
+ * (60.95 against 58.6 ms: the sweep is capped at 256 registers and the extra
+ * live doubles grew its spill from 144 to 224 bytes); with w / b in the LDS
+ * slab (io_wb_lds, 245 registers, no spill) it measured 53.8 against 58.5 ms
+ * (tools/ab_workload.py, one box, profiles/r02zh_ab_c3.log). */
 #ifndef HHMM_IO_ONELOG
-#define HHMM_IO_ONELOG 0
+#define HHMM_IO_ONELOG 1
 #endif
 __device__ __forceinline__ double rcp_refined(double x)
 {
@@ -237,6 +238,28 @@ __device__ __forceinline__ const double2 *mix_row(const double2 *slab, int L, in
     return slab + ((j * L + l) * 2 + f) * 64;
 }
 
+/* The regression sweep keeps w and b (2 K MMAX doubles per lane) in a per-lane
+ * LDS slab instead of registers: the correctly rounded functions of the
+ * Viterbi profile need the registers (two waves per SIMD, 256 of them), and
+ * the slab costs 16 ds_read_b128 per step against ~1,400 VALU. */
+#ifndef HHMM_IO_REG_LDSWB
+#define HHMM_IO_REG_LDSWB 1
+#endif
+template <int FAM>
+constexpr bool io_wb_lds() { return FAM == IO_REG && HHMM_IO_REG_LDSWB; }
+
+/* Row `row` of the w / b slab (rows 0..K-1: w_j, K..2K-1: b_j). */
+template <int MMAX>
+__device__ __forceinline__ void wb_row(const double2 *wb, int row, double (&r)[MMAX])
+{
+#pragma unroll
+    for (int mp = 0; mp < MMAX / 2; ++mp) {
+        const double2 v = wb[(row * (MMAX / 2) + mp) * 64];
+        r[2 * mp] = v.x;
+        r[2 * mp + 1] = v.y;
+    }
+}
+
 /* Per-lane parameters. */
 template <int FAM, int K, int MMAX>
 struct IoParams {
@@ -266,12 +289,16 @@ struct IoStep {
  * in order, max + log(sum). */
 template <int FAM, int K, int MMAX, int MATH>
 __device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, const double2 *slab, int L, int M,
-                                            double x, const double (&u)[MMAX], double (&o)[K])
+                                            double x, const double (&u)[MMAX], double (&o)[K],
+                                            const double2 *wb = nullptr)
 {
     if constexpr (FAM == IO_REG) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const double mu = sse_dot<MMAX>(u, pp.b[j], M);
+            double br[MMAX];
+            if constexpr (io_wb_lds<FAM>())
+                wb_row<MMAX>(wb, K + j, br);
+            const double mu = sse_dot<MMAX>(u, io_wb_lds<FAM>() ? br : pp.b[j], M);
             const double z = (x - mu) * pp.isig[j];
             const double z2 = z * z;
             o[j] = pp.c0[j] + (-0.5 * z2);
@@ -349,12 +376,16 @@ __device__ __forceinline__ void io_mix_factor(const double2 *slab, int L, double
  * (iohmm-reg.stan:40-49; iohmm-mix.stan:42-51, :69; iohmm-hmix.stan:36-48). */
 template <int FAM, int K, int MMAX, int MATH>
 __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, int M, const double (&u)[MMAX],
-                                              IoStep<K> &st, bool need_lA)
+                                              IoStep<K> &st, bool need_lA, const double2 *wb = nullptr)
 {
     double v[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-        v[j] = sse_dot<MMAX>(u, pp.w[j], M);
+    for (int j = 0; j < K; ++j) {
+        double wr[MMAX];
+        if constexpr (io_wb_lds<FAM>())
+            wb_row<MMAX>(wb, j, wr);
+        v[j] = sse_dot<MMAX>(u, io_wb_lds<FAM>() ? wr : pp.w[j], M);
+    }
     if constexpr (MATH == IO_CR && HHMM_IO_ONELOG) {
         if (need_lA) { /* the Viterbi's log A from the softmax's own exps */
             softmax_cr_log<K>(v, st.A, st.lA);
@@ -411,6 +442,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 
     /* ---- per-pair parameters ---- */
     IoParams<FAM, K, MMAX> pp;
+    double2 *wb = lds + (size_t)wave * K * MMAX * 64 + lane; /* io_wb_lds: K*MMAX double2 per lane */
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         pp.p[k] = a.p_1k[d + a.S * k];
@@ -419,6 +451,13 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
             pp.w[k][m] = (m < M) ? a.w_km[d + a.S * ((int64_t)k + (int64_t)K * m)] : 0.0;
             if constexpr (FAM == IO_REG)
                 pp.b[k][m] = (m < M) ? a.b_km[d + a.S * ((int64_t)k + (int64_t)K * m)] : 0.0;
+        }
+        if constexpr (io_wb_lds<FAM>()) {
+#pragma unroll
+            for (int mp = 0; mp < MMAX / 2; ++mp) {
+                wb[(k * (MMAX / 2) + mp) * 64] = make_double2(pp.w[k][2 * mp], pp.w[k][2 * mp + 1]);
+                wb[((K + k) * (MMAX / 2) + mp) * 64] = make_double2(pp.b[k][2 * mp], pp.b[k][2 * mp + 1]);
+            }
         }
         if constexpr (FAM == IO_REG) {
             const double s = a.s_k[d + a.S * k];
@@ -467,7 +506,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
              * where an output reads it */
             constexpr bool MIXF = (FAM == IO_MIX && MATH != IO_CR);
             if (!MIXF || (out & (HHMM_OUT_OBLIK_TK | HHMM_OUT_UNALPHA)))
-                io_emission<FAM, K, MMAX, MATH>(pp, slab, L, M, x, u, st.o);
+                io_emission<FAM, K, MMAX, MATH>(pp, slab, L, M, x, u, st.o, wb);
             if (t == 0) {
                 /* A_ij[1] = p_1k (filler, iohmm-reg.stan:41-42); logA_ij[1] = log(p_1k) (iohmm-hmix.stan:40) */
 #pragma unroll
@@ -477,7 +516,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                 }
                 st.den = 1.0;
             } else {
-                io_transition<FAM, K, MMAX, MATH>(pp, M, u, st, need_lA);
+                io_transition<FAM, K, MMAX, MATH>(pp, M, u, st, need_lA, wb);
             }
             if ((out & HHMM_OUT_OBLIK_TK) && a.oblik)
                 store_tk<K>(a.oblik, a, p, t, st.o);
@@ -939,7 +978,8 @@ static bool io_states(const DevArgs &a)
 template <int FAM, int K, int MMAX, int MATH, bool HOT>
 static hhmm_status launch_io5(const DevArgs &a, hipStream_t st)
 {
-    const size_t per_wave = (FAM == IO_MIX) ? (size_t)K * a.L * 2 * 64 * sizeof(double2) : 0;
+    const size_t per_wave = (FAM == IO_MIX) ? (size_t)K * a.L * 2 * 64 * sizeof(double2)
+                                            : (io_wb_lds<FAM>() ? (size_t)K * MMAX * 64 * sizeof(double2) : 0);
     int waves = 4;
     while (per_wave > 0 && waves > 1 && per_wave * waves > kLdsLimit)
         --waves;
