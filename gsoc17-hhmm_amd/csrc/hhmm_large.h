@@ -103,23 +103,27 @@ __device__ __forceinline__ double grp_sum(double v)
     return v;
 }
 
-/* Per-lane state of one pair's group. */
-template <int MODEL, int G>
+/* Per-lane state of one pair's group.  KM (<= G, a multiple of 4): the
+ * state capacity of the compile-time loops and of the per-lane K-vectors
+ * (column / row of A, the exchanged state vector): 24 for 16 < K <= 24 keeps
+ * the forward-backward at two waves per SIMD (lanes 24..31 of the group stay
+ * idle without a register copy of their neutral entries). */
+template <int MODEL, int G, int KM>
 struct LkLane {
     int j;          /* this lane's state (>= K: idle) */
     bool on;        /* j < K */
     int64_t p, n, d;
     int Tp, K, L;
-    double col[G]; /* A[i][j] (probabilities; Viterbi: log) */
-    double row[G]; /* A[j][i] (backward) */
+    double col[KM]; /* A[i][j] (probabilities; Viterbi: log) */
+    double row[KM]; /* A[j][i] (backward) */
     double pj;       /* p_1k[j] */
     double mu, isig, c0, lsig; /* gauss, state j */
     double *xch;     /* this pair's LDS exchange slots: 2 x G doubles */
     const double *tab; /* multinomial: this pair's [L][G] emission table */
 };
 
-template <int MODEL, int G>
-__device__ __forceinline__ void lk_setup(LkLane<MODEL, G> &ln, const DevArgs &a, double *lds, bool LOG)
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ void lk_setup(LkLane<MODEL, G, KM> &ln, const DevArgs &a, double *lds, bool LOG)
 {
     const int tid = threadIdx.x;
     const int g = tid / G;                 /* group in the workgroup */
@@ -133,9 +137,9 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G> &ln, const DevArgs &a,
     ln.Tp = pair_len(a, ln.n);
     const int jj = ln.on ? ln.j : 0;
     const int64_t S = a.S, d = ln.d;
-    double rawc[G], rawr[G];
+    double rawc[KM], rawr[KM];
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
+    for (int i = 0; i < KM; ++i) {
         rawc[i] = 0.0;
         rawr[i] = 0.0;
         if (i < a.K) {
@@ -144,7 +148,7 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G> &ln, const DevArgs &a,
         }
     }
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
+    for (int i = 0; i < KM; ++i) {
         ln.col[i] = (LOG && i < a.K) ? dev_cr_log(rawc[i]) : rawc[i];
         ln.row[i] = rawr[i];
     }
@@ -185,8 +189,8 @@ struct LkObs {
     double xr;
 };
 
-template <int MODEL, int G>
-__device__ __forceinline__ LkObs<MODEL, G> lk_block(const LkLane<MODEL, G> &ln, const DevArgs &a, int b)
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ LkObs<MODEL, G> lk_block(const LkLane<MODEL, G, KM> &ln, const DevArgs &a, int b)
 {
     const int tc = min(max(b * G + ln.j, 0), a.Tmax - 1);
     LkObs<MODEL, G> o;
@@ -244,8 +248,8 @@ __device__ __forceinline__ void lk_get(const LkObs<MODEL, G> &blk, int u, int &x
 }
 
 /* Stan's normal_lpdf(y | mu_j, sigma_j), as gauss_lpdf. */
-template <int MODEL, int G>
-__device__ __forceinline__ double lk_lpdf(const LkLane<MODEL, G> &ln, double y)
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ double lk_lpdf(const LkLane<MODEL, G, KM> &ln, double y)
 {
     const double z = (y - ln.mu) * ln.isig;
     const double z2 = z * z;
@@ -254,11 +258,11 @@ __device__ __forceinline__ double lk_lpdf(const LkLane<MODEL, G> &ln, double y)
 
 /* Linear-space emission e_t(j) and its log scale m (gauss: densities over
  * their group max, as emit_prob); idle lanes 0. */
-template <int MODEL, int G>
-__device__ __forceinline__ double lk_emit(const LkLane<MODEL, G> &ln, int x, double xr, double &m)
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ double lk_emit(const LkLane<MODEL, G, KM> &ln, int x, double xr, double &m)
 {
     if constexpr (LkTraits<MODEL>::kGauss) {
-        const double lp = ln.on ? lk_lpdf<MODEL, G>(ln, xr) : dev_ninf();
+        const double lp = ln.on ? lk_lpdf<MODEL, G, KM>(ln, xr) : dev_ninf();
         m = grp_max<G>(lp);
         return ln.on ? exp(lp - m) : 0.0;
     } else {
@@ -270,8 +274,8 @@ __device__ __forceinline__ double lk_emit(const LkLane<MODEL, G> &ln, int x, dou
 
 /* The group's vector v (this lane's entry) through LDS slot `slot`: w[i] = v
  * of lane i for all G lanes (idle lanes carry the neutral entry). */
-template <int G>
-__device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, double v, double (&w)[G])
+template <int G, int KM>
+__device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, double v, double (&w)[KM])
 {
     double *s = xch + slot * G;
     s[j] = v;
@@ -282,7 +286,7 @@ __device__ __forceinline__ void grp_exchange(double *xch, int slot, int j, doubl
     __asm__ __volatile__("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < G; i += 2) {
+    for (int i = 0; i < KM; i += 2) {
         const double2 q = *reinterpret_cast<const double2 *>(s + i);
         w[i] = q.x;
         w[i + 1] = q.y;
@@ -302,54 +306,54 @@ __device__ __forceinline__ double grp_renorm(double v, int &ex)
 /* sum_i w_i c_i over the G entries (idle ones 0 x 0) as four interleaved fma
  * chains (a quarter of the dependent latency of one chain; the posteriors are
  * tolerance outputs, 1e-9 relative, so the association is free) */
-template <int G>
-__device__ __forceinline__ double lk_dot(const double (&w)[G], const double (&c)[G])
+template <int KM>
+__device__ __forceinline__ double lk_dot(const double (&w)[KM], const double (&c)[KM])
 {
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int i = 0; i < G; ++i)
+    for (int i = 0; i < KM; ++i)
         acc[i & 3] = fma(w[i], c[i], acc[i & 3]);
     return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 /* alpha_t(j) = e_t(j) * sum_i alpha_{t-1}(i) A(i, j) (fwd_step_raw) */
-template <int MODEL, int G>
-__device__ __forceinline__ double lk_fwd(const LkLane<MODEL, G> &ln, const double (&w)[G], double e)
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ double lk_fwd(const LkLane<MODEL, G, KM> &ln, const double (&w)[KM], double e)
 {
-    return ln.on ? lk_dot<G>(w, ln.col) * e : 0.0;
+    return ln.on ? lk_dot<KM>(w, ln.col) * e : 0.0;
 }
 
 /* beta_{t-1}(j) = sum_i A(j, i) b_i, b_i = e_t(i) beta_t(i) (bwd_step) */
-template <int MODEL, int G>
-__device__ __forceinline__ double lk_bwd(const LkLane<MODEL, G> &ln, const double (&w)[G])
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ double lk_bwd(const LkLane<MODEL, G, KM> &ln, const double (&w)[KM])
 {
-    return ln.on ? lk_dot<G>(w, ln.row) : 0.0;
+    return ln.on ? lk_dot<KM>(w, ln.row) : 0.0;
 }
 
-template <int MODEL, int G>
-__device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLane<MODEL, G> &ln, int t, double v)
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLane<MODEL, G, KM> &ln, int t, double v)
 {
     if (ln.on && out)
         out[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
 }
 
 /* Forward-backward: loglik, alpha, beta, ungamma, gamma. */
-template <int MODEL, int G>
+template <int MODEL, int G, int KM>
 __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
-    LkLane<MODEL, G> ln;
-    lk_setup<MODEL, G>(ln, a, lds, false);
+    LkLane<MODEL, G, KM> ln;
+    lk_setup<MODEL, G, KM>(ln, a, lds, false);
     const uint32_t out = a.outputs;
     const bool need_bwd = (out & (HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
     const int Tp = ln.Tp; /* per pair: uniform over the group (the wave's two groups may differ) */
     const int K = ln.K;
-    double w[G];
+    double w[KM];
     int slot = 0;
     auto ckpt = [&](int c) -> double & { return a.ckpt[ln.p + a.P * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
 
     /* ---- forward: alpha_1 (hmm.stan:30 Q2 / hmm-multinom.stan:31), then the recursion ---- */
-    LkObs<MODEL, G> bcur = lk_block<MODEL, G>(ln, a, 0), bnxt = lk_block<MODEL, G>(ln, a, 1);
+    LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, 0), bnxt = lk_block<MODEL, G, KM>(ln, a, 1);
     double al, lsc = 0.0;
     int ex = 0;
     {
@@ -363,7 +367,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             lsc += grp_sum<G>(tk);
             al = ln.on ? ln.pj : 0.0;
         } else {
-            const double e = lk_emit<MODEL, G>(ln, x, xr, m);
+            const double e = lk_emit<MODEL, G, KM>(ln, x, xr, m);
             al = ln.on ? ln.pj * e : 0.0;
         }
         al = grp_renorm<G>(al, ex);
@@ -372,25 +376,25 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         if (ln.on)
             ckpt(0) = al;
     } else if ((out & HHMM_OUT_ALPHA) && a.alpha) {
-        lk_put<MODEL, G>(a.alpha, a, ln, 0, al / grp_sum<G>(al));
+        lk_put<MODEL, G, KM>(a.alpha, a, ln, 0, al / grp_sum<G>(al));
     }
     for (int t = 1; t < Tp; ++t) {
         const int u = t % G;
         if (u == 0) { /* group-uniform: next block of observations, prefetch the one after */
             bcur = bnxt;
-            bnxt = lk_block<MODEL, G>(ln, a, t / G + 1);
+            bnxt = lk_block<MODEL, G, KM>(ln, a, t / G + 1);
         }
         int x;
         double xr, m;
         lk_get<MODEL, G>(bcur, u, x, xr);
-        const double e = lk_emit<MODEL, G>(ln, x, xr, m);
-        grp_exchange<G>(ln.xch, slot, ln.j, al, w);
+        const double e = lk_emit<MODEL, G, KM>(ln, x, xr, m);
+        grp_exchange<G, KM>(ln.xch, slot, ln.j, al, w);
         slot ^= 1;
         lsc += m;
-        al = grp_renorm<G>(lk_fwd<MODEL, G>(ln, w, e), ex);
+        al = grp_renorm<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex);
         if (!need_bwd) {
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
-                lk_put<MODEL, G>(a.alpha, a, ln, t, al / grp_sum<G>(al));
+                lk_put<MODEL, G, KM>(a.alpha, a, ln, t, al / grp_sum<G>(al));
         } else if (t % kLChunk == 0 && ln.on) {
             ckpt(t / kLChunk) = al;
         }
@@ -411,13 +415,13 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     constexpr int CPB = G / kLChunk; /* chunks per observation block */
     const int nck = (Tp + kLChunk - 1) / kLChunk;
     int cb = (nck - 1) / CPB;
-    LkObs<MODEL, G> ob = lk_block<MODEL, G>(ln, a, cb), obp = lk_block<MODEL, G>(ln, a, cb - 1);
+    LkObs<MODEL, G> ob = lk_block<MODEL, G, KM>(ln, a, cb), obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
     double ck = ckpt(nck - 1), ckn = ckpt(max(nck - 2, 0));
     for (int c = nck - 1; c >= 0; --c) {
         if (c / CPB != cb) { /* group-uniform: step back one observation block */
             cb = c / CPB;
             ob = obp;
-            obp = lk_block<MODEL, G>(ln, a, cb - 1);
+            obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
         }
         const int t0 = c * kLChunk;
         const int ub = t0 % G; /* the chunk's first step inside the block */
@@ -427,7 +431,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             int x;
             double xr, m;
             lk_get_var<MODEL, G>(ob, ub + u, x, xr);
-            es[u] = lk_emit<MODEL, G>(ln, x, xr, m);
+            es[u] = lk_emit<MODEL, G, KM>(ln, x, xr, m);
         }
         double abuf[kLChunk];
         abuf[0] = ln.on ? ck : 0.0;
@@ -438,9 +442,9 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         for (int u = 1; u < kLChunk; ++u) {
             abuf[u] = 0.0;
             if (t0 + u < Tp) { /* group-uniform */
-                grp_exchange<G>(ln.xch, slot, ln.j, abuf[u - 1], w);
+                grp_exchange<G, KM>(ln.xch, slot, ln.j, abuf[u - 1], w);
                 slot ^= 1;
-                abuf[u] = grp_renorm<G>(lk_fwd<MODEL, G>(ln, w, es[u]), exb);
+                abuf[u] = grp_renorm<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb);
             }
         }
 #pragma unroll
@@ -451,23 +455,23 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             const double av = abuf[u];
             const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
-                lk_put<MODEL, G>(a.alpha, a, ln, t, av / sa);
+                lk_put<MODEL, G, KM>(a.alpha, a, ln, t, av / sa);
             if ((out & HHMM_OUT_BETA) && a.beta)
-                lk_put<MODEL, G>(a.beta, a, ln, t, be / sb);
+                lk_put<MODEL, G, KM>(a.beta, a, ln, t, be / sb);
             if (out & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
                 /* gamma = normalize(alpha .* beta) from the normalised vectors (hmm.stan:89-96) */
                 const double ug = (av / sa) * (be / sb);
                 if ((out & HHMM_OUT_UNGAMMA) && a.ungamma)
-                    lk_put<MODEL, G>(a.ungamma, a, ln, t, ug);
+                    lk_put<MODEL, G, KM>(a.ungamma, a, ln, t, ug);
                 if ((out & HHMM_OUT_GAMMA) && a.gamma) {
                     const double sg = grp_sum<G>(ug);
-                    lk_put<MODEL, G>(a.gamma, a, ln, t, ug / sg);
+                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug / sg);
                 }
             }
             if (t > 0) {
-                grp_exchange<G>(ln.xch, slot, ln.j, es[u] * be, w);
+                grp_exchange<G, KM>(ln.xch, slot, ln.j, es[u] * be, w);
                 slot ^= 1;
-                be = grp_renorm<G>(lk_bwd<MODEL, G>(ln, w), bex);
+                be = grp_renorm<G>(lk_bwd<MODEL, G, KM>(ln, w), bex);
             }
         }
     }
@@ -477,7 +481,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
 
 /* SSE2 maxCoeff order of stan_max_vec for a runtime K (oracle stan_max_vec). */
 template <int G>
-__device__ __forceinline__ double stan_max_rt(const double (&d)[G], int n)
+__device__ __forceinline__ double stan_max_rt(const double (&d)[G], int n) /* G: the array capacity */
 {
     if (n < 2)
         return d[0];
@@ -513,19 +517,19 @@ __device__ __forceinline__ double stan_max_rt(const double (&d)[G], int n)
     return res;
 }
 
-template <int MODEL, int G>
+template <int MODEL, int G, int KM>
 __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
-    LkLane<MODEL, G> ln;
-    lk_setup<MODEL, G>(ln, a, lds, true);
+    LkLane<MODEL, G, KM> ln;
+    lk_setup<MODEL, G, KM>(ln, a, lds, true);
     const int Tp = ln.Tp;
     const int K = ln.K;
-    double w[G];
+    double w[KM];
     int slot = 0;
     auto emit_log = [&](int x, double xr) -> double {
         if constexpr (LkTraits<MODEL>::kGauss)
-            return ln.on ? lk_lpdf<MODEL, G>(ln, xr) : 0.0;
+            return ln.on ? lk_lpdf<MODEL, G, KM>(ln, xr) : 0.0;
         else
             return ln.on ? ln.tab[(min(max(x, 1), ln.L) - 1) * G + ln.j] : 0.0;
     };
@@ -535,7 +539,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
     uint8_t *bp = reinterpret_cast<uint8_t *>(a.bp) + ((int64_t)ln.p * K + (ln.on ? ln.j : 0)) * Tb;
 
     /* delta_tk[1, K] = emission of state K only (Q3: the others keep NaN) */
-    LkObs<MODEL, G> bcur = lk_block<MODEL, G>(ln, a, 0), bnxt = lk_block<MODEL, G>(ln, a, 1);
+    LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, 0), bnxt = lk_block<MODEL, G, KM>(ln, a, 1);
     int x;
     double xr;
     lk_get<MODEL, G>(bcur, 0, x, xr);
@@ -545,18 +549,18 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
         const int u = t % G;
         if (u == 0) {
             bcur = bnxt;
-            bnxt = lk_block<MODEL, G>(ln, a, t / G + 1);
+            bnxt = lk_block<MODEL, G, KM>(ln, a, t / G + 1);
         }
         lk_get<MODEL, G>(bcur, u, x, xr);
         const double le = emit_log(x, xr);
-        grp_exchange<G>(ln.xch, slot, ln.j, dl, w);
+        grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
         slot ^= 1;
         /* candidate (delta + log A) + emission, strict '>' from -inf; the
          * running max as fmax (vit_step): NaN never wins, first i on ties */
         double best = dev_ninf();
         int arg = 0;
 #pragma unroll
-        for (int i = 0; i < G; ++i) { /* idle i: delta -inf, never greater */
+        for (int i = 0; i < KM; ++i) { /* idle i: delta -inf, never greater */
             const double cand = (w[i] + ln.col[i]) + le;
             const bool gt = cand > best;
             best = fmax(best, cand);
@@ -567,11 +571,11 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
             bp[t] = (uint8_t)arg;
     }
     /* logp_zstar = max(delta_T) (SSE2 order); zstar_T = LAST j attaining it */
-    grp_exchange<G>(ln.xch, slot, ln.j, dl, w);
-    const double lp = stan_max_rt<G>(w, K);
+    grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
+    const double lp = stan_max_rt<KM>(w, K);
     int z = -1;
 #pragma unroll
-    for (int j = 0; j < G; ++j)
+    for (int j = 0; j < KM; ++j)
         if (j < K && w[j] == lp)
             z = j;
     const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
@@ -628,7 +632,7 @@ static inline size_t lk_lds(const DevArgs &a, int threads, bool discrete)
     return groups * 2 * G * sizeof(double) + (discrete ? groups * (size_t)a.L * G * sizeof(double) : 0);
 }
 
-template <int MODEL, int G>
+template <int MODEL, int G, int KM>
 static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
 {
     constexpr bool discrete = !LkTraits<MODEL>::kGauss;
@@ -649,17 +653,27 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
     }
     const int gpb = threads / G;
     const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
-    /* checkpoints use the [rows][K][P] layout of the lane kernels */
-    if (out & fb)
-        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
+    /* checkpoints use the [rows][K][P] layout of the lane kernels.  With both
+     * halves requested the decoder runs on the library's side stream, forked
+     * from and joined back into the caller's: the two kernels' registers fit
+     * one wave of each per SIMD (K <= 24: 224 + 160), so they overlap */
+    hipStream_t vs = st;
+    if ((out & fb) && (out & vit) && !(a.flags & HHMM_FLAG_NO_FUSE)) {
+        const hhmm_status r = fork_stream(st, &vs);
+        if (r != HHMM_OK)
+            return r;
+    }
     if (out & vit)
-        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
+        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), vs, a);
+    if (out & fb)
+        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
     hipError_t e = hipGetLastError();
+    const hhmm_status j = (vs != st) ? join_stream(st, vs) : HHMM_OK;
     if (e != hipSuccess) {
         set_error("large-K kernel launch: %s", hipGetErrorString(e));
         return HHMM_ERR_HIP;
     }
-    return HHMM_OK;
+    return j;
 }
 
 } // namespace hhmm

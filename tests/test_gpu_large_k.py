@@ -22,14 +22,14 @@ def run_both(engine, oracle, model, data, draws, pars=PARS, pairing="grid"):
     assert got["status"] == ref["status"]
 
 
-@pytest.mark.parametrize("K", [9, 12, 16, 23, 32])
+@pytest.mark.parametrize("K", [9, 12, 16, 17, 23, 24, 25, 32])
 @pytest.mark.parametrize("T", [1, 2, 37, 300])
 def test_multinom_large_K(engine, oracle, K, T):
     data, draws = synth.hmm_multinom(N=3, S=21, T=T, K=K, L=9)
     run_both(engine, oracle, "hmm-multinom", data, draws)
 
 
-@pytest.mark.parametrize("K", [12, 23])
+@pytest.mark.parametrize("K", [12, 23, 25])
 @pytest.mark.parametrize("T", [1, 2, 130])
 def test_gauss_large_K(engine, oracle, K, T):
     data, draws = synth.hmm_gauss(N=2, S=17, T=T, K=K)
