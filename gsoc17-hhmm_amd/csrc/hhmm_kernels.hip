@@ -105,9 +105,17 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
         return sp;
     const int C = fb_chunk(K);
     const int log2cl = (int)((flags >> 8) & 0xffu);
+    /* a batch of under 16384 pairs (256 waves: a quarter of the chip's SIMDs)
+     * is latency-bound on its T sequential steps already at T of a few hundred:
+     * chunks of 4 C steps (C1, 1000 pairs x T = 500: 0.32 -> 0.10 ms) */
+    const bool small = P < 16384 && Tmax >= 256;
     int cl;
     if (log2cl > 0) {
         cl = 1 << log2cl;
+    } else if (small) {
+        cl = 4 * C;
+        while ((int64_t)P * ((Tmax + cl - 1) / cl) > 524288 && cl < 65536)
+            cl *= 2;
     } else {
         const int64_t want = (int64_t)Tmax * P / 524288;
         cl = 8 * C;
@@ -118,7 +126,9 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
         cl = C;
     cl -= cl % C;
     const int nc = (Tmax + cl - 1) / cl;
-    if (!(flags & HHMM_FLAG_SCAN_FORCE) && (P >= 131072 || Tmax < 16384 || nc < 4))
+    if (!(flags & HHMM_FLAG_SCAN_FORCE) && !small && (P >= 131072 || Tmax < 16384 || nc < 4))
+        return sp;
+    if (!(flags & HHMM_FLAG_SCAN_FORCE) && nc < 4)
         return sp;
     if (scan_lanes_per_chunk(P) * nc >= (int64_t(1) << 29)) /* checkpoint columns are 32-bit byte offsets */
         return sp;
