@@ -49,10 +49,22 @@
  * chunk exits disagree is decoded sequentially.
  */
 #pragma once
+#include <type_traits>
 
 namespace hhmm {
 
 constexpr int32_t kVsTie = 1 << 30;     /* vs_k: a grid rounding tie inside the chunk */
+#ifndef HHMM_VS_APPROX_F32
+#define HHMM_VS_APPROX_F32 1 /* the approximate product pass in float */
+#endif
+/* Discrete models' tie products inside the grid pass (1) or in
+ * vs_prod_tie_kernel (0).  Out of line the grid pass drops from 293 to 125
+ * registers, but the extra launch over every (pair, chunk, parity) lane cost
+ * more at C5 than the occupancy gained: 14.17 against 13.78 ms (one box,
+ * profiles/r02zl_ab_c5.log; the float approximate pass alone 13.46). */
+#ifndef HHMM_VS_TIE_INLINE
+#define HHMM_VS_TIE_INLINE 1
+#endif
 constexpr int32_t kVsNoGrid = -(1 << 20); /* vs_k: no finite magnitude estimate */
 constexpr int32_t kVsSeq = -(1 << 21);    /* vs_k after the exact scan: the chunk was decoded step by step */
 
@@ -234,8 +246,9 @@ __device__ __forceinline__ void vs_tie_product(const DevArgs &a, const VsLane &v
             out[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = M[r][j] * u;
 }
 
-/* Gaussian emissions (continuous log densities: a tie shows up during the
- * grid pass): the tie chunks' two parity products, one lane per parity. */
+/* The tie chunks' two parity products, one lane per parity, for the chunks
+ * the grid pass flagged (kVsTie): Gaussian emissions (a tie shows up during
+ * the pass), and discrete models when HHMM_VS_TIE_INLINE is 0. */
 template <int MODEL, int K>
 __global__ void __launch_bounds__(kBlock) vs_prod_tie_kernel(const DevArgs a)
 {
@@ -314,8 +327,11 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
                 any = any || vs_term(e.x, iu).tie || (2 * kp + 1 < K && vs_term(e.y, iu).tie);
             }
         if (any) {
-            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 0.0, a.vs_m);
-            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 1.0, a.vs_m1);
+            /* the two parity products (HHMM_VS_TIE_INLINE) */
+            if (HHMM_VS_TIE_INLINE) {
+                vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 0.0, a.vs_m);
+                vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 1.0, a.vs_m1);
+            }
             a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
             return;
         }
@@ -327,12 +343,23 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
             for (int j = 0; j < K; ++j)
                 pp.A[i][j] = vs_grid(pp.A[i][j], iu, u, tie);
     }
-    double M[K][K];
+    /* the approximate pass (GRID = false) only predicts the binade of each
+     * chunk's entry for the exact pass, which checks it: its products run in
+     * float (half the registers; the exact scan decodes a chunk whose entry
+     * misses the predicted binade step by step) */
+    using V = typename std::conditional<GRID || !HHMM_VS_APPROX_F32, double, float>::type;
+    V Av[K][K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            Av[i][j] = (V)pp.A[i][j];
+    V M[K][K];
 #pragma unroll
     for (int r = 0; r < K; ++r)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            M[r][j] = (r == j) ? 0.0 : dev_ninf();
+            M[r][j] = (r == j) ? (V)0.0 : (V)dev_ninf();
     if constexpr (GRID && ModelTraits<MODEL>::kDiscrete) {
         /* the emission table on the grid, once (no tie: checked above) */
         for (int l = 0; l < a.L; ++l)
@@ -349,18 +376,20 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
         double le[K];
         emit_log<MODEL, K>(pp, slab, a.L, o, le);
         bool on[K];
+        V lv[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             if constexpr (GRID && ModelTraits<MODEL>::kGauss)
                 le[j] = vs_grid(le[j], iu, u, tie);
+            lv[j] = (V)le[j];
             on[j] = true;
             if constexpr (ModelTraits<MODEL>::kTayal)
                 on[j] = tayal_pred(o.aux, j);
         }
 #pragma unroll
         for (int r = 0; r < K; ++r) {
-            double nm[K];
-            double rm = M[r][0];
+            V nm[K];
+            V rm = M[r][0];
             if constexpr (ModelTraits<MODEL>::kTayal) {
 #pragma unroll
                 for (int i = 1; i < K; ++i)
@@ -368,16 +397,16 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
             }
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-                double best;
+                V best;
                 if (ModelTraits<MODEL>::kTayal && !on[j]) {
                     best = rm;
                 } else {
-                    best = M[r][0] + pp.A[0][j];
+                    best = M[r][0] + Av[0][j];
 #pragma unroll
                     for (int i = 1; i < K; ++i)
-                        best = fmax(best, M[r][i] + pp.A[i][j]);
+                        best = fmax(best, M[r][i] + Av[i][j]);
                 }
-                nm[j] = best + le[j];
+                nm[j] = best + lv[j];
             }
 #pragma unroll
             for (int j = 0; j < K; ++j)
@@ -388,7 +417,7 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
     for (int r = 0; r < K; ++r)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            a.vs_m[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = M[r][j];
+            a.vs_m[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = (double)M[r][j];
     if (GRID && tie)
         a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid; /* |delta| < 1: decode it */
 }
@@ -999,7 +1028,7 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, false>), gc, bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, true>), gc, bc, lds_c, st, a);
-        if (ModelTraits<MODEL>::kGauss) /* discrete models resolve their ties inside the grid pass */
+        if (ModelTraits<MODEL>::kGauss || !HHMM_VS_TIE_INLINE)
             hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3((unsigned)((2 * lanes + kBlock - 1) / kBlock)), bc,
                                lds_c, st, a);
         hipLaunchKernelGGL((vs_scan1_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
