@@ -54,6 +54,14 @@ HHMM_MATH_FN double hhmm_det_pow2(int k)
     return hhmm_det_bits((uint64_t)(k + 1023) << 52);
 }
 
+/* HHMM_DET_K(c): a polynomial coefficient.  The device build defines it as a
+ * register-class hint that keeps the double in a scalar register pair, so
+ * each Horner step is one fma with a scalar operand instead of two 32-bit
+ * literal moves and an fma; the value (and so every result) is unchanged. */
+#ifndef HHMM_DET_K
+#define HHMM_DET_K(c) (c)
+#endif
+
 HHMM_MATH_FN double hhmm_det_exp(double x)
 {
     /* clamp into [-746, 710]: below, exp rounds to 0; above, to +inf -- the
@@ -63,16 +71,16 @@ HHMM_MATH_FN double hhmm_det_exp(double x)
     double r = __builtin_fma(-kd, HHMM_DET_LN2_HI, xc);
     r = __builtin_fma(-kd, HHMM_DET_LN2_LO, r);
     double p = 0x1.6124613a86d09p-33;
-    p = __builtin_fma(p, r, 0x1.1eed8eff8d898p-29);
-    p = __builtin_fma(p, r, 0x1.ae64567f544e4p-26);
-    p = __builtin_fma(p, r, 0x1.27e4fb7789f5cp-22);
-    p = __builtin_fma(p, r, 0x1.71de3a556c734p-19);
-    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-16);
-    p = __builtin_fma(p, r, 0x1.a01a01a01a01ap-13);
-    p = __builtin_fma(p, r, 0x1.6c16c16c16c17p-10);
-    p = __builtin_fma(p, r, 0x1.1111111111111p-7);
-    p = __builtin_fma(p, r, 0x1.5555555555555p-5);
-    p = __builtin_fma(p, r, 0x1.5555555555555p-3);
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.1eed8eff8d898p-29));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.ae64567f544e4p-26));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.27e4fb7789f5cp-22));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.71de3a556c734p-19));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.a01a01a01a01ap-16));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.a01a01a01a01ap-13));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.6c16c16c16c17p-10));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.1111111111111p-7));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.5555555555555p-5));
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.5555555555555p-3));
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     p = __builtin_fma(p, r, 1.0);
@@ -95,15 +103,15 @@ HHMM_MATH_FN double hhmm_det_log(double x)
     const double s = (m - 1.0) / (m + 1.0); /* m - 1 exact */
     const double s2 = s * s;
     double q = 0x1.8618618618618p-4;
-    q = __builtin_fma(q, s2, 0x1.af286bca1af28p-4);
-    q = __builtin_fma(q, s2, 0x1.e1e1e1e1e1e1ep-4);
-    q = __builtin_fma(q, s2, 0x1.1111111111111p-3);
-    q = __builtin_fma(q, s2, 0x1.3b13b13b13b14p-3);
-    q = __builtin_fma(q, s2, 0x1.745d1745d1746p-3);
-    q = __builtin_fma(q, s2, 0x1.c71c71c71c71cp-3);
-    q = __builtin_fma(q, s2, 0x1.2492492492492p-2);
-    q = __builtin_fma(q, s2, 0x1.999999999999ap-2);
-    q = __builtin_fma(q, s2, 0x1.5555555555555p-1);
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.af286bca1af28p-4));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.e1e1e1e1e1e1ep-4));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.1111111111111p-3));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.3b13b13b13b14p-3));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.745d1745d1746p-3));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.c71c71c71c71cp-3));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.2492492492492p-2));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.999999999999ap-2));
+    q = __builtin_fma(q, s2, HHMM_DET_K(0x1.5555555555555p-1));
     const double lm = __builtin_fma(s * s2, q, 2.0 * s);
     const double E = (double)e;
     const double y = __builtin_fma(E, HHMM_DET_LN2_HI, __builtin_fma(E, HHMM_DET_LN2_LO, lm));

@@ -15,6 +15,14 @@
 #define HHMM_MATH_TABLE static __constant__
 #endif
 #include "hhmm_crmath.h"
+/* hhmm_detmath.h's coefficients through a scalar-register-class hint (an
+ * empty asm: no instruction, value unchanged) */
+static __device__ __forceinline__ double hhmm_det_sgpr(double c)
+{
+    __asm__("" : "+s"(c));
+    return c;
+}
+#define HHMM_DET_K(c) hhmm_det_sgpr(c)
 #include "hhmm_detmath.h"
 
 namespace hhmm {
