@@ -346,6 +346,8 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     lk_setup<MODEL, G, KM>(ln, a, lds, false);
     const uint32_t out = a.outputs;
     const bool need_bwd = (out & (HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
+    const bool gamma_only = (out & (HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) ==
+                            HHMM_OUT_GAMMA && a.gamma;
     const int Tp = ln.Tp; /* per pair: uniform over the group (the wave's two groups may differ) */
     const int K = ln.K;
     double w[KM];
@@ -453,6 +455,21 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             if (t >= Tp)
                 continue;
             const double av = abuf[u];
+            if (gamma_only) {
+                /* gamma = (alpha .* beta) / sum: the normalisations cancel, one
+                 * group sum per step instead of three (emit_posteriors' FB_GAMMA
+                 * form); the reference's normalised-vector formula where the
+                 * product underflows (group-uniform test) */
+                const double ug = av * be;
+                const double sg = grp_sum<G>(ug);
+                if (sg > 0x1p-960) {
+                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug / sg);
+                } else {
+                    const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
+                    const double un = (av / sa) * (be / sb);
+                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, un / grp_sum<G>(un));
+                }
+            } else {
             const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
                 lk_put<MODEL, G, KM>(a.alpha, a, ln, t, av / sa);
@@ -467,6 +484,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
                     const double sg = grp_sum<G>(ug);
                     lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug / sg);
                 }
+            }
             }
             if (t > 0) {
                 grp_exchange<G, KM>(ln.xch, slot, ln.j, es[u] * be, w);
