@@ -43,6 +43,13 @@ namespace hhmm {
 
 constexpr int kLChunk = 8;  /* steps per forward checkpoint */
 constexpr int kLBack = 16;  /* backtrack steps per back-pointer chunk */
+/* The filters renormalise (a group max, an exact power of two) every kLRenorm
+ * steps, not every step: the group max is a five-level reduction on the
+ * step's dependency chain, and between renormalisations the vectors shrink by
+ * the per-step factor only (emission x transition mass, ~1e-4 over four
+ * steps), far above the subnormal range.  A multiple-of-kLRenorm step (every
+ * checkpoint step) is always renormalised. */
+constexpr int kLRenorm = 4;
 
 /* bytes per (pair, state) back-pointer row */
 __host__ __device__ constexpr int lk_row_bytes(int Tmax) { return (Tmax + 15) & ~15; }
@@ -303,6 +310,13 @@ __device__ __forceinline__ double grp_renorm(double v, int &ex)
     return ldexp(v, -e);
 }
 
+/* grp_renorm on every kLRenorm-th step t */
+template <int G>
+__device__ __forceinline__ double grp_renorm_at(double v, int &ex, int t)
+{
+    return (t % kLRenorm == 0) ? grp_renorm<G>(v, ex) : v;
+}
+
 /* sum_i w_i c_i over the G entries (idle ones 0 x 0) as four interleaved fma
  * chains (a quarter of the dependent latency of one chain; the posteriors are
  * tolerance outputs, 1e-9 relative, so the association is free) */
@@ -393,7 +407,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         grp_exchange<G, KM>(ln.xch, slot, ln.j, al, w);
         slot ^= 1;
         lsc += m;
-        al = grp_renorm<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex);
+        al = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex, t);
         if (!need_bwd) {
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
                 lk_put<MODEL, G, KM>(a.alpha, a, ln, t, al / grp_sum<G>(al));
@@ -446,7 +460,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             if (t0 + u < Tp) { /* group-uniform */
                 grp_exchange<G, KM>(ln.xch, slot, ln.j, abuf[u - 1], w);
                 slot ^= 1;
-                abuf[u] = grp_renorm<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb);
+                abuf[u] = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb, t0 + u);
             }
         }
 #pragma unroll
@@ -489,7 +503,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             if (t > 0) {
                 grp_exchange<G, KM>(ln.xch, slot, ln.j, es[u] * be, w);
                 slot ^= 1;
-                be = grp_renorm<G>(lk_bwd<MODEL, G, KM>(ln, w), bex);
+                be = grp_renorm_at<G>(lk_bwd<MODEL, G, KM>(ln, w), bex, t);
             }
         }
     }
