@@ -329,25 +329,29 @@ __device__ __forceinline__ void fwd_step_raw(const double (&al)[K], double (&out
         out[j] = s[j] * e[j];
 }
 
+/* rn: renormalise after this step (every step, except the FB_BIG gamma
+ * profile's every kBigRenorm-th; the flag is a compile-time constant after
+ * unrolling) */
 template <int MODEL, int K>
 __device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
-                                            const double (&e)[K], const Obs &o, int &ex)
+                                            const double (&e)[K], const Obs &o, int &ex, bool rn = true)
 {
     fwd_step_raw<MODEL, K>(al, out, pp, e, o);
-    renorm<K>(out, ex);
+    if (rn)
+        renorm<K>(out, ex);
 }
 
 template <int MODEL, int K>
 __device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL, K> &pp, const double (&e)[K],
-                                         const Obs &o, int &ex)
+                                         const Obs &o, int &ex, bool rn = true)
 {
-    fwd_step_to<MODEL, K>(al, al, pp, e, o, ex);
+    fwd_step_to<MODEL, K>(al, al, pp, e, o, ex, rn);
 }
 
 /* beta_{t-1} from beta_t and step t's emission / masks. */
 template <int MODEL, int K>
 __device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL, K> &pp,
-                                         const double (&e)[K], const Obs &o, int &ex)
+                                         const double (&e)[K], const Obs &o, int &ex, bool rn = true)
 {
     double b[K];
 #pragma unroll
@@ -374,7 +378,8 @@ __device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL
 #pragma unroll
     for (int j = 0; j < K; ++j)
         be[j] = s[j];
-    renorm<K>(be, ex);
+    if (rn)
+        renorm<K>(be, ex);
 }
 
 /* alpha_1 (t = 0) from the step-0 observation / emission. */
@@ -458,6 +463,14 @@ constexpr int kBigChunk = 16; /* checkpoint interval of FB_BIG (a multiple of fb
  * (loglik, checkpoints, packed symbols) and then the backward sweep, with the
  * Viterbi decoding the packed symbols beside the latter. */
 enum FbPhase { FB_PH_BOTH = 0, FB_PH_FWD = 1, FB_PH_BWD = 2 };
+/* FB_BIG renormalises every kBigRenorm-th step (every checkpoint step
+ * included): the max-exponent renormalisation is ~9 VALU on each step's
+ * chain, and over four steps the state only shrinks by the emission x
+ * transition mass, far above the subnormal range. */
+#ifndef HHMM_BIG_RENORM
+#define HHMM_BIG_RENORM 4
+#endif
+constexpr int kBigRenorm = HHMM_BIG_RENORM;
 constexpr int kGroup = 2;     /* pass 1 keeps every kGroup-th state (32 steps / groups of 4 need
                                * ~300 VGPRs: occupancy 1) */
 
@@ -590,7 +603,7 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
                 fwd_init<MODEL, K>(al, ln.pp, ecur, cur[0], lsc, ex);
             } else {
                 lsc += ecur.m;
-                fwd_step<MODEL, K>(al, ln.pp, ecur.e, cur[u], ex);
+                fwd_step<MODEL, K>(al, ln.pp, ecur.e, cur[u], ex, !fb_big(MODE) || u % kBigRenorm == 0);
             }
             if constexpr (fb_base(MODE) == FB_FWD) {
                 emit_alpha<K>(a, ln.p, t, al, lsc + kLn2 * ex);
@@ -751,7 +764,7 @@ __device__ __forceinline__ void bwd_block_big(const DevArgs &a, const FbLane<MOD
         if (u + 1 < B)
             emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, u + 1 < B ? u + 1 : u), enx);
         if (FULLB || t0 + u < ln.Tp)
-            fwd_step<MODEL, K>(al, ln.pp, ecur.e, unpack_obs(w, u), exb);
+            fwd_step<MODEL, K>(al, ln.pp, ecur.e, unpack_obs(w, u), exb, u % kBigRenorm == 0);
         if (u % G == 0) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
@@ -776,7 +789,7 @@ __device__ __forceinline__ void bwd_block_big(const DevArgs &a, const FbLane<MOD
             /* next: the following recompute step, or (after the last) the group's last step again */
             emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, r + 1 < G ? u + 1 : g * G + G - 1), e2);
             if (FULLB || t0 + u < ln.Tp)
-                fwd_step_to<MODEL, K>(gb[r - 1], gb[r], ln.pp, e1.e, unpack_obs(w, u), exb);
+                fwd_step_to<MODEL, K>(gb[r - 1], gb[r], ln.pp, e1.e, unpack_obs(w, u), exb, u % kBigRenorm == 0);
             e1 = e2;
         }
         /* e1 = emission of step g*G + G-1 */
@@ -789,7 +802,7 @@ __device__ __forceinline__ void bwd_block_big(const DevArgs &a, const FbLane<MOD
             if (FULLB || t < ln.Tp) {
                 emit_posteriors<K, MODE>(a, ln.p, t, gb[r], be, 0.0, 0.0);
                 if (t > ln.t0)
-                    bwd_step<MODEL, K>(be, ln.pp, e1.e, unpack_obs(w, u), bex);
+                    bwd_step<MODEL, K>(be, ln.pp, e1.e, unpack_obs(w, u), bex, u % kBigRenorm == 0);
             }
             e1 = e2;
         }
