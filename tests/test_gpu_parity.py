@@ -279,6 +279,29 @@ def test_viterbi_log_softmax_regimes(engine, oracle, model, scale):
     compare_all(got, ref, pars + ["pair_status"])
 
 
+@pytest.mark.parametrize("tiny", [1e-30, 1e-70])
+def test_gamma_profile_near_impossible_runs(engine, oracle, tiny):
+    """The gamma profile renormalises every 4 steps (FB_BIG, kBigRenorm): a
+    run of observations that every state emits with probability `tiny`
+    shrinks the filter by ~tiny per step between renormalisations, far from
+    underflow for 1e-70 over 3 steps; results stay within tolerance of the
+    oracle's log-space recursion, on the lane decoder path of the 1M-pair bench."""
+    import hhmm_amd
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    data, draws = synth.hmm_multinom(N=64, S=64, T=200, K=4, L=9)
+    phi = np.array(draws["phi_k"], dtype=np.float64)
+    phi[:, :, 8] = tiny
+    phi /= phi.sum(axis=2, keepdims=True)
+    draws["phi_k"] = phi
+    x = np.array(data["x"])
+    x[:, 60:100] = 9
+    data["x"] = x
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, pairing="zip",
+                       flags=_abi.FLAG_VIT_LANES, return_status=True)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
 def test_unsupported_shape_leaves_no_kernel_running(engine, oracle):
     """hmm-multinom K = 4 with L = 100: the forward-backward's emission table
     (L * 4 doubles per lane) does not fit in LDS while the state-parallel
