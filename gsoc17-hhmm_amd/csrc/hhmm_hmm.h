@@ -2339,11 +2339,13 @@ static size_t lds_floor(const char *name)
     return v ? (size_t)atoi(v) * 1024 : 0;
 }
 
-static bool shape_for(const DevArgs &a, bool discrete, LaunchShape &s)
+static bool shape_for(const DevArgs &a, bool discrete, LaunchShape &s, const char *probe = nullptr)
 {
     const int KP = (a.K + 1) / 2;
     size_t per_wave = discrete ? (size_t)a.L * KP * 64 * sizeof(double2) : 0;
     int waves = 4;
+    if (probe && getenv(probe)) /* probe knob (tools/ab_bench.py --env): waves per workgroup, 1..4 */
+        waves = std::min(std::max(atoi(getenv(probe)), 1), 4);
     if (per_wave > 0) {
         while (waves > 0 && per_wave * waves > kLdsLimit)
             --waves;
@@ -2361,7 +2363,7 @@ template <int MODEL, int K>
 static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
 {
     LaunchShape s;
-    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s, "HHMM_PROBE_FB_WAVES")) {
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
@@ -2482,7 +2484,7 @@ static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st, bool packed 
         }
     }
     LaunchShape s;
-    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s, "HHMM_PROBE_VIT_WAVES")) {
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
