@@ -12,9 +12,16 @@ fb_kernel on the caller's stream beside viterbi_kernel on a side stream
 (fbv_kernel: one sweep, x read once); both halves alone and the other
 schedule are reported after the timed region.
 
-Multi-GPU (torch.distributed.run, one process per GPU): every rank evaluates
-its own 1M pairs (weak scaling, no data-path collective); the per-step
-summed log-likelihood is all-reduced over RCCL (the path's only exchange).
+Multi-GPU (one process per GPU): every rank evaluates its own 1M pairs (weak
+scaling, no data-path collective); the per-step summed log-likelihood is
+all-reduced over RCCL (the path's only exchange).  `--gpus N` with N > 1 and
+no WORLD_SIZE in the environment re-launches this script as N ranks under
+torch.distributed.run (a child process started before anything touches the
+GPU); under a launcher the world size must equal --gpus.  The decoded paths
+leave the device after the timed region: each rank copies its zstar_t slice
+into a pinned host buffer (the per-rank D2H the R host would do into its
+slice of the caller's array), timed on its own (`path_gather`).  `--stub`
+rehearses the launcher and the timing harness on CPU ranks over gloo.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 `roofline` for the dominant kernel (HIP events on the launch stream) and
@@ -66,7 +73,154 @@ def parse():
     ap.add_argument("--flags", type=int, default=0, help="c3-c5 probes: hhmm_request.flags")
     ap.add_argument("--fused", action="store_true",
                     help="time the one-kernel fused sweep (HHMM_FLAG_FUSED) instead of the two-kernel schedule")
+    ap.add_argument("--no-path-gather", action="store_true",
+                    help="skip the timed D2H of the decoded paths after the timed region")
+    ap.add_argument("--stub", action="store_true",
+                    help="launcher rehearsal without a GPU: CPU ranks over gloo, a fixed numpy step")
+    ap.add_argument("--master-port", type=int, default=0, help="rendezvous port for --gpus N > 1 (0: a free one)")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# Ranks: launch, rendezvous, timing over ranks
+# ---------------------------------------------------------------------------
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv=None):
+    """`--gpus N` (N > 1) without a launcher: start N ranks of this script
+    under torch.distributed.run as a CHILD process (no exec, and nothing in
+    this parent has touched the GPU) and return its exit code."""
+    import subprocess
+    argv = list(sys.argv[1:] if argv is None else argv)
+    port = a.master_port or _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(pathlib.Path(__file__).resolve())] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+class Ranks:
+    """World/rank from the launcher's environment; the process group (nccl =
+    RCCL on a GPU box, gloo for --stub) and the collectives the timing needs."""
+
+    def __init__(self, a):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={self.world} ranks")
+        self.stub = a.stub
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            if not self.stub:
+                torch.cuda.set_device(self.local)
+            dist.init_process_group("gloo" if self.stub else "nccl")
+            self.dist = dist
+        self.dev = torch.device("cpu") if self.stub else torch.device("cuda", self.local)
+
+    def sync(self):
+        if not self.stub:
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def all_reduce_sum(self, t):
+        if self.dist:
+            self.dist.all_reduce(t)
+        return t
+
+    def gather(self, values):
+        """Per-rank float vectors -> list over ranks (every rank gets it)."""
+        t = torch.tensor(values, dtype=torch.float64, device=self.dev)
+        if not self.dist:
+            return [t.tolist()]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [o.tolist() for o in out]
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed_region(rk, step, steps, warmup, before_timing=None):
+    """W untimed steps, then exactly K steps bracketed by barrier + device
+    synchronize on both sides.  Returns the wall time of this rank, the max
+    over ranks and the per-rank list."""
+    for _ in range(warmup):
+        step(None)
+    rk.sync()
+    if before_timing:
+        before_timing()
+    rk.barrier()
+    rk.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    rk.sync()
+    rk.barrier()
+    elapsed = time.perf_counter() - t0
+    per_rank = [v[0] for v in rk.gather([elapsed])]
+    return elapsed, max(per_rank), per_rank
+
+
+def path_gather(rk, zs):
+    """The decoded paths leave the device: this rank's zstar_t slice is copied
+    into a pinned host buffer (a direct D2H per rank into its
+    slice of the caller's array), all ranks at once, timed after the timed
+    region.  Returns bytes per rank and the max time over ranks."""
+    host = torch.empty(zs.shape, dtype=zs.dtype, pin_memory=True)
+    rk.sync()
+    rk.barrier()
+    t0 = time.perf_counter()
+    host.copy_(zs, non_blocking=True)
+    rk.sync()
+    dt = time.perf_counter() - t0
+    rk.barrier()
+    per_rank = [v[0] for v in rk.gather([dt])]
+    nbytes = zs.numel() * zs.element_size()
+    ok = bool(torch.equal(host[:1], zs[:1].cpu()))
+    del host
+    return {"bytes_per_rank": nbytes, "ms_max_over_ranks": max(per_rank) * 1e3,
+            "ms_per_rank": [x * 1e3 for x in per_rank],
+            "GBps_per_rank": nbytes / max(per_rank) / 1e9,
+            "GBps_aggregate": rk.world * nbytes / max(per_rank) / 1e9,
+            "destination": "pinned host buffer per rank (zstar_t [T, P] int32)", "first_row_verified": ok}
+
+
+def stub_workload(a, rk):
+    """--stub: the launcher, rendezvous and timing harness on CPU ranks (gloo):
+    each step is a fixed numpy recursion over this rank's own block."""
+    rng = np.random.default_rng(rk.rank)
+    P, T = 4096, 64
+    x = rng.random((T, P))
+    acc = torch.zeros(1, dtype=torch.float64)
+
+    def step(i):
+        f = np.ones(P)
+        for t in range(T):
+            f = f * x[t] + 1e-3
+            f /= f.max()
+        acc.fill_(float(f.sum()))
+        rk.all_reduce_sum(acc)
+
+    elapsed, emax, per_rank = timed_region(rk, step, a.steps, a.warmup)
+    if rk.rank == 0:
+        print(json.dumps({"metric": "stub (launcher rehearsal)", "value": rk.world * P * T * a.steps / emax,
+                          "unit": "series-timesteps/s", "n_gpus": rk.world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": emax / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "rank_ms_per_step": [x / a.steps * 1e3 for x in per_rank],
+                          "all_reduce_check": float(acc.item())}), flush=True)
 
 
 K, L = 4, 9
@@ -239,68 +393,61 @@ def load_traffic(kernel, P, T):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    lib = hhmm_amd.load_library()
-    assert lib.hhmm_init(1) == 0, lib.hhmm_last_error().decode()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    rk = Ranks(a)
+    try:
+        if a.stub:
+            return stub_workload(a, rk)
+        torch.cuda.set_device(rk.dev)
+        lib = hhmm_amd.load_library()
+        assert lib.hhmm_init(1) == 0, lib.hhmm_last_error().decode()
+        if a.workload == "f1":
+            return features_workload(a, lib, rk)
+        if a.workload != "c2":
+            return other_workload(a, lib, rk)
+        return c2_workload(a, lib, rk)
+    finally:
+        rk.close()
 
-    if a.workload == "f1":
-        return features_workload(a, lib, dev, world, rank)
-    if a.workload != "c2":
-        return other_workload(a, lib, dev, world, rank)
+
+def c2_workload(a, lib, rk):
+    world, rank, dev = rk.world, rk.rank, rk.dev
     P, T = a.pairs, a.T
     x, draws = make_batch(P, T, a.seed + 7919 * rank, dev)
     run = DeviceRun(lib, x, draws, P, T, dev)
     torch.cuda.synchronize()
     s0 = torch.cuda.current_stream()
     name = "fused" if a.fused else "step"
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(a.steps)]
+    total = torch.zeros(1, dtype=torch.float64, device=dev)
 
-    def step(ev=None):
+    def step(i):
         """One pass of the hot path: one request for gamma_tk, loglik, zstar_t
         and logp_zstar (two kernels, joined on the launch stream; --fused:
-        the one-kernel sweep), bracketed by events on the launch stream."""
-        if ev:
-            ev[0].record(s0)
+        the one-kernel sweep), bracketed by events on the launch stream; then
+        the all-reduce of the summed log-likelihood over ranks."""
+        if i is not None:
+            evs[i][0].record(s0)
         run.launch(name)
-        if ev:
-            ev[1].record(s0)
+        if i is not None:
+            evs[i][1].record(s0)
         if world > 1:
-            import torch.distributed as dist
-            s = run.out["loglik"].sum().reshape(1)
-            dist.all_reduce(s)
+            torch.sum(run.out["loglik"], dim=0, keepdim=True, out=total)
+            rk.all_reduce_sum(total)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    checked = None
-    if not a.no_check and rank == 0:
-        checked = check_slice(run, x, draws, P, T)
+    checked = []
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(a.steps)]
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def check():
+        if not a.no_check and rank == 0:
+            checked.append(check_slice(run, x, draws, P, T))
+
+    elapsed_rank, elapsed, per_rank = timed_region(rk, step, a.steps, a.warmup, before_timing=check)
+    checked = checked[0] if checked else None
     step_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    rank_step_ms = [v[0] for v in rk.gather([step_ms])]
     bad = int((run.out["pair_status"] != 0).sum().item())
+    gather = None if a.no_path_gather else path_gather(rk, run.out["zstar_t"])
     # after the timed region: the other schedules once each (untimed for `value`):
     # the two halves alone (the north star's "batched forward-backward") and the
     # two-kernel schedule
@@ -351,6 +498,9 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic, "algorithmic_bytes_per_series_timestep": whole_b,
                          "duration_ms": step_ms},
+            "rank_ms_per_step": [x / a.steps * 1e3 for x in per_rank],
+            "rank_kernel_ms": rank_step_ms,
+            "path_gather": gather,
             "pair_failures": bad,
             "check": checked,
             "alone_after_timing": {
@@ -364,8 +514,6 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(T, a.cpu_seconds, a.seed)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def cpu_model():
@@ -462,33 +610,23 @@ def prepare_other(a, lib, dev, rank):
                 T=T, outs=outs, status=status)
 
 
-def other_workload(a, lib, dev, world, rank):
+def other_workload(a, lib, rk):
     """C3 / C4 / C5: one request per step through hhmm_run_device on resident
     device buffers (synthetic inputs from hhmm_amd.synth, copied once)."""
+    world, rank, dev = rk.world, rk.rank, rk.dev
     w = prepare_other(a, lib, dev, rank)
-    step, model, kw, pars, bps, desc = w["step"], w["model"], w["kw"], w["pars"], w["bps"], w["desc"]
+    run1, model, kw, pars, bps, desc = w["step"], w["model"], w["kw"], w["pars"], w["bps"], w["desc"]
     data, draws, P, T, status = w["data"], w["draws"], w["P"], w["T"], w["status"]
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev[0].record()
-    for _ in range(a.steps):
-        step()
-    ev[1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+
+    def step(i):
+        if i == 0:
+            ev[0].record()
+        run1()
+        if i == a.steps - 1:
+            ev[1].record()
+
+    _, elapsed, per_rank = timed_region(rk, step, a.steps, a.warmup)
     dev_ms = ev[0].elapsed_time(ev[1]) / a.steps
     units = P * T
     B = bps(T, kw["S"])
@@ -503,13 +641,12 @@ def other_workload(a, lib, dev, world, rank):
             "roofline": {"kernel": "whole request", "bound": "hbm", "achieved": B * units / (dev_ms * 1e-3) / 1e9,
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": B * units / (dev_ms * 1e-3) / HBM_PEAK,
                          "traffic": None, "algorithmic_bytes_per_series_timestep": B, "duration_ms": dev_ms},
+            "rank_ms_per_step": [x / a.steps * 1e3 for x in per_rank],
             "pair_failures": int((status != 0).sum().item()),
         }
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_grid(model, data, draws, pars, T, a.cpu_seconds, a.seed)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def cpu_baseline_grid(model, data, draws, pars, T, target_s, seed):
@@ -534,11 +671,12 @@ def cpu_baseline_grid(model, data, draws, pars, T, target_s, seed):
                       f"{threads} threads, oracle libm-log build", "cpu_model": cpu_model()}
 
 
-def features_workload(a, lib, dev, world, rank):
+def features_workload(a, lib, rk):
     """F1: extract_features (tayal2009/R/feature-extraction.R:8-133) over a
     synthetic tick series resident in HBM; one step = the whole pipeline
     (change points, compaction, per-leg rows and features) through
     hhmm_extract_features_device.  Weak scaling: every rank owns its own ticks."""
+    world, rank, dev = rk.world, rk.rank, rk.dev
     from hhmm_amd import features as F
     F.declare(lib)
     n = a.ticks
@@ -552,33 +690,19 @@ def features_workload(a, lib, dev, world, rank):
     assert lib.hhmm_features_workspace_size(n, C.byref(wsb)) == 0
     ws = torch.empty(int(wsb.value), dtype=torch.uint8, device=dev)
 
-    def step():
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def step(i):
+        if i == 0:
+            ev[0].record()
         st = lib.hhmm_extract_features_device(C.byref(tk), C.byref(legs), ws.data_ptr(), ws.numel(),
                                               torch.cuda.current_stream().cuda_stream)
         if st < 0:
             raise RuntimeError(lib.hhmm_last_error().decode())
+        if i == a.steps - 1:
+            ev[1].record()
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev[0].record()
-    for _ in range(a.steps):
-        step()
-    ev[1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    _, elapsed, per_rank = timed_region(rk, step, a.steps, a.warmup)
     dev_ms = ev[0].elapsed_time(ev[1]) / a.steps
     m = int(legs.n_legs)
     # algorithmic bytes: price + size per tick; per leg the two index times and 52 B of leg columns
@@ -609,8 +733,6 @@ def features_workload(a, lib, dev, world, rank):
                                     "sample": f"first {ns} ticks of the same series, sequential C oracle "
                                               f"(oracle/features_oracle.c), {cs:.1f} s"}
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def check_slice(run, x, draws, P, T):

@@ -160,6 +160,31 @@ hhmm_status join_stream(hipStream_t st, hipStream_t side)
     return HHMM_OK;
 }
 
+/* Waits for a request's work: its own stream and, when this device has one,
+ * the library's side stream (a failed launch can leave a forked kernel there
+ * unjoined).  Other streams -- other threads' requests -- are not waited on. */
+static hipError_t sync_request(hipStream_t st)
+{
+    hipError_t e = hipStreamSynchronize(st);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return e;
+    SideStreams &ss = side_streams();
+    hipStream_t side = nullptr;
+    {
+        std::lock_guard<std::mutex> g(ss.mu);
+        auto it = ss.by_dev.find(dev);
+        if (it != ss.by_dev.end())
+            side = it->second.first;
+    }
+    if (side) {
+        hipError_t e2 = hipStreamSynchronize(side);
+        if (e == hipSuccess)
+            e = e2;
+    }
+    return e;
+}
+
 static void pool_release_all()
 {
     Pool &p = pool();
@@ -623,13 +648,19 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
 
     s = launch_all(&dreq, &dres, P, ws, nullptr);
     if (s != HHMM_OK) {
-        /* a failed launch may follow one that is still running: drain the
-         * device before the pooled buffers can be handed to another request */
-        (void)hipDeviceSynchronize();
+        /* a failed launch may follow one that is still running: drain this
+         * request's streams before its pooled buffers can be handed to another
+         * request; a sticky device error from an earlier fault is reported
+         * beside the launch error instead of being buried under it */
+        e = sync_request(nullptr);
         cleanup();
+        if (e != hipSuccess) {
+            std::string first = hhmm_last_error();
+            set_error("%s; draining the request's streams then failed: %s", first.c_str(), hipGetErrorString(e));
+        }
         return s;
     }
-    e = hipDeviceSynchronize();
+    e = sync_request(nullptr);
     if (e != hipSuccess) {
         cleanup();
         return hip_fail(e, "kernel execution");

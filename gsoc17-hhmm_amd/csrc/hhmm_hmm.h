@@ -445,16 +445,21 @@ enum FbMode {
     FB_PACK = 8,  /* flag: the forward sweep packs each chunk's symbols (4 bits, L <= 16)
                    * into the checkpoint record; the backward sweep reads those
                    * instead of re-reading x (hmm-multinom: 4 B -> 1 B per step) */
-    FB_BIG = 16   /* flag (gamma profile): checkpoints every kBigChunk steps, and a
+    FB_BIG = 16,  /* flag (gamma profile): checkpoints every kBigChunk steps, and a
                    * two-level recompute in the backward sweep (every kGroup-th
                    * state kept, each group recomputed before it is consumed):
                    * checkpoint traffic 8 -> 4 B per step for ~1.44 forward
                    * recomputes per step instead of 1 */
+    FB_RN1 = 32   /* flag (with FB_BIG): renormalise every step -- the waves whose
+                   * pairs' parameters do not bound the kBigRenorm-step shrink
+                   * (renorm_sparse_safe) */
 };
 constexpr int fb_base(int mode) { return mode & 3; }
 constexpr bool fb_ffbs(int mode) { return (mode & FB_FFBS) != 0; }
 constexpr bool fb_pack(int mode) { return (mode & FB_PACK) != 0; }
 constexpr bool fb_big(int mode) { return (mode & FB_BIG) != 0; }
+/* steps between renormalisations */
+constexpr int fb_rp(int mode);
 constexpr int kFwdGroup = 4;  /* forward chunks per observation prefetch group */
 constexpr int kVitGroup = 2;  /* Viterbi chunks per observation prefetch group */
 constexpr int kBigChunk = 16; /* checkpoint interval of FB_BIG (a multiple of fb_chunk(K) = 8) */
@@ -471,6 +476,49 @@ enum FbPhase { FB_PH_BOTH = 0, FB_PH_FWD = 1, FB_PH_BWD = 2 };
 #define HHMM_BIG_RENORM 4
 #endif
 constexpr int kBigRenorm = HHMM_BIG_RENORM;
+constexpr int fb_rp(int mode) { return (fb_big(mode) && !(mode & FB_RN1)) ? kBigRenorm : 1; }
+/* Is the kBigRenorm-step cadence safe for this pair?  Renormalisation leaves
+ * the filter's max in [0.5, 1).  One forward step keeps the max at least
+ * max * min_i max_j A(i,j) phi(j,x) >= max * (min_i rowmax_i) * phi_min, one
+ * backward step at least max * (min_i colmax_i) * phi_min (rowmax / colmax:
+ * the largest entry of row / column i of A; phi_min: the smallest emission
+ * probability).  With b = phi_min * min(rowmax, colmax) >= 2^-39, kBigRenorm = 4
+ * unrenormalised steps keep the max above 2^-157, so every component down to
+ * 2^-865 of it stays a normal double -- far below the 1e-250 tolerance floor,
+ * as with per-step renormalisation.  Pairs with a smaller b (rare symbols,
+ * near-zero transitions; the reference's log space stays finite there) make
+ * their wave renormalise every step (FB_RN1), the exact per-step form. */
+constexpr double kRenormSafeBound = 0x1p-39;
+template <int MODEL, int K>
+__device__ __forceinline__ bool renorm_sparse_safe(const PairParams<MODEL, K> &pp, const double2 *slab, int L)
+{
+    static_assert(!ModelTraits<MODEL>::kGauss, "discrete emissions only");
+    double tmin = 1.0 / 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double rmax = pp.A[i][0], cmax = pp.A[0][i];
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+            rmax = fmax(rmax, pp.A[i][j]);
+            cmax = fmax(cmax, pp.A[j][i]);
+        }
+        tmin = fmin(tmin, fmin(rmax, cmax));
+    }
+    double emin = 1.0 / 0.0;
+    for (int l = 1; l <= L; ++l) {
+        double e[K];
+        read_table<K>(slab, l, L, e);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            emin = fmin(emin, e[k]);
+    }
+    return emin * tmin >= kRenormSafeBound; /* NaN: unsafe */
+}
+/* true when any lane of the wave is unsafe (wave-uniform) */
+__device__ __forceinline__ bool wave_any(bool v)
+{
+    return __builtin_amdgcn_readfirstlane((int)(__ballot(v) != 0)) != 0;
+}
 constexpr int kGroup = 2;     /* pass 1 keeps every kGroup-th state (32 steps / groups of 4 need
                                * ~300 VGPRs: occupancy 1) */
 
@@ -603,7 +651,7 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
                 fwd_init<MODEL, K>(al, ln.pp, ecur, cur[0], lsc, ex);
             } else {
                 lsc += ecur.m;
-                fwd_step<MODEL, K>(al, ln.pp, ecur.e, cur[u], ex, !fb_big(MODE) || u % kBigRenorm == 0);
+                fwd_step<MODEL, K>(al, ln.pp, ecur.e, cur[u], ex, u % fb_rp(MODE) == 0);
             }
             if constexpr (fb_base(MODE) == FB_FWD) {
                 emit_alpha<K>(a, ln.p, t, al, lsc + kLn2 * ex);
@@ -764,7 +812,7 @@ __device__ __forceinline__ void bwd_block_big(const DevArgs &a, const FbLane<MOD
         if (u + 1 < B)
             emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, u + 1 < B ? u + 1 : u), enx);
         if (FULLB || t0 + u < ln.Tp)
-            fwd_step<MODEL, K>(al, ln.pp, ecur.e, unpack_obs(w, u), exb, u % kBigRenorm == 0);
+            fwd_step<MODEL, K>(al, ln.pp, ecur.e, unpack_obs(w, u), exb, u % fb_rp(MODE) == 0);
         if (u % G == 0) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
@@ -789,7 +837,7 @@ __device__ __forceinline__ void bwd_block_big(const DevArgs &a, const FbLane<MOD
             /* next: the following recompute step, or (after the last) the group's last step again */
             emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, unpack_obs(w, r + 1 < G ? u + 1 : g * G + G - 1), e2);
             if (FULLB || t0 + u < ln.Tp)
-                fwd_step_to<MODEL, K>(gb[r - 1], gb[r], ln.pp, e1.e, unpack_obs(w, u), exb, u % kBigRenorm == 0);
+                fwd_step_to<MODEL, K>(gb[r - 1], gb[r], ln.pp, e1.e, unpack_obs(w, u), exb, u % fb_rp(MODE) == 0);
             e1 = e2;
         }
         /* e1 = emission of step g*G + G-1 */
@@ -802,7 +850,7 @@ __device__ __forceinline__ void bwd_block_big(const DevArgs &a, const FbLane<MOD
             if (FULLB || t < ln.Tp) {
                 emit_posteriors<K, MODE>(a, ln.p, t, gb[r], be, 0.0, 0.0);
                 if (t > ln.t0)
-                    bwd_step<MODEL, K>(be, ln.pp, e1.e, unpack_obs(w, u), bex, u % kBigRenorm == 0);
+                    bwd_step<MODEL, K>(be, ln.pp, e1.e, unpack_obs(w, u), bex, u % fb_rp(MODE) == 0);
             }
             e1 = e2;
         }
@@ -1029,6 +1077,12 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
     for (int k = 0; k < K; ++k) {
         al[k] = 0.0;
         be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
+    }
+    if constexpr (fb_big(MODE)) {
+        if (wave_any(!renorm_sparse_safe<MODEL, K>(ln.pp, ln.slab, a.L))) {
+            fb_sweep<MODEL, K, MODE | FB_RN1, false, PH>(a, ln, sp, al, 0.0, be, 0.0);
+            return;
+        }
     }
     fb_sweep<MODEL, K, MODE, false, PH>(a, ln, sp, al, 0.0, be, 0.0);
 }
@@ -1269,10 +1323,9 @@ constexpr bool fbv_ok()
     return fb_big_ok<MODEL, K>() && vit_chunk(K) == fb_chunk(K);
 }
 
-template <int MODEL, int K>
+template <int MODEL, int K, int MODE = FB_GAMMA | FB_PACK | FB_BIG>
 __device__ __forceinline__ void fbv_block(const DevArgs &a, uint32_t block)
 {
-    constexpr int MODE = FB_GAMMA | FB_PACK | FB_BIG;
     constexpr int C = fb_chunk(K);
     constexpr int SPW = bp_steps_per_word(K);
     constexpr int WPC = C / SPW;
@@ -1303,6 +1356,12 @@ __device__ __forceinline__ void fbv_block(const DevArgs &a, uint32_t block)
     load_params<MODEL, K, true>(lpp, a, d);
     fill_table<K, false>(slab, a, d);
     fill_table<K, true>(slab + tab, a, d);
+    if constexpr (!(MODE & FB_RN1)) {
+        if (wave_any(!renorm_sparse_safe<MODEL, K>(ln.pp, slab, a.L))) {
+            fbv_block<MODEL, K, MODE | FB_RN1>(a, block); /* per-step renormalisation (renorm_sparse_safe) */
+            return;
+        }
+    }
     const SeriesPtrs sp = series_ptrs<MODEL, false>(a, n);
     const int Tp = ln.Tp;
     const int Tw_min = wave_min(Tp);

@@ -50,6 +50,12 @@ constexpr int kLBack = 16;  /* backtrack steps per back-pointer chunk */
  * steps), far above the subnormal range.  A multiple-of-kLRenorm step (every
  * checkpoint step) is always renormalised. */
 constexpr int kLRenorm = 4;
+/* The cadence is taken only where the pair's parameters bound the shrink:
+ * b = phi_min * min(min_i rowmax_i(A), min_i colmax_i(A)) >= 2^-39 (the lane
+ * kernels' renorm_sparse_safe argument, hhmm_hmm.h).  Gaussian emissions have
+ * no such bound (a density ratio can be anything), and a wave holding an
+ * unbounded pair renormalises every step. */
+constexpr double kLRenormSafeBound = 0x1p-39;
 
 /* bytes per (pair, state) back-pointer row */
 __host__ __device__ constexpr int lk_row_bytes(int Tmax) { return (Tmax + 15) & ~15; }
@@ -127,6 +133,7 @@ struct LkLane {
     double mu, isig, c0, lsig; /* gauss, state j */
     double *xch;     /* this pair's LDS exchange slots: 2 x G doubles */
     const double *tab; /* multinomial: this pair's [L][G] emission table */
+    bool dense;        /* wave-uniform: renormalise every step (kLRenormSafeBound) */
 };
 
 template <int MODEL, int G, int KM>
@@ -171,6 +178,7 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G, KM> &ln, const DevArgs
     ln.xch = lds + (size_t)g * 2 * G;
     double *tab = lds + (size_t)gpb * 2 * G + (size_t)g * a.L * G;
     ln.tab = tab;
+    double emin = 1.0 / 0.0;
     if constexpr (!LkTraits<MODEL>::kGauss) {
         for (int l0 = 0; l0 < a.L; l0 += 8) {
             double v[8];
@@ -179,9 +187,29 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G, KM> &ln, const DevArgs
                 v[r] = a.phi_k[d + S * ((int64_t)jj + (int64_t)a.K * min(l0 + r, a.L - 1))];
 #pragma unroll
             for (int r = 0; r < 8; ++r)
-                if (l0 + r < a.L)
+                if (l0 + r < a.L) {
                     tab[(l0 + r) * G + ln.j] = (LOG && ln.on) ? dev_cr_log(v[r]) : v[r];
+                    emin = fmin(emin, v[r]);
+                }
         }
+    }
+    ln.dense = true;
+    if (!LOG && !LkTraits<MODEL>::kGauss) {
+        double rmax = rawr[0], cmax = rawc[0];
+#pragma unroll
+        for (int i = 1; i < KM; ++i)
+            if (i < a.K) {
+                rmax = fmax(rmax, rawr[i]);
+                cmax = fmax(cmax, rawc[i]);
+            }
+        /* group minima of phi and of the row / column maxima (idle lanes +inf;
+         * every lane takes part in the butterflies); a NaN parameter anywhere
+         * in the pair or an unsafe pair makes the wave dense */
+        const double inf = 1.0 / 0.0;
+        const double ge = -grp_max<G>(ln.on ? -emin : -inf);
+        const double gm = -grp_max<G>(ln.on ? -fmin(rmax, cmax) : -inf);
+        const bool bad = !(ge * gm >= kLRenormSafeBound) || (ln.on && !(emin * fmin(rmax, cmax) >= 0.0));
+        ln.dense = __builtin_amdgcn_readfirstlane((int)(__ballot(bad) != 0)) != 0;
     }
     __syncthreads();
 }
@@ -310,11 +338,12 @@ __device__ __forceinline__ double grp_renorm(double v, int &ex)
     return ldexp(v, -e);
 }
 
-/* grp_renorm on every kLRenorm-th step t */
+/* grp_renorm on every kLRenorm-th step t (every step when `dense`, a
+ * wave-uniform flag) */
 template <int G>
-__device__ __forceinline__ double grp_renorm_at(double v, int &ex, int t)
+__device__ __forceinline__ double grp_renorm_at(double v, int &ex, int t, bool dense)
 {
-    return (t % kLRenorm == 0) ? grp_renorm<G>(v, ex) : v;
+    return (dense || t % kLRenorm == 0) ? grp_renorm<G>(v, ex) : v;
 }
 
 /* sum_i w_i c_i over the G entries (idle ones 0 x 0) as four interleaved fma
@@ -407,7 +436,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         grp_exchange<G, KM>(ln.xch, slot, ln.j, al, w);
         slot ^= 1;
         lsc += m;
-        al = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex, t);
+        al = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex, t, ln.dense);
         if (!need_bwd) {
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
                 lk_put<MODEL, G, KM>(a.alpha, a, ln, t, al / grp_sum<G>(al));
@@ -460,7 +489,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             if (t0 + u < Tp) { /* group-uniform */
                 grp_exchange<G, KM>(ln.xch, slot, ln.j, abuf[u - 1], w);
                 slot ^= 1;
-                abuf[u] = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb, t0 + u);
+                abuf[u] = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb, t0 + u, ln.dense);
             }
         }
 #pragma unroll
@@ -503,7 +532,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             if (t > 0) {
                 grp_exchange<G, KM>(ln.xch, slot, ln.j, es[u] * be, w);
                 slot ^= 1;
-                be = grp_renorm_at<G>(lk_bwd<MODEL, G, KM>(ln, w), bex, t);
+                be = grp_renorm_at<G>(lk_bwd<MODEL, G, KM>(ln, w), bex, t, ln.dense);
             }
         }
     }

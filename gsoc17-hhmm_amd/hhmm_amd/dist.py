@@ -57,14 +57,31 @@ def slice_draws(draws, b, e):
     return {k: np.asarray(v)[b:e] for k, v in draws.items()}
 
 
-def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=None, device=None):
+def pair_range(N, S, pairing, b, e):
+    """Global ABI pair range [begin, end) of series block [b, e): contiguous in
+    every pairing (grid p = s + S*n, zip p = n, block p = j + B*n)."""
+    per = {"grid": S, "zip": 1, "block": S // N if N else 0}[pairing]
+    return b * per, e * per
+
+
+def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=None, device=None,
+                paths_out=None):
     """Evaluates this rank's shard and performs the two exchanges.
 
     Returns (local, summed_loglik, paths):
       local          this rank's outputs (pairs of its series block, ABI order)
-      summed_loglik  [S] per-draw log-likelihood summed over ALL series (all-reduce;
-                     zip / block pairing: each draw's own series)
-      paths          on rank 0: zstar_t of every pair in global ABI order, else None
+      summed_loglik  [S] per-draw log-likelihood summed over ALL series (all-reduce
+                     of a device tensor under nccl; zip / block pairing: each
+                     draw's own series)
+      paths          zstar_t of every pair in global ABI order:
+                     * paths_out given (an array of shape (P, T) that every rank
+                       can write, e.g. a np.memmap on the node's shared memory):
+                       each rank writes its own contiguous pair slice into it
+                       (SURVEY §8e's direct per-rank copy into the caller's
+                       buffer; no collective moves the paths); returns paths_out
+                       on every rank after a barrier;
+                     * otherwise a tensor gather to rank 0 (padded device tensors
+                       under nccl, no pickling); rank 0 gets the array, others None.
     """
     import torch
     import torch.distributed as dist
@@ -77,6 +94,10 @@ def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=No
     N = np.atleast_2d(np.asarray(data[xkey])).shape[0] if np.asarray(data[xkey]).ndim > 1 or \
         not model.startswith("iohmm") else 1
     S = next(np.asarray(v).shape[0] for v in draws.values())
+    if pairing == "block" and S % N:
+        raise ValueError(f"block pairing needs n_draws ({S}) to be a multiple of n_series ({N})")
+    if pairing == "zip" and S != N:
+        raise ValueError(f"zip pairing needs n_draws ({S}) == n_series ({N})")
     b, e = shard_range(N, world, rank)
     ldata = slice_series(data, b, e)
     B = S // N if pairing == "block" else 1  # draws per series (block pairing: one fit per series)
@@ -99,10 +120,30 @@ def gqs_sharded(model, data, draws, pars, pairing="grid", compute=None, group=No
 
     paths = None
     if "zstar_t" in pars:
-        mine = np.asarray(local.get("zstar_t", np.zeros((0, 0), dtype=np.int32)))
-        gathered = [None] * world if rank == 0 else None
-        dist.gather_object(mine, gathered, dst=0, group=group)
+        p0, p1 = pair_range(N, S, pairing, b, e)
+        if paths_out is not None:
+            if e > b:
+                paths_out[p0:p1] = np.asarray(local["zstar_t"])
+            dist.barrier(group=group)
+            return local, summed, paths_out
+        T = int(np.asarray(local["zstar_t"]).shape[1]) if e > b else 0
+        T = int(_all_max(T, dev, group))
+        rows = [pair_range(N, S, pairing, *shard_range(N, world, r)) for r in range(world)]
+        cap = max(r1 - r0 for r0, r1 in rows)
+        buf = torch.zeros((cap, T), dtype=torch.int32, device=dev)
+        if e > b:
+            buf[:p1 - p0] = torch.from_numpy(np.ascontiguousarray(local["zstar_t"])).to(dev)
+        bufs = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+        dist.gather(buf, bufs, dst=0, group=group)
         if rank == 0:
-            paths = np.concatenate([g for g in gathered if g.size], axis=0) if any(g.size for g in gathered) \
-                else mine
+            paths = np.concatenate([g[:r1 - r0].cpu().numpy() for g, (r0, r1) in zip(bufs, rows)], axis=0)
+            paths = np.asfortranarray(paths)
     return local, summed, paths
+
+
+def _all_max(v, dev, group):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())

@@ -1,0 +1,56 @@
+"""CPU: bench.py's multi-rank launcher and timing harness (no GPU).
+
+`bench.py --gpus 2 --stub` without a launcher must start two ranks under
+torch.distributed.run (gloo), time exactly K steps on each, take the max over
+ranks and print one JSON line with n_gpus == 2; a launcher whose world size
+differs from --gpus must fail loudly instead of measuring fewer GPUs."""
+import json
+import os
+import pathlib
+import subprocess
+import sys
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_gpus_two_launches_two_ranks():
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--stub", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, env=_env(), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["warmup"] == 1
+    assert len(line["rank_ms_per_step"]) == 2
+    assert abs(line["ms_per_step"] - max(line["rank_ms_per_step"])) < 1e-9
+    # the per-step all-reduce ran over both ranks: rank 0 holds the sum of two positive terms
+    assert line["all_reduce_check"] > 0
+
+
+def test_gpus_one_is_a_single_process():
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "1", "--stub", "--steps", "2",
+                        "--warmup", "0"], capture_output=True, text=True, env=_env(), timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    assert line["n_gpus"] == 1 and len(line["rank_ms_per_step"]) == 1
+
+
+def test_world_size_mismatch_fails_loudly():
+    env = _env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--stub", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in (r.stderr + r.stdout)

@@ -45,24 +45,29 @@ def _log_softmax(v):
     return v - (m + np.log(np.sum(np.exp(v - m), axis=-1, keepdims=True)))
 
 
-def compare_tayal_gamma(got, ref):
+def compare_tayal_gamma(got, ref, max_forgiven=0):
     """Tayal's gamma = normalize(alpha .* beta) is 0/0 = NaN wherever the
     reference's disagreeing forward/backward masks drive the
     overlap of alpha and beta below the double range.  NaN rows must agree,
     except rows whose exact overlap max_k alpha_k beta_k (from the oracle's
     log-space unalpha_tk / unbeta_tk) is below e^-700 ~ 1e-304: there the
-    result depends on the last bits of products at the subnormal edge.  Every
+    result depends on the last bits of products at the subnormal edge.  At
+    most `max_forgiven` rows may be forgiven (the count is printed); every
     row that is finite on both sides is within tolerance."""
     g, r = got["gamma_tk"], ref["gamma_tk"]
     n1, n2 = np.isnan(g).any(axis=-1), np.isnan(r).any(axis=-1)
     diff = n1 != n2
+    nd = int(diff.sum())
     if diff.any():
         over = np.max(_log_softmax(ref["unalpha_tk"]) + _log_softmax(ref["unbeta_tk"]), axis=-1)
         assert (over[diff] < -700.0).all(), \
             f"NaN rows differ away from the underflow edge (max log overlap {over[diff].max():.1f})"
-    assert diff.mean() < 1e-3, f"NaN rows differ: {diff.sum()} of {diff.size}"
+    print(f"compare_tayal_gamma: {nd} of {diff.size} rows forgiven (NaN on one side only, log overlap < -700); "
+          f"{int(n2.sum())} NaN rows in the oracle")
+    assert nd <= max_forgiven, f"NaN rows differ: {nd} of {diff.size} (bound {max_forgiven})"
     ok = ~(n1 | n2)
     compare("gamma_tk", g[ok], r[ok])
+    return nd
 
 
 # ---- C1: hmm/main.R Gaussian HMM, K=3, T=500, 1 series x 1000 draws -------------------
@@ -158,6 +163,18 @@ def test_c3_grid(engine, oracle):
 
 # ---- C4: iohmm-hmix K=4, L=3, M=4, T=10k, batched FFBS -----------------------------------
 
+def test_c4_bench_output_set(engine, oracle):
+    """The C4 bench's exact request -- loglik, gamma_tk and z_ffbs -- which the
+    library runs as ONE state-parallel IO_DET sweep (io_states, hhmm_iohmm.h),
+    oracle-checked at the config's T = 10^4 (test_c4_ffbs asks for zstar_t too,
+    which takes the IO_CR lane sweep plus an FFBS-only sweep instead)."""
+    data, draws = synth.iohmm_mix(N=2, S=64, T=10_000, K=4, L=3, M=4)
+    pars = ["loglik", "gamma_tk", "z_ffbs"]
+    u = synth.ffbs_uniforms(2 * 64, 10_000)
+    got, ref = gpu_and_oracle(engine, oracle, "iohmm-hmix", data, draws, pars, uniforms=u)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
 def test_c4_ffbs(engine, oracle):
     data, draws = synth.iohmm_mix(N=2, S=64, T=10_000, K=4, L=3, M=4)
     pars = ["loglik", "gamma_tk", "z_ffbs", "oblik_t", "zstar_t", "logp_zstar"]
@@ -183,7 +200,7 @@ def test_c5_few_pairs(engine, oracle, c5_data):
     ref = oracle.gqs("hhmm-tayal2009", data, d4, pars=HOT + ["unalpha_tk", "unbeta_tk"], return_status=True,
                      nthreads=threads())
     compare_all(got, ref, ["loglik", "zstar_t", "logp_zstar", "pair_status"])
-    compare_tayal_gamma(got, ref)
+    compare_tayal_gamma(got, ref, max_forgiven=1000)
 
 
 def test_c5_full_shape(engine, oracle, c5_data):
@@ -209,4 +226,4 @@ def test_c5_full_shape(engine, oracle, c5_data):
     ref = oracle.gqs("hhmm-tayal2009", data, dsub, pars=HOT + ["unalpha_tk", "unbeta_tk"], nthreads=3)
     got = {k: r.host_pairs(k, idx) for k in HOT}
     compare_all(got, ref, ["loglik", "zstar_t", "logp_zstar"])
-    compare_tayal_gamma(got, ref)
+    compare_tayal_gamma(got, ref, max_forgiven=1000)

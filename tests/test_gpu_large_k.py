@@ -61,6 +61,39 @@ def test_large_K_invalid_backpointer(engine, oracle):
     run_both(engine, oracle, "hmm-multinom", data, draws)
 
 
+@pytest.mark.parametrize("K", [12, 23, 32])
+def test_gamma_only_large_K_ragged(engine, oracle, K):
+    """The bench's N1 output set (loglik, gamma, zstar, logp_zstar) runs the
+    one-group-sum gamma (alpha .* beta / sum, lk_fb_kernel's gamma_only
+    branch); ragged T inside the wave's two groups."""
+    data, draws = synth.hmm_multinom(N=5, S=7, T=400, K=K, L=9)
+    data["T"] = np.array([400, 1, 257, 399, 64], dtype=np.int32)
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk", "zstar_t", "logp_zstar"])
+
+
+def test_gamma_only_large_K_disjoint_filters(engine, oracle):
+    """alpha and beta nearly disjoint (states that the forward pass makes
+    improbable are the ones the backward pass favours) so the product's sum
+    drops below 2^-960 and the gamma-only branch takes the reference's
+    normalised-vector formula."""
+    K = 12
+    data, draws = synth.hmm_multinom(N=1, S=4, T=600, K=K, L=9)
+    A = np.full((4, K, K), 1e-300)
+    for i in range(K):
+        A[:, i, i] = 1.0
+    A /= A.sum(axis=2, keepdims=True)
+    draws["A_ij"] = A
+    phi = np.full((4, K, 9), 1e-3)
+    phi[:, : K // 2, 0] = 1.0
+    phi[:, K // 2:, 1] = 1.0
+    phi /= phi.sum(axis=2, keepdims=True)
+    draws["phi_k"] = phi
+    x = np.ones((1, 600), dtype=np.int32)
+    x[0, 300:] = 2
+    data["x"] = x
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk", "zstar_t", "logp_zstar"])
+
+
 def test_large_K_unsupported_outputs(engine):
     import hhmm_amd
     data, draws = synth.hmm_multinom(N=1, S=2, T=10, K=12, L=9)

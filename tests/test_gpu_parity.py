@@ -279,27 +279,61 @@ def test_viterbi_log_softmax_regimes(engine, oracle, model, scale):
     compare_all(got, ref, pars + ["pair_status"])
 
 
-@pytest.mark.parametrize("tiny", [1e-30, 1e-70])
-def test_gamma_profile_near_impossible_runs(engine, oracle, tiny):
-    """The gamma profile renormalises every 4 steps (FB_BIG, kBigRenorm): a
-    run of observations that every state emits with probability `tiny`
-    shrinks the filter by ~tiny per step between renormalisations, far from
-    underflow for 1e-70 over 3 steps; results stay within tolerance of the
-    oracle's log-space recursion, on the lane decoder path of the 1M-pair bench."""
-    import hhmm_amd
-    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
-    data, draws = synth.hmm_multinom(N=64, S=64, T=200, K=4, L=9)
+def _near_impossible_runs(tiny, K=4, N=192, which=(70,)):
+    """hmm-multinom, zip pairing: the pairs in `which` emit symbol 9 with
+    probability `tiny` under every state (others keep their Dirichlet draw),
+    and every series holds a run of 40 nines -- so the waves of those pairs
+    shrink the filter by ~tiny per step while the other waves do not."""
+    data, draws = synth.hmm_multinom(N=N, S=N, T=200, K=K, L=9)
     phi = np.array(draws["phi_k"], dtype=np.float64)
-    phi[:, :, 8] = tiny
+    for p in which:
+        phi[p, :, 8] = tiny
     phi /= phi.sum(axis=2, keepdims=True)
     draws["phi_k"] = phi
     x = np.array(data["x"])
     x[:, 60:100] = 9
     data["x"] = x
-    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, pairing="zip",
-                       flags=_abi.FLAG_VIT_LANES, return_status=True)
+    return data, draws
+
+
+@pytest.mark.parametrize("tiny", [1e-30, 1e-70, 1e-90, 1e-200])
+@pytest.mark.parametrize("flags", [_abi.FLAG_VIT_LANES, _abi.FLAG_VIT_LANES | _abi.FLAG_FUSED,
+                                   _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT], ids=["default", "fused", "split"])
+def test_gamma_profile_near_impossible_runs(engine, oracle, tiny, flags):
+    """The gamma profile renormalises every 4 steps (FB_BIG, kBigRenorm) only
+    in waves whose pairs bound the 4-step shrink (renorm_sparse_safe: the
+    smallest emission times the smallest row / column max of A >= 2^-39);
+    a wave holding a pair with a symbol of probability 1e-90 or 1e-200 under
+    every state renormalises every step, which keeps the filter normal down to
+    ~1e-300 per step like the reference's log space.  Every schedule of the
+    C2 request (the bench's lane decoder, the fused sweep, the split
+    launches), against the oracle, with the safe and the dense waves in one
+    batch."""
+    import hhmm_amd
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    data, draws = _near_impossible_runs(tiny)
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, pairing="zip", flags=flags,
+                       return_status=True)
     ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True)
     compare_all(got, ref, pars + ["pair_status"])
+    assert np.isfinite(got["loglik"]).all()
+
+
+@pytest.mark.parametrize("tiny", [1e-70, 1e-90, 1e-200])
+@pytest.mark.parametrize("K", [12, 23])
+@pytest.mark.parametrize("pars", [["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
+                                  ["loglik", "alpha_tk", "beta_tk", "gamma_tk"]], ids=["gamma-only", "full"])
+def test_large_K_near_impossible_runs(engine, oracle, tiny, K, pars):
+    """The large-K filters' every-kLRenorm-steps cadence under the same
+    bound (hhmm_large.h, kLRenormSafeBound): pairs 5 and 70 carry the tiny
+    symbol, so their waves renormalise every step and the rest keep the
+    cadence; the gamma-only request runs the one-group-sum gamma."""
+    import hhmm_amd
+    data, draws = _near_impossible_runs(tiny, K=K, N=96, which=(5, 70))
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, pairing="zip", return_status=True)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True, nthreads=8)
+    compare_all(got, ref, pars + ["pair_status"])
+    assert np.isfinite(got["loglik"]).all()
 
 
 def test_unsupported_shape_leaves_no_kernel_running(engine, oracle):
