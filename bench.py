@@ -62,10 +62,11 @@ def parse():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the 64-pair oracle check of the timed data (run after warmup, outside the "
                          "timed region)")
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "n1", "f1"],
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "n1", "n2", "f1"],
                     help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
                          "printed as its own line: c1 hmm Gaussian K=3 T=500, c3 iohmm-reg grid, c4 iohmm-hmix "
                          "+ FFBS, c5 Tayal T=1e6 (parallel scan over T); n1 = hmm-multinom at K=23 (SURVEY §8 N1); "
+                         "n2 = hmm-multinom K=23, T=1e6, 250 pairs (the large-K parallel scan, MFMA chunk products); "
                          "f1 = the tick -> leg feature extractor (SURVEY §8 F1)")
     ap.add_argument("--ticks", type=int, default=100_000_000, help="f1: ticks per GPU")
     ap.add_argument("--pars", default=None,
@@ -549,6 +550,12 @@ WORKLOADS = {
            ["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
            lambda T, S: 23 * 8 + 4 + 4 / S + 8 * (23 + 23 * 23 + 23 * 9) / T,
            "N1 hmm-multinom K=23 L=9 T=1000 (large-K state-parallel kernels), 1000 series x 100 draws, grid"),
+    "n2": ("hmm-multinom", dict(N=1, S=250, T=1_000_000, K=23, L=9), "grid",
+           ["loglik", "gamma_tk"],
+           lambda T, S: 23 * 8 + 4 / S + (8 * (23 + 23 * 23 + 23 * 9) + 8) / T,
+           "N2 hmm-multinom K=23 L=9 T=1e6, 1 series x 250 draws (a flattened-HHMM-sized state space over a long "
+           "tick series): parallel scan over T with fp64 MFMA chunk products (hhmm_lkscan.h); forward-backward "
+           "profile (loglik + gamma)"),
     "c5": ("hhmm-tayal2009", dict(N=1, S=250, T=1_000_000, L=9), "grid",
            ["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
            lambda T, S: 32 + 4 + 8 / S + (8 * (1 + 4 + 36) + 16) / T,
@@ -610,6 +617,51 @@ def prepare_other(a, lib, dev, rank):
                 T=T, outs=outs, status=status)
 
 
+F64_PEAK = 78.6e12      # FLOP/s, MI355X fp64 vector and fp64 matrix (dense) peak
+VALU_ISSUE = 1024 * 2.4e9 / 4.0  # wave-instructions/s: 1024 SIMDs x 2.4 GHz, 4 cycles per fp64-rate VALU op
+
+
+def load_workload_pmc(name):
+    """Per-step PMC totals of workload `name` (tools/pmc_workloads.sh ->
+    tools/workload_pmc.py -> profiles/bench_traffic.json["workloads"]), or {}."""
+    try:
+        bt = json.loads((ROOT / "profiles" / "bench_traffic.json").read_text())
+        return bt.get("workloads", {}).get(name, {}) or {}
+    except Exception:
+        return {}
+
+
+def compute_rooflines(name, B, units, dev_ms, algo_flops=None):
+    """HBM roofline of the whole request (algorithmic bytes over the live
+    duration) beside the VALU and, where the request uses the matrix cores,
+    the f64-MFMA ones: the committed PMC instruction counts per step over the
+    same live duration.  `bound` names the larger fraction."""
+    t = dev_ms * 1e-3
+    pm = load_workload_pmc(name)
+    hbm_frac = B * units / t / HBM_PEAK
+    r = {"kernel": "whole request", "bound": "hbm", "achieved": B * units / t / 1e9, "peak": HBM_PEAK / 1e9,
+         "unit": "GB/s", "frac": hbm_frac, "traffic": pm.get("hbm_bytes_per_step"),
+         "algorithmic_bytes_per_series_timestep": B, "duration_ms": dev_ms, "pmc_source": pm.get("source")}
+    vi = pm.get("valu_insts_per_step")
+    if vi:
+        r["valu_insts_per_step"] = vi
+        r["valu_frac"] = vi / t / VALU_ISSUE
+        r["valu_frac_definition"] = ("SQ_INSTS_VALU per step x 4 cycles / (1024 SIMDs x 2.4 GHz x live step "
+                                     "time); every VALU op priced at the fp64 issue rate")
+    mi = pm.get("mfma_f64_insts_per_step")
+    if mi:
+        r["mfma_f64_insts_per_step"] = mi
+        r["mfma_frac"] = mi * 2048.0 / t / F64_PEAK
+        r["mfma_frac_definition"] = ("v_mfma_f64_16x16x4_f64 instructions per step (PMC SQ_INSTS_VALU_MFMA_F64) x "
+                                     "2048 FLOP / live step time / 78.6 TFLOP/s")
+    if algo_flops:
+        r["algorithmic_flops_per_step"] = algo_flops
+        r["algorithmic_mfma_frac"] = algo_flops / t / F64_PEAK
+    cands = {"hbm": hbm_frac, "valu": r.get("valu_frac", 0.0), "mfma": r.get("mfma_frac", 0.0)}
+    r["bound"] = max(cands, key=cands.get)
+    return r
+
+
 def other_workload(a, lib, rk):
     """C3 / C4 / C5: one request per step through hhmm_run_device on resident
     device buffers (synthetic inputs from hhmm_amd.synth, copied once)."""
@@ -638,9 +690,8 @@ def other_workload(a, lib, rk):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (hhmm_amd.synth generators, seeded)",
             "config": {"workload": desc, "model": model, "pairs_per_gpu": P, "T": T, "outputs": pars},
-            "roofline": {"kernel": "whole request", "bound": "hbm", "achieved": B * units / (dev_ms * 1e-3) / 1e9,
-                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": B * units / (dev_ms * 1e-3) / HBM_PEAK,
-                         "traffic": None, "algorithmic_bytes_per_series_timestep": B, "duration_ms": dev_ms},
+            "roofline": compute_rooflines(a.workload, B, units, dev_ms,
+                                          algo_flops=(2.0 * kw["K"] ** 3 * units if a.workload == "n2" else None)),
             "rank_ms_per_step": [x / a.steps * 1e3 for x in per_rank],
             "pair_failures": int((status != 0).sum().item()),
         }

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "hhmm_internal.h"
+#include "build_id.h" /* HHMM_SOURCE_HASH (Makefile) */
 
 namespace hhmm {
 
@@ -494,7 +495,7 @@ using namespace hhmm;
 
 extern "C" {
 
-const char *hhmm_version(void) { return "hhmm-mi355x 0.2.0 gfx950 abi 2"; }
+const char *hhmm_version(void) { return "hhmm-mi355x 0.3.0 gfx950 abi 2 src " HHMM_SOURCE_HASH; }
 
 const char *hhmm_last_error(void) { return g_last_error.c_str(); }
 

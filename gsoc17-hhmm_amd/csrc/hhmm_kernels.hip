@@ -100,11 +100,32 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
     const uint32_t fb_out = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
                             HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
     /* the log-scale outputs run the sequential log-space recursion (hhmm_hmm.h) */
-    if (!family || K > kMaxK || (flags & HHMM_FLAG_SCAN_OFF) ||
+    if (!family || (flags & HHMM_FLAG_SCAN_OFF) ||
         (outputs & (HHMM_OUT_FFBS | HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) || !(outputs & fb_out))
         return sp;
-    const int C = fb_chunk(K);
     const int log2cl = (int)((flags >> 8) & 0xffu);
+    if (K > kMaxK) {
+        /* large K (hhmm_lkscan.h): hmm-multinom; chunks a multiple of the
+         * 32-step observation blocks; automatic when the batch is under 4096
+         * pairs (2048 waves of two groups: two per SIMD) and long, with about
+         * 64k (pair, chunk) groups for the chunks' sweeps */
+        if (model != HHMM_MODEL_HMM_MULTINOM || K > kMaxKLarge)
+            return sp;
+        if (!(flags & HHMM_FLAG_SCAN_FORCE) && !(P < 4096 && Tmax >= 8192))
+            return sp;
+        int cl = 256;
+        if (log2cl > 0) {
+            cl = max(32, 1 << log2cl);
+        } else {
+            while ((int64_t)P * ((Tmax + cl - 1) / cl) > 65536 && cl < (1 << 20))
+                cl *= 2;
+        }
+        cl = (cl + 31) & ~31;
+        sp.cl = cl;
+        sp.nc = (Tmax + cl - 1) / cl;
+        return sp;
+    }
+    const int C = fb_chunk(K);
     /* a batch of under 16384 pairs (256 waves: a quarter of the chip's SIMDs)
      * is latency-bound on its T sequential steps already at T of a few hundred:
      * chunks of 4 C steps (C1, 1000 pairs x T = 500: 0.32 -> 0.10 ms) */
@@ -177,8 +198,21 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     const size_t d = sizeof(double);
     w.sp = scan_plan(model, K, Tmax, P, outputs, flags);
     if (large_k(K)) {
-        if (needs_ckpt(model, outputs))
+        if (w.sp.cl > 0) {
+            /* hhmm_lkscan.h: chunk products [P][nc][K][K] and row exponents
+             * [P][nc][K]; entry states, their log scales and exit betas per
+             * (pair, chunk); the chunks' sweeps' checkpoints [rows][K][P * nc] */
+            const size_t nc = (size_t)w.sp.nc, Q = (size_t)P * nc;
+            w.mf = take(Q * K * K * d);
+            w.mx = take(Q * K * d);
+            w.st = take(Q * K * d);
+            w.sl = take(Q * d);
+            w.be = take(Q * K * d);
+            if (needs_ckpt(model, outputs))
+                w.ckpt = take((size_t)((w.sp.cl + 7) / 8) * K * Q * d);
+        } else if (needs_ckpt(model, outputs)) {
             w.ckpt = take((size_t)((Tmax + 7) / 8) * K * P * d);
+        }
         if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
             w.bp = take((size_t)P * K * (size_t)((Tmax + 15) & ~15));
         w.total = off + 256;

@@ -136,8 +136,15 @@ struct LkLane {
     bool dense;        /* wave-uniform: renormalise every step (kLRenormSafeBound) */
 };
 
+/* The group index of this lane's group (blockIdx.x * groups per block + group), clamped to nq - 1. */
+template <int G>
+__device__ __forceinline__ int64_t lk_group(int64_t nq)
+{
+    return min((int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G, nq - 1);
+}
+
 template <int MODEL, int G, int KM>
-__device__ __forceinline__ void lk_setup(LkLane<MODEL, G, KM> &ln, const DevArgs &a, double *lds, bool LOG)
+__device__ __forceinline__ void lk_setup(LkLane<MODEL, G, KM> &ln, const DevArgs &a, double *lds, bool LOG, int64_t p)
 {
     const int tid = threadIdx.x;
     const int g = tid / G;                 /* group in the workgroup */
@@ -146,7 +153,7 @@ __device__ __forceinline__ void lk_setup(LkLane<MODEL, G, KM> &ln, const DevArgs
     ln.K = a.K;
     ln.L = a.L;
     ln.on = ln.j < a.K;
-    ln.p = min((int64_t)blockIdx.x * gpb + g, a.P - 1);
+    ln.p = p;
     pair_coords(a, ln.p, ln.n, ln.d);
     ln.Tp = pair_len(a, ln.n);
     const int jj = ln.on ? ln.j : 0;
@@ -380,28 +387,42 @@ __device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLa
         out[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
 }
 
-/* Forward-backward: loglik, alpha, beta, ungamma, gamma. */
+/* Forward-backward: loglik, alpha, beta, ungamma, gamma.  One group sweeps a
+ * whole series, or -- under the parallel scan over T (a.scan_cl > 0,
+ * hhmm_lkscan.h) -- one T-chunk [t0, t1) of a pair (group q = pair + P *
+ * chunk), entering with the forward state f_{t0-1} and leaving with beta at
+ * t1 - 1 that the scan computed (the log-likelihood is the scan's then). */
 template <int MODEL, int G, int KM>
 __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
+    const bool scan = a.scan_cl > 0;
+    const int64_t nq = scan ? a.P * (int64_t)a.scan_nc : a.P;
+    const int64_t q = lk_group<G>(nq);
+    const int64_t pq = scan ? q % a.P : q;
+    const int cq = scan ? (int)(q / a.P) : 0;
     LkLane<MODEL, G, KM> ln;
-    lk_setup<MODEL, G, KM>(ln, a, lds, false);
+    lk_setup<MODEL, G, KM>(ln, a, lds, false, pq);
     const uint32_t out = a.outputs;
     const bool need_bwd = (out & (HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
     const bool gamma_only = (out & (HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) ==
                             HHMM_OUT_GAMMA && a.gamma;
-    const int Tp = ln.Tp; /* per pair: uniform over the group (the wave's two groups may differ) */
+    /* this group's span (uniform over the group; the wave's two groups may differ) */
+    const int t0 = scan ? cq * a.scan_cl : 0;
+    const int t1 = scan ? max(min(t0 + a.scan_cl, ln.Tp), t0) : ln.Tp;
     const int K = ln.K;
+    const int64_t sbase = ((int64_t)pq * a.scan_nc + cq) * K + (ln.on ? ln.j : 0); /* scan vectors */
     double w[KM];
     int slot = 0;
-    auto ckpt = [&](int c) -> double & { return a.ckpt[ln.p + a.P * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
+    auto ckpt = [&](int c) -> double & { return a.ckpt[q + nq * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
 
-    /* ---- forward: alpha_1 (hmm.stan:30 Q2 / hmm-multinom.stan:31), then the recursion ---- */
-    LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, 0), bnxt = lk_block<MODEL, G, KM>(ln, a, 1);
-    double al, lsc = 0.0;
+    /* ---- forward: alpha_1 (hmm.stan:30 Q2 / hmm-multinom.stan:31), or the
+     * scan's entry state, then the recursion ---- */
+    LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, t0 / G), bnxt = lk_block<MODEL, G, KM>(ln, a, t0 / G + 1);
+    double al = 0.0, lsc = 0.0;
     int ex = 0;
-    {
+    int tb = t0;
+    if (t0 == 0) {
         int x;
         double xr, m;
         lk_get<MODEL, G>(bcur, 0, x, xr);
@@ -416,14 +437,21 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             al = ln.on ? ln.pj * e : 0.0;
         }
         al = grp_renorm<G>(al, ex);
+        if (t1 > 0) {
+            if (need_bwd) {
+                if (ln.on)
+                    ckpt(0) = al;
+            } else if ((out & HHMM_OUT_ALPHA) && a.alpha) {
+                lk_put<MODEL, G, KM>(a.alpha, a, ln, 0, al / grp_sum<G>(al));
+            }
+        }
+        tb = 1;
+    } else {
+        bnxt = bcur; /* the first step (t0 % G == 0) moves bnxt into bcur and fetches the next block */
+        al = (ln.on && t0 < t1) ? a.sc_st[sbase] : 0.0;
+        lsc = t0 < t1 ? a.sc_sl[(int64_t)pq * a.scan_nc + cq] : 0.0;
     }
-    if (need_bwd) {
-        if (ln.on)
-            ckpt(0) = al;
-    } else if ((out & HHMM_OUT_ALPHA) && a.alpha) {
-        lk_put<MODEL, G, KM>(a.alpha, a, ln, 0, al / grp_sum<G>(al));
-    }
-    for (int t = 1; t < Tp; ++t) {
+    for (int t = tb; t < t1; ++t) {
         const int u = t % G;
         if (u == 0) { /* group-uniform: next block of observations, prefetch the one after */
             bcur = bnxt;
@@ -440,36 +468,37 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         if (!need_bwd) {
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
                 lk_put<MODEL, G, KM>(a.alpha, a, ln, t, al / grp_sum<G>(al));
-        } else if (t % kLChunk == 0 && ln.on) {
-            ckpt(t / kLChunk) = al;
+        } else if ((t - t0) % kLChunk == 0 && ln.on) {
+            ckpt((t - t0) / kLChunk) = al;
         }
     }
-    {
+    if (!scan) {
         const double sa = grp_sum<G>(al); /* every lane takes part in the shuffle */
         if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0)
             a.loglik[ln.p] = log(sa) + (lsc + kLn2 * ex);
     }
-    if (!need_bwd)
+    if (!need_bwd || t1 <= t0)
         return;
 
     /* ---- backward sweep, chunk by chunk from the end: recompute alpha from
      * the checkpoint (prefetched a chunk ahead), then walk the chunk
      * backwards emitting the posteriors and stepping beta (bwd_chunk) ---- */
-    double be = ln.on ? 1.0 : 0.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
+    double be = ln.on ? (scan ? a.sc_be[sbase] : 1.0) : 0.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
     int bex = 0;
     constexpr int CPB = G / kLChunk; /* chunks per observation block */
-    const int nck = (Tp + kLChunk - 1) / kLChunk;
+    const int nck = (t1 - t0 + kLChunk - 1) / kLChunk;
+    const int b0 = t0 / G; /* the span starts on a block boundary */
     int cb = (nck - 1) / CPB;
-    LkObs<MODEL, G> ob = lk_block<MODEL, G, KM>(ln, a, cb), obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
+    LkObs<MODEL, G> ob = lk_block<MODEL, G, KM>(ln, a, b0 + cb), obp = lk_block<MODEL, G, KM>(ln, a, b0 + cb - 1);
     double ck = ckpt(nck - 1), ckn = ckpt(max(nck - 2, 0));
     for (int c = nck - 1; c >= 0; --c) {
         if (c / CPB != cb) { /* group-uniform: step back one observation block */
             cb = c / CPB;
             ob = obp;
-            obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
+            obp = lk_block<MODEL, G, KM>(ln, a, b0 + cb - 1);
         }
-        const int t0 = c * kLChunk;
-        const int ub = t0 % G; /* the chunk's first step inside the block */
+        const int tc = t0 + c * kLChunk;
+        const int ub = tc % G; /* the chunk's first step inside the block */
         double es[kLChunk];
 #pragma unroll
         for (int u = 0; u < kLChunk; ++u) {
@@ -486,16 +515,16 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
 #pragma unroll
         for (int u = 1; u < kLChunk; ++u) {
             abuf[u] = 0.0;
-            if (t0 + u < Tp) { /* group-uniform */
+            if (tc + u < t1) { /* group-uniform */
                 grp_exchange<G, KM>(ln.xch, slot, ln.j, abuf[u - 1], w);
                 slot ^= 1;
-                abuf[u] = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb, t0 + u, ln.dense);
+                abuf[u] = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb, tc + u, ln.dense);
             }
         }
 #pragma unroll
         for (int u = kLChunk - 1; u >= 0; --u) {
-            const int t = t0 + u;
-            if (t >= Tp)
+            const int t = tc + u;
+            if (t >= t1)
                 continue;
             const double av = abuf[u];
             if (gamma_only) {
@@ -529,7 +558,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
                 }
             }
             }
-            if (t > 0) {
+            if (t > t0) {
                 grp_exchange<G, KM>(ln.xch, slot, ln.j, es[u] * be, w);
                 slot ^= 1;
                 be = grp_renorm_at<G>(lk_bwd<MODEL, G, KM>(ln, w), bex, t, ln.dense);
@@ -583,7 +612,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
     LkLane<MODEL, G, KM> ln;
-    lk_setup<MODEL, G, KM>(ln, a, lds, true);
+    lk_setup<MODEL, G, KM>(ln, a, lds, true, lk_group<G>(a.P));
     const int Tp = ln.Tp;
     const int K = ln.K;
     double w[KM];
@@ -683,58 +712,6 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
         q0 = q1;
         q1 = q2;
     }
-}
-
-/* LDS bytes of a launch with `threads` lanes: exchange slots + tables. */
-template <int G>
-static inline size_t lk_lds(const DevArgs &a, int threads, bool discrete)
-{
-    const size_t groups = (size_t)threads / G;
-    return groups * 2 * G * sizeof(double) + (discrete ? groups * (size_t)a.L * G * sizeof(double) : 0);
-}
-
-template <int MODEL, int G, int KM>
-static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
-{
-    constexpr bool discrete = !LkTraits<MODEL>::kGauss;
-    const uint32_t out = a.outputs;
-    const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
-    const uint32_t vit = HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
-    if (out & ~(fb | vit)) {
-        set_error("K = %d > %d: this build evaluates loglik, alpha, beta, ungamma, gamma, zstar and logp_zstar "
-                  "(no log-scale unalpha / unbeta, no FFBS)", a.K, kMaxK);
-        return HHMM_ERR_UNSUPPORTED;
-    }
-    int threads = kBlock;
-    while (threads > G && lk_lds<G>(a, threads, discrete) > kLdsLimit)
-        threads /= 2;
-    if (lk_lds<G>(a, threads, discrete) > kLdsLimit) {
-        set_error("emission table of L = %d symbols does not fit in LDS", a.L);
-        return HHMM_ERR_UNSUPPORTED;
-    }
-    const int gpb = threads / G;
-    const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
-    /* checkpoints use the [rows][K][P] layout of the lane kernels.  With both
-     * halves requested the decoder runs on the library's side stream, forked
-     * from and joined back into the caller's: the two kernels' registers fit
-     * one wave of each per SIMD (K <= 24: 224 + 160), so they overlap */
-    hipStream_t vs = st;
-    if ((out & fb) && (out & vit) && !(a.flags & HHMM_FLAG_NO_FUSE)) {
-        const hhmm_status r = fork_stream(st, &vs);
-        if (r != HHMM_OK)
-            return r;
-    }
-    if (out & vit)
-        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), vs, a);
-    if (out & fb)
-        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
-    hipError_t e = hipGetLastError();
-    const hhmm_status j = (vs != st) ? join_stream(st, vs) : HHMM_OK;
-    if (e != hipSuccess) {
-        set_error("large-K kernel launch: %s", hipGetErrorString(e));
-        return HHMM_ERR_HIP;
-    }
-    return j;
 }
 
 } // namespace hhmm

@@ -1,0 +1,405 @@
+/*
+ * hhmm_lkscan.h -- the parallel scan over T at large K (8 < K <= 32; SURVEY.md
+ * §8 A16 + N1, the verdict's N2): hmm-multinom with few pairs and long series,
+ * e.g. a flattened HHMM with 23 states (log.md:657-658) over a tick series of
+ * 10^6 zig-zags (tayal2009/main.Rmd:310-346).  The sequential state-parallel
+ * kernels (hhmm_large.h) give one 32-lane group per pair: 250 pairs are 125
+ * waves on a 1024-SIMD chip, and 10^6 dependent steps each.
+ *
+ * The forward map is linear, f_t = f_{t-1} F_t with F_t = A diag(e_t), and
+ * the backward map uses the same matrices, beta_{t-1} = F_t beta_t
+ * (hmm-multinom.stan:36-44 forward, :73-88 backward: no masks in this
+ * program).  So ONE chunk product M_c = prod_{t in chunk c} F_t serves both
+ * scans:
+ *   phase 1  (lks_prod_kernel, MFMA) the chunk products.  Row i of M_c is the
+ *            forward filter started from state i at the chunk's entry, i.e.
+ *            column i of M_c^T, and v <- diag(e_t) A^T v is a dense K x K by
+ *            K x 16 product for 16 such columns that share the pair's A: the
+ *            batched K x K contraction the north star reserves the matrix
+ *            cores for.  v_mfma_f64_16x16x4_f64 with A^T as the A operand
+ *            (fixed in registers for the whole chunk) and the columns as the
+ *            B operand; the result registers of one step ARE the next step's
+ *            B operand (C/D row (lane>>4) + 4r = B row of k-step r), so the
+ *            recursion needs no lane movement.  After every step each column
+ *            (one filter) is renormalised by an exact power of two and its
+ *            exponent kept: M_c = diag(2^s) M'_c.
+ *   phase 2  (lks_bound_kernel, one wave per pair) the forward scan over the
+ *            chunks (the filter entering each chunk, its log scale, the
+ *            log-likelihood) and the backward scan (beta at each chunk's last
+ *            step), with the row exponents folded in exactly.
+ *   phase 3  (lk_fb_kernel over (pair, chunk) groups, hhmm_large.h) the
+ *            forward-backward sweep of every chunk from those vectors:
+ *            alpha, beta, ungamma, gamma.
+ * The chunk products' entries are sums of non-negative terms, so they keep
+ * their relative precision like the sequential recursion; the outputs are
+ * tolerance outputs (1e-9 relative), the Viterbi stays sequential (exact).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "hhmm_large.h"
+
+namespace hhmm {
+
+typedef double lks_d4 __attribute__((ext_vector_type(4)));
+
+/* v_mfma_f64_16x16x4_f64 operand maps (cdna_hip_programming.md §3, "f64 MFMA
+ * does NOT use these maps"): lane l holds A[row l & 15][k l >> 4] and
+ * B[k l >> 4][col l & 15]; result register r holds D[row (l >> 4) + 4r][col l & 15]. */
+__device__ __forceinline__ lks_d4 lks_mfma(double a, double b, lks_d4 c)
+{
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+/* Columns of M'^T per wave: TPW tiles of 16.  RT row tiles of 16 states, KSM
+ * k-steps of 4 states (K <= 16: 1 / 4; K <= 24: 2 / 6; K <= 32: 2 / 8). */
+constexpr int kLksTiles = 2;
+
+template <int RT, int KSM>
+__global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
+{
+    constexpr int TPW = kLksTiles;
+    constexpr int KR = 16 * RT; /* padded rows of the emission table */
+    HIP_DYNAMIC_SHARED(double, lds)
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int K = a.K, cl = a.scan_cl, nc = a.scan_nc;
+    const int ks = (K + 3) / 4;
+    const int ntile = (nc * K + 15) / 16;
+    const int wpp = (ntile + TPW - 1) / TPW;
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const int64_t p = min(w / wpp, a.P - 1); /* surplus waves redo the last pair's last tiles */
+    const int tg = (int)min(w - p * wpp, (int64_t)wpp - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int64_t S = a.S;
+
+    /* the pair's emission table phi[l][j] (rows j >= K zero), one per wave */
+    double *tab = lds + (size_t)wv * a.L * KR;
+    for (int idx = lane; idx < a.L * KR; idx += 64) {
+        const int l = idx / KR, j = idx - l * KR;
+        tab[idx] = j < K ? a.phi_k[d + S * ((int64_t)j + (int64_t)K * l)] : 0.0;
+    }
+    /* A operand: Aop[rt][kk] = A^T[j][i] = A(i, j), i = 4kk + (lane >> 4), j = 16rt + (lane & 15) */
+    double aop[RT][KSM];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk) {
+            const int i = 4 * kk + (lane >> 4), j = 16 * rt + (lane & 15);
+            aop[rt][kk] = (i < K && j < K) ? a.A_ij[d + S * ((int64_t)i + (int64_t)K * j)] : 0.0;
+        }
+    __syncthreads();
+
+    /* this lane's column in each tile: (chunk c, initial state i); B operand
+     * Q[u][kk] = row 4kk + (lane >> 4) of the column */
+    double q[TPW][KSM];
+    int ex[TPW], t0[TPW], t1[TPW];
+    bool valid[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int col = (tg * TPW + u) * 16 + (lane & 15);
+        valid[u] = col < nc * K;
+        const int c = valid[u] ? col / K : 0, i = valid[u] ? col - c * K : 0;
+        t0[u] = c * cl;
+        t1[u] = valid[u] ? min(t0[u] + cl, Tp) : t0[u];
+        ex[u] = 0;
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            q[u][kk] = (valid[u] && 4 * kk + (lane >> 4) == i) ? 1.0 : 0.0;
+    }
+    /* the wave's step count: the longest of its columns' chunks */
+    int smax = 0;
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+        smax = max(smax, t1[u] - t0[u]);
+    smax = wave_max(smax);
+
+    /* observations a block of kB steps ahead (clamped, unconditional) */
+    constexpr int kB = 8;
+    auto ldx = [&](int u, int s) -> int {
+        const int t = min(max(t0[u] + s, 0), a.Tmax - 1);
+        return a.x[n + a.N * (int64_t)t];
+    };
+    int xb[TPW][kB], xn[TPW][kB];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int v = 0; v < kB; ++v)
+            xb[u][v] = ldx(u, v);
+    for (int s0 = 0; s0 < smax; s0 += kB) {
+#pragma unroll
+        for (int u = 0; u < TPW; ++u)
+#pragma unroll
+            for (int v = 0; v < kB; ++v)
+                xn[u][v] = ldx(u, s0 + kB + v);
+#pragma unroll
+        for (int v = 0; v < kB; ++v) {
+            const int s = s0 + v;
+            if (s >= smax)
+                break;
+            /* D = A^T Q for every tile (independent accumulators interleaved) */
+            lks_d4 acc[TPW][RT];
+#pragma unroll
+            for (int u = 0; u < TPW; ++u)
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+                    acc[u][rt] = lks_d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kk = 0; kk < KSM; ++kk) {
+                if (kk < ks) {
+#pragma unroll
+                    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt)
+                            acc[u][rt] = lks_mfma(aop[rt][kk], q[u][kk], acc[u][rt]);
+                }
+            }
+            /* emission of the column's step, renormalisation of the column */
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                const int t = t0[u] + s;
+                const bool on = t >= 1 && t < t1[u];
+                const int xc = min(max(xb[u][v], 1), a.L);
+                const double *row = tab + (xc - 1) * KR + (lane >> 4);
+                double nv[KSM];
+                double mx = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < KSM; ++kk) {
+                    const double e = row[4 * kk];
+                    nv[kk] = acc[u][kk >> 2][kk & 3] * e;
+                    mx = fmax(mx, nv[kk]);
+                }
+                mx = fmax(mx, __shfl_xor(mx, 16));
+                mx = fmax(mx, __shfl_xor(mx, 32));
+                const int e2 = __builtin_amdgcn_frexp_exp(mx);
+#pragma unroll
+                for (int kk = 0; kk < KSM; ++kk)
+                    q[u][kk] = on ? ldexp(nv[kk], -e2) : q[u][kk];
+                ex[u] += on ? e2 : 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < TPW; ++u)
+#pragma unroll
+            for (int v = 0; v < kB; ++v)
+                xb[u][v] = xn[u][v];
+    }
+    /* M'_c[i][j] (row i = this column, j = 4kk + (lane >> 4)) and the row
+     * exponent (-inf: the filter died, the row is zero) */
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        if (!valid[u])
+            continue;
+        const int col = (tg * TPW + u) * 16 + (lane & 15);
+        const int c = col / K, i = col - c * K;
+        double *m = a.sc_mf + (((int64_t)p * nc + c) * K + i) * K;
+        double mx = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk) {
+            const int j = 4 * kk + (lane >> 4);
+            if (j < K)
+                m[j] = q[u][kk];
+            mx = fmax(mx, q[u][kk]);
+        }
+        mx = fmax(mx, __shfl_xor(mx, 16));
+        mx = fmax(mx, __shfl_xor(mx, 32));
+        if ((lane >> 4) == 0)
+            a.sc_mx[((int64_t)p * nc + c) * K + i] = mx > 0.0 ? (double)ex[u] : dev_ninf();
+    }
+}
+
+/* Phase 2: one wave per pair, lane j = state j (j < K).  The chunk's M' is
+ * staged in LDS (K*K doubles) from a coalesced load that runs one chunk ahead. */
+template <int KM>
+__device__ __forceinline__ void lks_stage_load(const DevArgs &a, int64_t p, int c, double (&r)[(KM * KM + 63) / 64])
+{
+    const int K = a.K, nc = a.scan_nc;
+    const double *m = a.sc_mf + ((int64_t)p * nc + max(c, 0)) * K * K;
+#pragma unroll
+    for (int v = 0; v < (KM * KM + 63) / 64; ++v) {
+        const int idx = v * 64 + (int)(threadIdx.x & 63);
+        r[v] = idx < K * K ? m[idx] : 0.0;
+    }
+}
+
+template <int KM>
+__global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
+{
+    __shared__ double mt[KM * KM];
+    __shared__ double xv[64];
+    constexpr int NV = (KM * KM + 63) / 64;
+    const int64_t p = blockIdx.x;
+    const int j = threadIdx.x;
+    const int K = a.K, nc = a.scan_nc, cl = a.scan_cl;
+    const bool on = j < K;
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int ncp = (Tp + cl - 1) / cl;
+    const int64_t S = a.S;
+    const int jj = on ? j : 0;
+    auto base = [&](int c) { return ((int64_t)p * nc + c); };
+    auto wmax_d = [&](double v) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+            v = fmax(v, __shfl_xor(v, off));
+        return v;
+    };
+    auto wmax_i = [&](int v) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+            v = max(v, __shfl_xor(v, off));
+        return v;
+    };
+    auto wsum_d = [&](double v) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+            v += __shfl_xor(v, off);
+        return v;
+    };
+    /* exponent of a row: frexp exponent of the value + the row's scale; INT_MIN/2 for a zero */
+    constexpr int kDead = -(1 << 29);
+
+    /* ---- forward: f_0 = p_1k .* phi[., x_1] (hmm-multinom.stan:31), then f <- f M_c ---- */
+    const int x0 = min(max(a.x[n], 1), a.L);
+    double f = on ? a.p_1k[d + S * jj] * a.phi_k[d + S * ((int64_t)jj + (int64_t)K * (x0 - 1))] : 0.0;
+    int fe = __builtin_amdgcn_frexp_exp(wmax_d(f));
+    f = ldexp(f, -fe);
+    double lsc = kLn2 * fe;
+    double rb[NV];
+    lks_stage_load<KM>(a, p, 0, rb);
+    for (int c = 0; c < ncp; ++c) {
+        if (c > 0 && on) {
+            a.sc_st[base(c) * K + j] = f;
+            if (j == 0)
+                a.sc_sl[base(c)] = lsc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (v * 64 + j < KM * KM)
+                mt[v * 64 + j] = rb[v];
+        lks_stage_load<KM>(a, p, min(c + 1, ncp - 1), rb);
+        const double sr = on ? a.sc_mx[base(c) * K + j] : dev_ninf();
+        const int er = (f != 0.0 && sr != dev_ninf()) ? __builtin_amdgcn_frexp_exp(f) + (int)sr : kDead;
+        const int em = wmax_i(er);
+        xv[j] = (er == kDead || em == kDead) ? 0.0 : ldexp(f, (int)sr - em);
+        __syncthreads();
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < KM; ++i)
+            if (i < K)
+                acc[i & 3] = fma(xv[i], mt[i * K + jj], acc[i & 3]);
+        double nf = on ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+        const int e2 = __builtin_amdgcn_frexp_exp(wmax_d(nf));
+        f = ldexp(nf, -e2);
+        lsc += kLn2 * ((double)(em == kDead ? 0 : em) + e2);
+    }
+    const double sf = wsum_d(on ? f : 0.0);
+    if (j == 0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+        a.loglik[p] = log(sf) + lsc;
+
+    /* ---- backward: beta_T = 1 (unbeta_tk[T] = 1, Q1); b_{c-1} = M_c b_c ---- */
+    double b = on ? 1.0 : 0.0;
+    if (on && ncp > 0)
+        a.sc_be[base(ncp - 1) * K + j] = b;
+    lks_stage_load<KM>(a, p, ncp - 1, rb);
+    for (int c = ncp - 1; c >= 1; --c) {
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (v * 64 + j < KM * KM)
+                mt[v * 64 + j] = rb[v];
+        xv[j] = b;
+        lks_stage_load<KM>(a, p, c - 1, rb);
+        __syncthreads();
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < KM; ++i)
+            if (i < K)
+                acc[i & 3] = fma(mt[jj * K + i], xv[i], acc[i & 3]);
+        const double h = on ? (acc[0] + acc[1]) + (acc[2] + acc[3]) : 0.0;
+        const double sr = on ? a.sc_mx[base(c) * K + j] : dev_ninf();
+        const int er = (h != 0.0 && sr != dev_ninf()) ? __builtin_amdgcn_frexp_exp(h) + (int)sr : kDead;
+        const int em = wmax_i(er);
+        b = (er == kDead || em == kDead) ? 0.0 : ldexp(h, (int)sr - em);
+        if (on)
+            a.sc_be[base(c - 1) * K + j] = b;
+    }
+}
+
+/* LDS bytes of a launch with `threads` lanes: exchange slots + tables. */
+template <int G>
+static inline size_t lk_lds(const DevArgs &a, int threads, bool discrete)
+{
+    const size_t groups = (size_t)threads / G;
+    return groups * 2 * G * sizeof(double) + (discrete ? groups * (size_t)a.L * G * sizeof(double) : 0);
+}
+
+template <int MODEL, int G, int KM>
+static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
+{
+    constexpr bool discrete = !LkTraits<MODEL>::kGauss;
+    const uint32_t out = a.outputs;
+    const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
+    const uint32_t vit = HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+    if (a.scan_cl > 0 && (!discrete || a.L * 16 * ((KM + 15) / 16) * 4 * sizeof(double) > 64 * 1024)) {
+        set_error("K = %d: the parallel scan over T runs hmm-multinom with L <= %d", a.K, 64 * 1024 / (4 * 8 * 16 * ((KM + 15) / 16)));
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    if (out & ~(fb | vit)) {
+        set_error("K = %d > %d: this build evaluates loglik, alpha, beta, ungamma, gamma, zstar and logp_zstar "
+                  "(no log-scale unalpha / unbeta, no FFBS)", a.K, kMaxK);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    int threads = kBlock;
+    while (threads > G && lk_lds<G>(a, threads, discrete) > kLdsLimit)
+        threads /= 2;
+    if (lk_lds<G>(a, threads, discrete) > kLdsLimit) {
+        set_error("emission table of L = %d symbols does not fit in LDS", a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const int gpb = threads / G;
+    const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
+    /* checkpoints use the [rows][K][P] layout of the lane kernels.  With both
+     * halves requested the decoder runs on the library's side stream, forked
+     * from and joined back into the caller's: the two kernels' registers fit
+     * one wave of each per SIMD (K <= 24: 224 + 160), so they overlap */
+    hipStream_t vs = st;
+    if ((out & fb) && (out & vit) && !(a.flags & HHMM_FLAG_NO_FUSE)) {
+        const hhmm_status r = fork_stream(st, &vs);
+        if (r != HHMM_OK)
+            return r;
+    }
+    if (out & vit)
+        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), vs, a);
+    hipError_t e = hipGetLastError();
+    if ((out & fb) && a.scan_cl > 0 && e == hipSuccess) {
+        /* parallel scan over T (hhmm_lkscan.h): MFMA chunk products, the scan
+         * over chunks, then the chunks' sweeps as groups (pair, chunk) */
+        constexpr int RT = (KM + 15) / 16, KSM = KM / 4;
+        const int ntile = (a.scan_nc * a.K + 15) / 16;
+        const int64_t waves = a.P * (int64_t)((ntile + kLksTiles - 1) / kLksTiles);
+        const size_t plds = (size_t)4 * a.L * 16 * RT * sizeof(double);
+        hipLaunchKernelGGL((lks_prod_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
+        hipLaunchKernelGGL((lks_bound_kernel<KM>), dim3((unsigned)a.P), dim3(64), 0, st, a);
+        const int64_t nq = a.P * (int64_t)a.scan_nc;
+        if (out & (fb & ~HHMM_OUT_LOGLIK)) /* the chunks' sweeps: posteriors (the loglik is phase 2's) */
+            hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)), dim3(threads),
+                               lk_lds<G>(a, threads, discrete), st, a);
+        e = hipGetLastError();
+    } else if ((out & fb) && e == hipSuccess) {
+        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
+        e = hipGetLastError();
+    }
+    const hhmm_status j = (vs != st) ? join_stream(st, vs) : HHMM_OK;
+    if (e != hipSuccess) {
+        set_error("large-K kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return j;
+}
+
+} // namespace hhmm

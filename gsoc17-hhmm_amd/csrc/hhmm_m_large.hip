@@ -1,7 +1,7 @@
 /* hmm/stan/hmm.stan and hmm-multinom.stan at 8 < K <= 32: the state-parallel
  * kernels of hhmm_large.h, 16-lane groups up to K = 16 and
  * 32-lane groups above (24-state loops up to K = 24). */
-#include "hhmm_large.h"
+#include "hhmm_lkscan.h"
 
 namespace hhmm {
 

@@ -153,3 +153,25 @@ def test_no_cpu_fallback_without_gpu(engine):
 
 def test_version_string(engine):
     assert engine.hhmm_version().startswith(b"hhmm-mi355x")
+
+
+def _source_hash():
+    """sha256 over the library's sources in sorted-path order, as the Makefile
+    computes it for hhmm_version() (csrc/Makefile SRC_HASH)."""
+    import hashlib
+    import os
+    csrc = REPO / "gsoc17-hhmm_amd" / "csrc"
+    rel = [f for f in os.listdir(csrc) if f.endswith((".hip", ".cpp", ".h"))]
+    rel += ["../../include/" + f for f in os.listdir(REPO / "include") if f.endswith(".h")]
+    rel.append("Makefile")
+    h = hashlib.sha256()
+    for f in sorted(rel):
+        h.update((csrc / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def test_library_is_built_from_these_sources(engine):
+    """The shipped libhhmm.so names the hash of the sources it was built from;
+    it must be this tree's (a stale or foreign build fails here)."""
+    v = engine.hhmm_version().decode()
+    assert v.split(" src ")[-1] == _source_hash(), (v, _source_hash())
