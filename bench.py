@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--flags", type=int, default=0, help="c3-c5 probes: hhmm_request.flags")
     ap.add_argument("--fused", action="store_true",
                     help="time the one-kernel fused sweep (HHMM_FLAG_FUSED) instead of the two-kernel schedule")
+    ap.add_argument("--no-sequential", action="store_true",
+                    help="n2: skip the one untimed run on the sequential kernels after the timed region")
     ap.add_argument("--no-path-gather", action="store_true",
                     help="skip the timed D2H of the decoded paths after the timed region")
     ap.add_argument("--stub", action="store_true",
@@ -614,7 +616,7 @@ def prepare_other(a, lib, dev, rank):
         return keep
 
     return dict(step=step, model=model, kw=kw, pars=pars, bps=bps, desc=desc, data=data, draws=draws, P=P,
-                T=T, outs=outs, status=status)
+                T=T, outs=outs, status=status, req=req)
 
 
 F64_PEAK = 78.6e12      # FLOP/s, MI355X fp64 vector and fp64 matrix (dense) peak
@@ -682,6 +684,21 @@ def other_workload(a, lib, rk):
     dev_ms = ev[0].elapsed_time(ev[1]) / a.steps
     units = P * T
     B = bps(T, kw["S"])
+    sequential = None
+    if a.workload == "n2" and not a.no_sequential:
+        # after the timed region, once: the same request on the sequential
+        # state-parallel kernels (HHMM_FLAG_SCAN_OFF), what the scan replaces
+        req = w["req"]
+        keep_flags = req.flags
+        req.flags = keep_flags | _abi.FLAG_SCAN_OFF
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        run1()
+        e1.record()
+        torch.cuda.synchronize()
+        req.flags = keep_flags
+        sequential = {"ms": e0.elapsed_time(e1), "flags": "HHMM_FLAG_SCAN_OFF (lk_fb_kernel, one 32-lane group per pair)",
+                      "scan_speedup": e0.elapsed_time(e1) / dev_ms}
     if rank == 0:
         line = {
             "metric": "series-timesteps/sec (SURVEY §8d config) -- evidence line, not the headline",
@@ -695,6 +712,8 @@ def other_workload(a, lib, rk):
             "rank_ms_per_step": [x / a.steps * 1e3 for x in per_rank],
             "pair_failures": int((status != 0).sum().item()),
         }
+        if sequential:
+            line["sequential_after_timing"] = sequential
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_grid(model, data, draws, pars, T, a.cpu_seconds, a.seed)
         print(json.dumps(line), flush=True)

@@ -1044,9 +1044,10 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     }
 }
 
-/* One workgroup of the forward-backward: pairs [block * blockDim, +blockDim). */
+/* One wave of the forward-backward: pairs [64 gwave, 64 gwave + 64) (gwave =
+ * block * waves per block + wave in fb_kernel). */
 template <int MODEL, int K, int MODE, int PH>
-__device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
+__device__ __forceinline__ void fb_block(const DevArgs &a, int64_t gwave)
 {
     constexpr bool AUX = ModelTraits<MODEL>::kAux;
     HIP_DYNAMIC_SHARED(double2, lds)
@@ -1054,7 +1055,7 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
     const int wave = threadIdx.x >> 6;
     /* lanes past the last pair redo pair P-1 (identical values, benign
      * duplicate stores): every lane stays in the wave-wide reductions */
-    const int64_t p = min((int64_t)block * blockDim.x + threadIdx.x, a.P - 1);
+    const int64_t p = min(gwave * 64 + lane, a.P - 1);
     int64_t n, d;
     pair_coords(a, p, n, d);
     constexpr int KP = (K + 1) / 2;
@@ -1078,8 +1079,21 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
         al[k] = 0.0;
         be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1): beta_T uniform */
     }
-    if constexpr (fb_big(MODE)) {
-        if (wave_any(!renorm_sparse_safe<MODEL, K>(ln.pp, ln.slab, a.L))) {
+    if constexpr (fb_big(MODE) && !(MODE & FB_RN1)) {
+        const bool dense = wave_any(!renorm_sparse_safe<MODEL, K>(ln.pp, ln.slab, a.L));
+        if constexpr (PH == FB_PH_BOTH) {
+            /* a wave holding a pair without the bound appends itself to the
+             * list a.rnw (count, then wave ids) and leaves its sweep to
+             * fb_dense_kernel (per-step renormalisation), launched right after
+             * this kernel: the hot kernel carries one copy of the sweep */
+            if (dense) {
+                if (lane == 0) {
+                    const int slot = atomicAdd(&a.rnw[0], 1);
+                    a.rnw[1 + slot] = (int32_t)gwave;
+                }
+                return;
+            }
+        } else if (dense) { /* the split schedule's two launches decide alike */
             fb_sweep<MODEL, K, MODE | FB_RN1, false, PH>(a, ln, sp, al, 0.0, be, 0.0);
             return;
         }
@@ -1087,10 +1101,24 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, uint32_t block)
     fb_sweep<MODEL, K, MODE, false, PH>(a, ln, sp, al, 0.0, be, 0.0);
 }
 
+/* The FB_BIG waves fb_kernel listed in a.rnw, with per-step renormalisation:
+ * one-wave workgroups (one emission slab each) take list entries in turn;
+ * with none listed the launch reads the count and ends. */
+constexpr int kDenseBlocks = 256;
+template <int MODEL, int K, int MODE>
+__global__ void __launch_bounds__(64) fb_dense_kernel(const DevArgs a)
+{
+    const int n = __builtin_amdgcn_readfirstlane(a.rnw[0]);
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t gw = __builtin_amdgcn_readfirstlane(a.rnw[1 + i]);
+        fb_block<MODEL, K, MODE | FB_RN1, FB_PH_BOTH>(a, gw);
+    }
+}
+
 template <int MODEL, int K, int MODE, int PH = FB_PH_BOTH>
 __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
 {
-    fb_block<MODEL, K, MODE, PH>(a, blockIdx.x);
+    fb_block<MODEL, K, MODE, PH>(a, (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
 }
 
 /* ------------------------------------------------------------------ */
@@ -2449,9 +2477,15 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_FWD>), s.grid, s.block, s.lds, st, a);
     else if (MODEL == HHMM_MODEL_HMM_MULTINOM && a.xpk && !(a.outputs & extra) && ffbs)
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA | FB_FFBS | FB_PACK>), s.grid, s.block, s.lds, st, a);
-    else if (fb_big_ok<MODEL, K>() && a.xpk && !(a.outputs & extra))
-        hipLaunchKernelGGL((fb_kernel<MODEL, K, fb_big_ok<MODEL, K>() ? FB_GAMMA | FB_PACK | FB_BIG : FB_GAMMA>),
-                           s.grid, s.block, s.lds, st, a);
+    else if (fb_big_ok<MODEL, K>() && a.xpk && !(a.outputs & extra)) {
+        constexpr int BIG = fb_big_ok<MODEL, K>() ? FB_GAMMA | FB_PACK | FB_BIG : FB_GAMMA;
+        if constexpr (fb_big(BIG))
+            (void)hipMemsetAsync(a.rnw, 0, sizeof(int32_t), st); /* the dense-wave list's count */
+        hipLaunchKernelGGL((fb_kernel<MODEL, K, BIG>), s.grid, s.block, s.lds, st, a);
+        if constexpr (fb_big(BIG)) /* the waves it listed (renorm_sparse_safe) */
+            hipLaunchKernelGGL((fb_dense_kernel<MODEL, K, BIG>), dim3(kDenseBlocks), dim3(64),
+                               s.lds / (s.block.x / 64), st, a);
+    }
     else if (MODEL == HHMM_MODEL_HMM_MULTINOM && a.xpk && !(a.outputs & extra))
         hipLaunchKernelGGL((fb_kernel<MODEL, K, FB_GAMMA | FB_PACK>), s.grid, s.block, s.lds, st, a);
     else if ((a.outputs & extra) && ffbs)

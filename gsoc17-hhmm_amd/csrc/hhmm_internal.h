@@ -57,6 +57,7 @@ struct DevArgs {
     uint32_t *bp;       /* [nword][P]     packed Viterbi back-pointers */
     double *lam;        /* [Tmax][P]      IOHMM: running sum of log c_t (unbeta pass) */
     uint32_t *xpk;      /* [nchunk][P]    packed symbols of each checkpoint chunk (multinom, L <= 16) */
+    int32_t *rnw;       /* [waves]        FB_BIG: the wave renormalises every step (fb_dense_kernel) */
     /* parallel scan over T; scan_cl = 0: sequential sweeps */
     uint32_t flags;     /* hhmm_request.flags */
     int32_t scan_cl;    /* steps per T-chunk (multiple of fb_chunk(K)) */

@@ -176,7 +176,7 @@ int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t
 
 /* Offsets of every workspace region (SIZE_MAX = unused) and the total. */
 struct WsLayout {
-    size_t ckpt, ckpt_ls, xpk, bp, lam, mf, qb, mx, st, sl, be, bl, total;
+    size_t ckpt, ckpt_ls, xpk, rnw, bp, lam, mf, qb, mx, st, sl, be, bl, total;
     size_t vm, vm1, vd, vk, ve, vz, vf;
     int vnc;
     ScanPlan sp;
@@ -186,7 +186,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
 {
     WsLayout w;
     const size_t NONE = SIZE_MAX;
-    w.ckpt = w.ckpt_ls = w.xpk = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
+    w.ckpt = w.ckpt_ls = w.xpk = w.rnw = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
     w.vm = w.vm1 = w.vd = w.vk = w.ve = w.vz = w.vf = NONE;
     w.vnc = 0;
     size_t off = 0;
@@ -239,7 +239,10 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
         if (model == HHMM_MODEL_HMM_MULTINOM && L <= 16 && !(outputs & extra))
             /* ceil(T/8) words (8-step chunks, 1 word each) or ceil(T/32) * 4
              * (32-step chunks of the two-level recompute): at most T/8 + 4 */
+        {
             w.xpk = take(((size_t)nchunk_of(K, Tmax) + 4) * P * sizeof(uint32_t));
+            w.rnw = take(((size_t)P / 64 + 64) * sizeof(int32_t)); /* one flag per fb_kernel wave */
+        }
     }
     if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) {
         const int Tv = (model == HHMM_MODEL_TAYAL_LITE) ? Toos : Tmax;
@@ -275,6 +278,7 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
     a.ckpt = (double *)at_off(w.ckpt);
     a.ckpt_ls = (double *)at_off(w.ckpt_ls);
     a.xpk = (uint32_t *)at_off(w.xpk);
+    a.rnw = (int32_t *)at_off(w.rnw);
     a.bp = (uint32_t *)at_off(w.bp);
     a.lam = (double *)at_off(w.lam);
     a.scan_cl = w.sp.cl;

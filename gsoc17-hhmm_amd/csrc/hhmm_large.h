@@ -416,42 +416,20 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     int slot = 0;
     auto ckpt = [&](int c) -> double & { return a.ckpt[q + nq * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
 
-    /* ---- forward: alpha_1 (hmm.stan:30 Q2 / hmm-multinom.stan:31), or the
-     * scan's entry state, then the recursion ---- */
-    LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, t0 / G), bnxt = lk_block<MODEL, G, KM>(ln, a, t0 / G + 1);
+    /* ---- forward: alpha_1 (hmm.stan:30 Q2 / hmm-multinom.stan:31) at t = 0,
+     * or the scan's entry state, then the recursion.  Every group of the wave
+     * walks t = t0, t0 + 1, ... from a multiple of G (its span's start), so the
+     * step's position in the observation block, t % G, is the same for the
+     * wave's groups even when they belong to different T-chunks. ---- */
+    LkObs<MODEL, G> bcur, bnxt = lk_block<MODEL, G, KM>(ln, a, t0 / G);
+    bcur = bnxt;
     double al = 0.0, lsc = 0.0;
     int ex = 0;
-    int tb = t0;
-    if (t0 == 0) {
-        int x;
-        double xr, m;
-        lk_get<MODEL, G>(bcur, 0, x, xr);
-        if constexpr (LkTraits<MODEL>::kGauss) {
-            /* log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k): alpha_1 = p_1k */
-            const double z = (xr - ln.mu) * ln.isig;
-            const double tk = ln.on ? (HHMM_NEG_LOG_SQRT_TWO_PI - ln.lsig) + (-0.5 * (z * z)) : 0.0;
-            lsc += grp_sum<G>(tk);
-            al = ln.on ? ln.pj : 0.0;
-        } else {
-            const double e = lk_emit<MODEL, G, KM>(ln, x, xr, m);
-            al = ln.on ? ln.pj * e : 0.0;
-        }
-        al = grp_renorm<G>(al, ex);
-        if (t1 > 0) {
-            if (need_bwd) {
-                if (ln.on)
-                    ckpt(0) = al;
-            } else if ((out & HHMM_OUT_ALPHA) && a.alpha) {
-                lk_put<MODEL, G, KM>(a.alpha, a, ln, 0, al / grp_sum<G>(al));
-            }
-        }
-        tb = 1;
-    } else {
-        bnxt = bcur; /* the first step (t0 % G == 0) moves bnxt into bcur and fetches the next block */
+    if (t0 > 0) {
         al = (ln.on && t0 < t1) ? a.sc_st[sbase] : 0.0;
         lsc = t0 < t1 ? a.sc_sl[(int64_t)pq * a.scan_nc + cq] : 0.0;
     }
-    for (int t = tb; t < t1; ++t) {
+    for (int t = t0; t < t1; ++t) {
         const int u = t % G;
         if (u == 0) { /* group-uniform: next block of observations, prefetch the one after */
             bcur = bnxt;
@@ -460,11 +438,25 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         int x;
         double xr, m;
         lk_get<MODEL, G>(bcur, u, x, xr);
-        const double e = lk_emit<MODEL, G, KM>(ln, x, xr, m);
-        grp_exchange<G, KM>(ln.xch, slot, ln.j, al, w);
-        slot ^= 1;
-        lsc += m;
-        al = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex, t, ln.dense);
+        if (t == 0) {
+            if constexpr (LkTraits<MODEL>::kGauss) {
+                /* log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k): alpha_1 = p_1k */
+                const double z = (xr - ln.mu) * ln.isig;
+                const double tk = ln.on ? (HHMM_NEG_LOG_SQRT_TWO_PI - ln.lsig) + (-0.5 * (z * z)) : 0.0;
+                lsc += grp_sum<G>(tk);
+                al = ln.on ? ln.pj : 0.0;
+            } else {
+                const double e = lk_emit<MODEL, G, KM>(ln, x, xr, m);
+                al = ln.on ? ln.pj * e : 0.0;
+            }
+            al = grp_renorm<G>(al, ex);
+        } else {
+            const double e = lk_emit<MODEL, G, KM>(ln, x, xr, m);
+            grp_exchange<G, KM>(ln.xch, slot, ln.j, al, w);
+            slot ^= 1;
+            lsc += m;
+            al = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex, t, ln.dense);
+        }
         if (!need_bwd) {
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
                 lk_put<MODEL, G, KM>(a.alpha, a, ln, t, al / grp_sum<G>(al));
@@ -711,6 +703,339 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
             a.zstar[ln.p + a.P * (int64_t)t] = mine;
         q0 = q1;
         q1 = q2;
+    }
+}
+
+/* ---- FFBS at large K (the contract of DESIGN.md §5, oracle
+ * ffbs_contract): the filter f_t of the contract -- s_j = f(0) A(0,j), then
+ * fma(f(i), A(i,j), s_j) in state order, f_t(j) = s_j e_t(j), an exact
+ * power-of-two renormalisation (the frexp exponent of the max) every step --
+ * then z_{T-1} = cat(f_{T-1}), z_t = cat(f_t(i) A(i, z_{t+1})) with the
+ * caller's uniforms.  Lane j computes s_j with column j of A in registers
+ * and the state vector exchanged through LDS (the lk_fb layout), so the
+ * sums run in the contract's order and the draws are bit-exact.  Forward
+ * checkpoints every kLChunk steps; the backward sampling recomputes each
+ * chunk from its checkpoint (the same operations: the same bits). ---- */
+template <int KM>
+__device__ __forceinline__ int ffbs_cat_rt(const double (&w)[KM], int K, double u)
+{
+    double sum = w[0];
+#pragma unroll
+    for (int i = 1; i < KM; ++i)
+        if (i < K)
+            sum = sum + w[i];
+    const double us = u * sum;
+    int b = 0;
+    double cum = w[0];
+#pragma unroll
+    for (int i = 1; i < KM; ++i) {
+        const bool step = (i < K) & (b == i - 1) & (us > cum);
+        b = step ? i : b;
+        cum = step ? cum + w[i] : cum;
+    }
+    return ((sum > 0.0) & __builtin_isfinite(sum)) ? b : -1;
+}
+
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ double lkf_step(const LkLane<MODEL, G, KM> &ln, const double (&w)[KM], double e)
+{
+    double s = w[0] * ln.col[0];
+#pragma unroll
+    for (int i = 1; i < KM; ++i)
+        if (i < ln.K)
+            s = fma(w[i], ln.col[i], s);
+    return ln.on ? s * e : 0.0;
+}
+
+/* the contract's emission: phi[j, x] (discrete) or det_exp(lpdf_j - max_j lpdf_j) */
+template <int MODEL, int G, int KM>
+__device__ __forceinline__ double lkf_emit(const LkLane<MODEL, G, KM> &ln, int x, double xr)
+{
+    if constexpr (LkTraits<MODEL>::kGauss) {
+        const double lp = ln.on ? lk_lpdf<MODEL, G, KM>(ln, xr) : dev_ninf();
+        const double m = grp_max<G>(lp);
+        return ln.on ? hhmm_det_exp(lp - m) : 0.0;
+    } else {
+        const int xc = min(max(x, 1), ln.L);
+        return ln.on ? ln.tab[(xc - 1) * G + ln.j] : 0.0;
+    }
+}
+
+template <int MODEL, int G, int KM>
+__global__ void __launch_bounds__(kBlock) lk_ffbs_kernel(const DevArgs a)
+{
+    HIP_DYNAMIC_SHARED(double, lds)
+    LkLane<MODEL, G, KM> ln;
+    lk_setup<MODEL, G, KM>(ln, a, lds, false, lk_group<G>(a.P));
+    const int Tp = ln.Tp, K = ln.K;
+    double w[KM];
+    int slot = 0;
+    auto ckpt = [&](int c) -> double & { return a.ckpt[ln.p + a.P * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
+    auto renorm1 = [&](double v) {
+        const double mx = grp_max<G>(v);
+        return ldexp(v, -__builtin_amdgcn_frexp_exp(mx));
+    };
+    /* ---- forward filter ---- */
+    LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, 0), bnxt = lk_block<MODEL, G, KM>(ln, a, 1);
+    double f;
+    {
+        int x;
+        double xr;
+        lk_get<MODEL, G>(bcur, 0, x, xr);
+        const double e = lkf_emit<MODEL, G, KM>(ln, x, xr);
+        f = !ln.on ? 0.0 : (LkTraits<MODEL>::kGauss ? ln.pj : ln.pj * e); /* hmm.stan: p_1k (Q2) */
+        f = renorm1(f);
+    }
+    if (ln.on)
+        ckpt(0) = f;
+    for (int t = 1; t < Tp; ++t) {
+        const int u = t % G;
+        if (u == 0) {
+            bcur = bnxt;
+            bnxt = lk_block<MODEL, G, KM>(ln, a, t / G + 1);
+        }
+        int x;
+        double xr;
+        lk_get<MODEL, G>(bcur, u, x, xr);
+        const double e = lkf_emit<MODEL, G, KM>(ln, x, xr);
+        grp_exchange<G, KM>(ln.xch, slot, ln.j, f, w);
+        slot ^= 1;
+        f = renorm1(lkf_step<MODEL, G, KM>(ln, w, e));
+        if (t % kLChunk == 0 && ln.on)
+            ckpt(t / kLChunk) = f;
+    }
+    /* ---- backward sampling, chunk by chunk from the end ---- */
+    const int nck = (Tp + kLChunk - 1) / kLChunk;
+    constexpr int CPB = G / kLChunk;
+    int cb = (nck - 1) / CPB;
+    LkObs<MODEL, G> ob = lk_block<MODEL, G, KM>(ln, a, cb), obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
+    int z = -2; /* -2: not drawn yet (z_{T-1} comes from f_{T-1} alone) */
+    for (int c = nck - 1; c >= 0; --c) {
+        if (c / CPB != cb) {
+            cb = c / CPB;
+            ob = obp;
+            obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
+        }
+        const int t0 = c * kLChunk, ub = t0 % G;
+        double fb[kLChunk];
+        fb[0] = ln.on ? ckpt(c) : 0.0;
+#pragma unroll
+        for (int u = 1; u < kLChunk; ++u) {
+            fb[u] = 0.0;
+            if (t0 + u < Tp) {
+                int x;
+                double xr;
+                lk_get_var<MODEL, G>(ob, ub + u, x, xr);
+                const double e = lkf_emit<MODEL, G, KM>(ln, x, xr);
+                grp_exchange<G, KM>(ln.xch, slot, ln.j, fb[u - 1], w);
+                slot ^= 1;
+                fb[u] = renorm1(lkf_step<MODEL, G, KM>(ln, w, e));
+            }
+        }
+#pragma unroll
+        for (int u = kLChunk - 1; u >= 0; --u) {
+            const int t = t0 + u;
+            if (t >= Tp)
+                continue;
+            double wt = fb[u];
+            if (z >= 0) { /* weight f_t(i) A(i, z_{t+1}): lane i's row, entry z */
+                double az = ln.row[0];
+#pragma unroll
+                for (int k = 1; k < KM; ++k)
+                    az = (z == k) ? ln.row[k] : az;
+                wt = ln.on ? wt * az : 0.0;
+            }
+            grp_exchange<G, KM>(ln.xch, slot, ln.j, wt, w);
+            slot ^= 1;
+            const double uu = a.ffbs_u[ln.p + a.P * (int64_t)t];
+            z = (z == -1) ? -1 : ffbs_cat_rt<KM>(w, K, uu);
+            if (ln.j == 0)
+                a.z_ffbs[ln.p + a.P * (int64_t)t] = z + 1;
+        }
+    }
+}
+
+/* ---- The log-scale profile at large K (unalpha_tk / unbeta_tk requested):
+ * the reference's log-space recursion, as fb_log_kernel does at K <= 8 --
+ * log A and log phi once per pair, Stan's log_sum_exp per (t, j) over the
+ * accumulator (unalpha(t-1, i) + log A(i, j)) + emission (hmm.stan:37,
+ * hmm-multinom.stan:39) and (unbeta(t, i) + log A(j, i)) + emission(i)
+ * (hmm.stan:79), so a state thousands of nats below the others keeps a
+ * finite log value where the linear filter underflows.  Lane j runs state j
+ * (K exp and one log per lane-step); unalpha checkpoints every kLChunk steps,
+ * recomputed chunk by chunk in the backward sweep; posteriors by the
+ * reference's formulas (alpha = softmax(unalpha), beta = softmax(unbeta),
+ * ungamma = alpha .* beta, gamma = ungamma / sum: hmm.stan:60-63, 85-96). ---- */
+template <int KM>
+__device__ __forceinline__ double lk_lse(const double (&acc)[KM], int K)
+{
+    double mx = dev_ninf();
+#pragma unroll
+    for (int i = 0; i < KM; ++i)
+        if (i < K && acc[i] > mx)
+            mx = acc[i];
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < KM; ++i)
+        if (i < K && acc[i] != dev_ninf())
+            sum += exp(acc[i] - mx);
+    return mx + log(sum);
+}
+
+template <int G>
+__device__ __forceinline__ double grp_softmax(double v, bool on)
+{
+    const double m = grp_max<G>(on ? v : dev_ninf());
+    const double e = on ? exp(v - m) : 0.0;
+    return e / grp_sum<G>(e);
+}
+
+template <int MODEL, int G, int KM>
+__global__ void __launch_bounds__(kBlock) lk_log_kernel(const DevArgs a)
+{
+    HIP_DYNAMIC_SHARED(double, lds)
+    LkLane<MODEL, G, KM> ln;
+    lk_setup<MODEL, G, KM>(ln, a, lds, true, lk_group<G>(a.P)); /* col: log A(i, j); tab: log phi */
+    double lrow[KM];                                             /* log A(j, i) */
+#pragma unroll
+    for (int i = 0; i < KM; ++i)
+        lrow[i] = (i < ln.K) ? log(ln.row[i]) : 0.0;
+    const uint32_t out = a.outputs;
+    const int Tp = ln.Tp, K = ln.K;
+    const bool need_bwd = (out & (HHMM_OUT_UNBETA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
+    double w[KM];
+    int slot = 0;
+    auto ckpt = [&](int c) -> double & { return a.ckpt[ln.p + a.P * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
+    auto le_of = [&](int x, double xr) -> double { /* log emission of state j */
+        if constexpr (LkTraits<MODEL>::kGauss)
+            return ln.on ? lk_lpdf<MODEL, G, KM>(ln, xr) : 0.0;
+        else
+            return ln.on ? ln.tab[(min(max(x, 1), ln.L) - 1) * G + ln.j] : 0.0;
+    };
+    auto fwd = [&](double uprev, double le) { /* unalpha_t(j) */
+        grp_exchange<G, KM>(ln.xch, slot, ln.j, uprev, w);
+        slot ^= 1;
+        double acc[KM];
+#pragma unroll
+        for (int i = 0; i < KM; ++i)
+            acc[i] = (w[i] + ln.col[i]) + le;
+        return ln.on ? lk_lse<KM>(acc, K) : dev_ninf();
+    };
+    auto emit_fwd = [&](int t, double u) {
+        if ((out & HHMM_OUT_UNALPHA) && a.unalpha)
+            lk_put<MODEL, G, KM>(a.unalpha, a, ln, t, u);
+        if ((out & HHMM_OUT_ALPHA) && a.alpha)
+            lk_put<MODEL, G, KM>(a.alpha, a, ln, t, grp_softmax<G>(u, ln.on));
+    };
+
+    LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, 0), bnxt = lk_block<MODEL, G, KM>(ln, a, 1);
+    double u;
+    {
+        int x;
+        double xr;
+        lk_get<MODEL, G>(bcur, 0, x, xr);
+        if constexpr (LkTraits<MODEL>::kGauss) {
+            /* log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k) (hmm.stan:30, Q2) */
+            const double tk = ln.on ? lk_lpdf<MODEL, G, KM>(ln, xr) : 0.0;
+            const double s = grp_sum<G>(tk); /* every lane takes part in the butterfly */
+            u = ln.on ? log(ln.pj) + s : dev_ninf();
+        } else {
+            u = ln.on ? log(ln.pj) + le_of(x, xr) : dev_ninf();
+        }
+    }
+    if (need_bwd) {
+        if (ln.on)
+            ckpt(0) = u;
+    } else {
+        emit_fwd(0, u);
+    }
+    for (int t = 1; t < Tp; ++t) {
+        const int uu = t % G;
+        if (uu == 0) {
+            bcur = bnxt;
+            bnxt = lk_block<MODEL, G, KM>(ln, a, t / G + 1);
+        }
+        int x;
+        double xr;
+        lk_get<MODEL, G>(bcur, uu, x, xr);
+        u = fwd(u, le_of(x, xr));
+        if (!need_bwd)
+            emit_fwd(t, u);
+        else if (t % kLChunk == 0 && ln.on)
+            ckpt(t / kLChunk) = u;
+    }
+    {
+        /* target += log_sum_exp(unalpha_tk[T]) (hmm.stan:46): every lane holds the group's vector */
+        grp_exchange<G, KM>(ln.xch, slot, ln.j, u, w);
+        slot ^= 1;
+        const double ll = lk_lse<KM>(w, K);
+        if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0)
+            a.loglik[ln.p] = ll;
+    }
+    if (!need_bwd)
+        return;
+
+    /* ---- backward: unbeta_tk[T] = 1 (Q1), chunks from the end ---- */
+    double ub = ln.on ? 1.0 : dev_ninf();
+    const int nck = (Tp + kLChunk - 1) / kLChunk;
+    constexpr int CPB = G / kLChunk;
+    int cb = (nck - 1) / CPB;
+    LkObs<MODEL, G> ob = lk_block<MODEL, G, KM>(ln, a, cb), obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
+    for (int c = nck - 1; c >= 0; --c) {
+        if (c / CPB != cb) {
+            cb = c / CPB;
+            ob = obp;
+            obp = lk_block<MODEL, G, KM>(ln, a, cb - 1);
+        }
+        const int t0 = c * kLChunk, ub0 = t0 % G;
+        double les[kLChunk], ubuf[kLChunk];
+#pragma unroll
+        for (int v = 0; v < kLChunk; ++v) {
+            int x;
+            double xr;
+            lk_get_var<MODEL, G>(ob, ub0 + v, x, xr);
+            les[v] = le_of(x, xr);
+        }
+        ubuf[0] = ln.on ? ckpt(c) : dev_ninf();
+#pragma unroll
+        for (int v = 1; v < kLChunk; ++v) {
+            ubuf[v] = dev_ninf();
+            if (t0 + v < Tp)
+                ubuf[v] = fwd(ubuf[v - 1], les[v]);
+        }
+#pragma unroll
+        for (int v = kLChunk - 1; v >= 0; --v) {
+            const int t = t0 + v;
+            if (t >= Tp)
+                continue;
+            emit_fwd(t, ubuf[v]);
+            if ((out & HHMM_OUT_UNBETA) && a.unbeta)
+                lk_put<MODEL, G, KM>(a.unbeta, a, ln, t, ub);
+            const double be = grp_softmax<G>(ub, ln.on);
+            if ((out & HHMM_OUT_BETA) && a.beta)
+                lk_put<MODEL, G, KM>(a.beta, a, ln, t, be);
+            if (out & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
+                const double ug = grp_softmax<G>(ubuf[v], ln.on) * be;
+                if ((out & HHMM_OUT_UNGAMMA) && a.ungamma)
+                    lk_put<MODEL, G, KM>(a.ungamma, a, ln, t, ug);
+                if ((out & HHMM_OUT_GAMMA) && a.gamma)
+                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug / grp_sum<G>(ug));
+            }
+            if (t > 0) {
+                /* unbeta_{t-1}(j) = LSE_i((unbeta_t(i) + log A(j, i)) + le_t(i)): lane i's
+                 * unbeta and emission travel together */
+                double wl[KM];
+                grp_exchange<G, KM>(ln.xch, slot, ln.j, ub, w);
+                slot ^= 1;
+                grp_exchange<G, KM>(ln.xch, slot, ln.j, les[v], wl);
+                slot ^= 1;
+                double acc[KM];
+#pragma unroll
+                for (int i = 0; i < KM; ++i)
+                    acc[i] = (w[i] + lrow[i]) + wl[i];
+                ub = ln.on ? lk_lse<KM>(acc, K) : dev_ninf();
+            }
+        }
     }
 }
 

@@ -345,13 +345,15 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
     const uint32_t out = a.outputs;
     const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
     const uint32_t vit = HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
+    const uint32_t ffbs = HHMM_OUT_FFBS;
     if (a.scan_cl > 0 && (!discrete || a.L * 16 * ((KM + 15) / 16) * 4 * sizeof(double) > 64 * 1024)) {
         set_error("K = %d: the parallel scan over T runs hmm-multinom with L <= %d", a.K, 64 * 1024 / (4 * 8 * 16 * ((KM + 15) / 16)));
         return HHMM_ERR_UNSUPPORTED;
     }
-    if (out & ~(fb | vit)) {
-        set_error("K = %d > %d: this build evaluates loglik, alpha, beta, ungamma, gamma, zstar and logp_zstar "
-                  "(no log-scale unalpha / unbeta, no FFBS)", a.K, kMaxK);
+    const uint32_t logs = HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA;
+    if (out & ~(fb | vit | ffbs | logs)) {
+        set_error("K = %d > %d: the large-K path evaluates loglik, unalpha, alpha, unbeta, beta, ungamma, gamma, "
+                  "zstar, logp_zstar and z_ffbs", a.K, kMaxK);
         return HHMM_ERR_UNSUPPORTED;
     }
     int threads = kBlock;
@@ -376,7 +378,21 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
     if (out & vit)
         hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), vs, a);
     hipError_t e = hipGetLastError();
-    if ((out & fb) && a.scan_cl > 0 && e == hipSuccess) {
+    if ((out & ffbs) && e == hipSuccess) {
+        /* the FFBS contract's filter and draws (sequential per pair); its
+         * checkpoints share the workspace with lk_fb_kernel's, so it runs
+         * first on the caller's stream */
+        DevArgs f = a;
+        f.outputs = HHMM_OUT_FFBS;
+        hipLaunchKernelGGL((lk_ffbs_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, f);
+        e = hipGetLastError();
+    }
+    if ((out & logs) && e == hipSuccess) {
+        /* the log-scale profile: every posterior output of the request from the
+         * reference's log-space recursion (as fb_log_kernel at K <= 8) */
+        hipLaunchKernelGGL((lk_log_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
+        e = hipGetLastError();
+    } else if ((out & fb) && a.scan_cl > 0 && e == hipSuccess) {
         /* parallel scan over T (hhmm_lkscan.h): MFMA chunk products, the scan
          * over chunks, then the chunks' sweeps as groups (pair, chunk) */
         constexpr int RT = (KM + 15) / 16, KSM = KM / 4;

@@ -200,7 +200,8 @@ def test_c5_few_pairs(engine, oracle, c5_data):
     ref = oracle.gqs("hhmm-tayal2009", data, d4, pars=HOT + ["unalpha_tk", "unbeta_tk"], return_status=True,
                      nthreads=threads())
     compare_all(got, ref, ["loglik", "zstar_t", "logp_zstar", "pair_status"])
-    compare_tayal_gamma(got, ref, max_forgiven=1000)
+    # 500 of 4e6 rows on this data (round 3, profiles/r03a); the bound keeps a 25 % margin
+    compare_tayal_gamma(got, ref, max_forgiven=625)
 
 
 def test_c5_full_shape(engine, oracle, c5_data):
@@ -226,4 +227,5 @@ def test_c5_full_shape(engine, oracle, c5_data):
     ref = oracle.gqs("hhmm-tayal2009", data, dsub, pars=HOT + ["unalpha_tk", "unbeta_tk"], nthreads=3)
     got = {k: r.host_pairs(k, idx) for k in HOT}
     compare_all(got, ref, ["loglik", "zstar_t", "logp_zstar"])
-    compare_tayal_gamma(got, ref, max_forgiven=1000)
+    # 392 of 3e6 rows on this data (round 3, profiles/r03a); the bound keeps a 25 % margin
+    compare_tayal_gamma(got, ref, max_forgiven=490)

@@ -95,7 +95,72 @@ def test_gamma_only_large_K_disjoint_filters(engine, oracle):
 
 
 def test_large_K_unsupported_outputs(engine):
+    """The IOHMM programs stop at K = 8 on the device (unsupported, with a message)."""
     import hhmm_amd
-    data, draws = synth.hmm_multinom(N=1, S=2, T=10, K=12, L=9)
+    data, draws = synth.iohmm_reg(N=1, S=2, T=10, K=12, M=4)
     with pytest.raises(api.HHMMError):
-        hhmm_amd.gqs("hmm-multinom", data, draws, pars=["unalpha_tk"], lib=engine)
+        hhmm_amd.gqs("iohmm-reg", data, draws, pars=["loglik"], lib=engine)
+
+
+LOGPARS = ["loglik", "unalpha_tk", "alpha_tk", "unbeta_tk", "beta_tk", "ungamma_tk", "gamma_tk"]
+
+
+@pytest.mark.parametrize("model", ["hmm-multinom", "hmm"])
+@pytest.mark.parametrize("K", [9, 16, 23, 32])
+@pytest.mark.parametrize("T", [1, 2, 37, 300])
+def test_log_profile_large_K(engine, oracle, model, K, T):
+    """unalpha_tk / unbeta_tk at large K (lk_log_kernel): the reference's
+    log-space recursion with every posterior of the request."""
+    gen = synth.hmm_multinom if model == "hmm-multinom" else synth.hmm_gauss
+    kw = dict(L=9) if model == "hmm-multinom" else {}
+    data, draws = gen(N=2, S=5, T=T, K=K, **kw)
+    run_both(engine, oracle, model, data, draws, pars=LOGPARS + ["zstar_t", "logp_zstar"])
+
+
+def test_log_profile_large_K_far_states(engine, oracle):
+    """A state thousands of nats below the others: its linear-space filter
+    underflows, the log-space unalpha / unbeta stay finite as in Stan."""
+    K = 12
+    data, draws = synth.hmm_multinom(N=1, S=3, T=800, K=K, L=9)
+    phi = np.array(draws["phi_k"], dtype=np.float64)
+    phi[:, 0, :] = 1e-6
+    phi[:, 0, 0] = 1.0
+    phi /= phi.sum(axis=2, keepdims=True)
+    draws["phi_k"] = phi
+    data["x"] = np.where(np.asarray(data["x"]) == 1, 2, np.asarray(data["x"]))
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=LOGPARS)
+
+
+def test_log_profile_forward_only_large_K(engine, oracle):
+    data, draws = synth.hmm_multinom(N=2, S=4, T=100, K=20, L=9)
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "unalpha_tk", "alpha_tk"])
+
+
+@pytest.mark.parametrize("model", ["hmm-multinom", "hmm"])
+@pytest.mark.parametrize("K", [9, 16, 23, 32])
+@pytest.mark.parametrize("T", [1, 2, 37, 300])
+def test_ffbs_large_K(engine, oracle, model, K, T):
+    """FFBS at large K (lk_ffbs_kernel): the contract's filter (state-order fma
+    sums, per-step power-of-two renormalisation) and draws, bit-exact against
+    the oracle's ffbs_contract given the same uniforms."""
+    import hhmm_amd
+    gen = synth.hmm_multinom if model == "hmm-multinom" else synth.hmm_gauss
+    kw = dict(L=9) if model == "hmm-multinom" else {}
+    data, draws = gen(N=2, S=7, T=T, K=K, **kw)
+    P = 14
+    u = synth.ffbs_uniforms(P, T)
+    pars = ["loglik", "gamma_tk", "z_ffbs"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, uniforms=u, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, uniforms=u, return_status=True, nthreads=8)
+    compare_all(got, ref, pars)
+
+
+def test_ffbs_large_K_ragged_with_viterbi(engine, oracle):
+    import hhmm_amd
+    data, draws = synth.hmm_multinom(N=3, S=5, T=500, K=23, L=9)
+    data["T"] = np.array([500, 3, 257], dtype=np.int32)
+    u = synth.ffbs_uniforms(15, 500)
+    pars = ["loglik", "gamma_tk", "z_ffbs", "zstar_t", "logp_zstar"]
+    got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, uniforms=u, return_status=True)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, uniforms=u, return_status=True, nthreads=8)
+    compare_all(got, ref, pars + ["pair_status"])
