@@ -615,10 +615,15 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
         else
             return ln.on ? ln.tab[(min(max(x, 1), ln.L) - 1) * G + ln.j] : 0.0;
     };
-    /* back-pointers [P][K][Tb] bytes, Tb = T_max rounded up to 16: a state's
-     * bytes are contiguous in t and its row 16-byte aligned */
-    const int Tb = lk_row_bytes(a.Tmax);
-    uint8_t *bp = reinterpret_cast<uint8_t *>(a.bp) + ((int64_t)ln.p * K + (ln.on ? ln.j : 0)) * Tb;
+    /* back-pointers in blocks of kLBack steps: [P][Tb/16][K][16] bytes (Tb =
+     * T_max rounded up to 16).  A lane gathers its state's 16 bytes of a block
+     * in registers and stores them with one 16-byte store, so the group's
+     * store covers K * 16 contiguous bytes (a byte store per lane and step,
+     * into rows T_max apart, moved 20x the bytes: 48 GB per N1 step, PMC
+     * profiles/r03d_workloads_pmc.json) */
+    const int Tb = lk_row_bytes(a.Tmax), NB = Tb / kLBack;
+    uint8_t *bpb = reinterpret_cast<uint8_t *>(a.bp) + (int64_t)ln.p * NB * K * kLBack;
+    auto bp_at = [&](int blk) { return bpb + ((int64_t)blk * K + (ln.on ? ln.j : 0)) * kLBack; };
 
     /* delta_tk[1, K] = emission of state K only (Q3: the others keep NaN) */
     LkObs<MODEL, G> bcur = lk_block<MODEL, G, KM>(ln, a, 0), bnxt = lk_block<MODEL, G, KM>(ln, a, 1);
@@ -627,30 +632,41 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
     lk_get<MODEL, G>(bcur, 0, x, xr);
     const double le0 = emit_log(x, xr);
     double dl = !ln.on ? dev_ninf() : ((ln.j == K - 1) ? le0 : dev_nan());
-    for (int t = 1; t < Tp; ++t) {
-        const int u = t % G;
-        if (u == 0) {
-            bcur = bnxt;
-            bnxt = lk_block<MODEL, G, KM>(ln, a, t / G + 1);
-        }
-        lk_get<MODEL, G>(bcur, u, x, xr);
-        const double le = emit_log(x, xr);
-        grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
-        slot ^= 1;
-        /* candidate (delta + log A) + emission, strict '>' from -inf; the
-         * running max as fmax (vit_step): NaN never wins, first i on ties */
-        double best = dev_ninf();
-        int arg = 0;
+    const int nblk = (wave_max(Tp) + kLBack - 1) / kLBack; /* wave-uniform: the groups walk t together */
+    for (int b = 0; b < nblk; ++b) {
+        uint32_t wd[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int i = 0; i < KM; ++i) { /* idle i: delta -inf, never greater */
-            const double cand = (w[i] + ln.col[i]) + le;
-            const bool gt = cand > best;
-            best = fmax(best, cand);
-            arg = gt ? i : arg;
+        for (int v = 0; v < kLBack; ++v) {
+            const int t = b * kLBack + v;
+            if (t == 0)
+                continue;
+            const int u = t % G;
+            if (u == 0) {
+                bcur = bnxt;
+                bnxt = lk_block<MODEL, G, KM>(ln, a, t / G + 1);
+            }
+            if (t < Tp) { /* group-uniform */
+                lk_get<MODEL, G>(bcur, u, x, xr);
+                const double le = emit_log(x, xr);
+                grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
+                slot ^= 1;
+                /* candidate (delta + log A) + emission, strict '>' from -inf; the
+                 * running max as fmax (vit_step): NaN never wins, first i on ties */
+                double best = dev_ninf();
+                int arg = 0;
+#pragma unroll
+                for (int i = 0; i < KM; ++i) { /* idle i: delta -inf, never greater */
+                    const double cand = (w[i] + ln.col[i]) + le;
+                    const bool gt = cand > best;
+                    best = fmax(best, cand);
+                    arg = gt ? i : arg;
+                }
+                dl = ln.on ? best : dev_ninf();
+                wd[v >> 2] |= (uint32_t)arg << (8 * (v & 3));
+            }
         }
-        dl = ln.on ? best : dev_ninf();
-        if (ln.on)
-            bp[t] = (uint8_t)arg;
+        if (ln.on && b * kLBack < Tp)
+            *reinterpret_cast<uint4 *>(bp_at(b)) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     }
     /* logp_zstar = max(delta_T) (SSE2 order); zstar_T = LAST j attaining it */
     grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
@@ -678,10 +694,9 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
      * chunk (one 16-byte load, prefetched two chunks ahead), the path state
      * moves by one shuffle per step, lane u keeps step t0 + u for the store */
     const int nb = (Tp + kLBack - 1) / kLBack;
-    const int wmax = Tb / kLBack - 1; /* last 16-byte chunk of the row */
     auto load = [&](int c) -> uint4 {
-        const int cc = min(max(c, 0), wmax);
-        return *reinterpret_cast<const uint4 *>(bp + (int64_t)cc * kLBack);
+        const int cc = min(max(c, 0), NB - 1);
+        return *reinterpret_cast<const uint4 *>(bp_at(cc));
     };
     uint4 q0 = load(nb - 1), q1 = load(nb - 2);
     for (int c = nb - 1; c >= 0; --c) {

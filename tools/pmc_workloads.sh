@@ -13,7 +13,7 @@ cd /tmp && export TMPDIR=/tmp
 for W in "$@"; do
   D=$OUT/$W
   mkdir -p $D
-  ARGS="$R/bench.py --workload $W --no-cpu-baseline --no-check --steps 1 --warmup 1"
+  ARGS="$R/bench.py --workload $W --no-cpu-baseline --no-check --no-sequential --no-path-gather --steps 1 --warmup 1"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o trace -- python $ARGS > $D/trace.log 2>&1
   rc=$?; echo "$W trace rc=$rc" >> $OUT/passes.txt; [ $rc -eq 0 ] || exit 1
   i=0
