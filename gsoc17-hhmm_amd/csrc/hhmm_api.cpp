@@ -547,7 +547,7 @@ hhmm_status hhmm_workspace_size(const hhmm_request *req, size_t *bytes)
         return HHMM_ERR_INVALID_ARGUMENT;
     }
     *bytes = workspace_bytes(req->model, req->data.K, req->data.L, req->data.T_max, req->data.T_oos_max, P, req->outputs,
-                            (uint32_t)req->flags);
+                            (uint32_t)req->flags, req->data.n_series, req->pairing);
     return HHMM_OK;
 }
 
@@ -638,7 +638,7 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
     dres.pair_status = (int32_t *)dstatus;
 
     size_t wsb = workspace_bytes(req->model, req->data.K, req->data.L, req->data.T_max, req->data.T_oos_max, P, req->outputs,
-                                 (uint32_t)req->flags);
+                                 (uint32_t)req->flags, req->data.n_series, req->pairing);
     void *ws = pool_get(dev, wsb);
     if (!ws) {
         cleanup();

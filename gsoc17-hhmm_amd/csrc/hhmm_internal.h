@@ -78,6 +78,7 @@ struct DevArgs {
     uint32_t *vs_e;     /* [nc][P]      chunk backtrack map: byte s = entry state of exit state s */
     int32_t *vs_z;      /* [nc][P]      path state at each chunk's last step (-1: no path) */
     int32_t *vs_fail;   /* [P]          a replayed chunk disagreed: decode again sequentially */
+    int32_t *vs_tl;     /* [1 + P*nc]   chunks with a grid rounding tie: count, then p + P c */
     const int32_t *vs_redo; /* state-parallel decoder: only pairs with vs_redo[p] != 0 (null: all) */
 };
 
@@ -97,6 +98,10 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
 constexpr int kVsChunk = 512;
 int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t flags);
 
+/* Large K under GRID pairing (hhmm_lkscan.h lkm_fb_kernel): the k-steps of
+ * its state capacity when it runs the forward-backward, else 0. */
+int lkm_plan(int model, int K, int64_t N, int pairing, uint32_t outputs, uint32_t flags, int scan_cl);
+
 /* Time steps between forward checkpoints kept for the backward sweep. */
 constexpr int fb_chunk(int K) { return K <= 4 ? 8 : 4; }
 
@@ -110,7 +115,8 @@ constexpr int kBlock = 256;
 constexpr size_t kLdsLimit = 160 * 1024;
 
 /* Bytes of workspace the kernels need for this launch shape. */
-size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags);
+size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags,
+                       int64_t N, int pairing);
 
 /* Carves the workspace into DevArgs pointers. */
 void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags);

@@ -158,6 +158,17 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
     return sp;
 }
 
+int lkm_plan(int model, int K, int64_t N, int pairing, uint32_t outputs, uint32_t flags, int scan_cl)
+{
+    const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
+                        HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
+    if (model != HHMM_MODEL_HMM_MULTINOM || K <= kMaxK || K > kMaxKLarge || pairing != HHMM_PAIR_GRID || N < 16 ||
+        scan_cl > 0 || (flags & HHMM_FLAG_MFMA_OFF) || !(outputs & fb) ||
+        (outputs & fb & ~(HHMM_OUT_LOGLIK | HHMM_OUT_GAMMA)))
+        return 0;
+    return K <= 16 ? 4 : (K <= 24 ? 6 : 8);
+}
+
 int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t flags)
 {
     const bool family = model == HHMM_MODEL_HMM_GAUSS || model == HHMM_MODEL_HMM_MULTINOM ||
@@ -177,17 +188,18 @@ int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t
 /* Offsets of every workspace region (SIZE_MAX = unused) and the total. */
 struct WsLayout {
     size_t ckpt, ckpt_ls, xpk, rnw, bp, lam, mf, qb, mx, st, sl, be, bl, total;
-    size_t vm, vm1, vd, vk, ve, vz, vf;
+    size_t vm, vm1, vd, vk, ve, vz, vf, vt;
     int vnc;
     ScanPlan sp;
 };
 
-static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
+static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags,
+                          int64_t N, int pairing)
 {
     WsLayout w;
     const size_t NONE = SIZE_MAX;
     w.ckpt = w.ckpt_ls = w.xpk = w.rnw = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
-    w.vm = w.vm1 = w.vd = w.vk = w.ve = w.vz = w.vf = NONE;
+    w.vm = w.vm1 = w.vd = w.vk = w.ve = w.vz = w.vf = w.vt = NONE;
     w.vnc = 0;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -210,6 +222,10 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
             w.be = take(Q * K * d);
             if (needs_ckpt(model, outputs))
                 w.ckpt = take((size_t)((w.sp.cl + 7) / 8) * K * Q * d);
+        } else if (lkm_plan(model, K, N, pairing, outputs, flags, 0) && needs_ckpt(model, outputs)) {
+            /* lkm_fb_kernel: [wave][chunk][KSM][64] per (draw, 16-series tile) */
+            const size_t ksm = (size_t)lkm_plan(model, K, N, pairing, outputs, flags, 0);
+            w.ckpt = take((size_t)(P / N) * (size_t)((N + 15) / 16) * ((Tmax + 7) / 8) * ksm * 64 * d);
         } else if (needs_ckpt(model, outputs)) {
             w.ckpt = take((size_t)((Tmax + 7) / 8) * K * P * d);
         }
@@ -257,6 +273,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
             w.ve = take(nc * P * sizeof(uint32_t));
             w.vz = take(nc * P * sizeof(int32_t));
             w.vf = take(P * sizeof(int32_t));
+            w.vt = take((1 + nc * P) * sizeof(int32_t));
         }
     }
     if (is_iohmm_model(model) && (outputs & HHMM_OUT_UNBETA))
@@ -265,15 +282,16 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     return w;
 }
 
-size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags)
+size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, uint32_t outputs, uint32_t flags,
+                       int64_t N, int pairing)
 {
-    return ws_layout(model, K, L, Tmax, Toos, P, outputs, flags).total;
+    return ws_layout(model, K, L, Tmax, Toos, P, outputs, flags, N, pairing).total;
 }
 
 void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
 {
     char *b = (char *)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
-    const WsLayout w = ws_layout(a.model, a.K, a.L, Tmax, Toos, a.P, a.outputs, flags);
+    const WsLayout w = ws_layout(a.model, a.K, a.L, Tmax, Toos, a.P, a.outputs, flags, a.N, a.pairing);
     auto at_off = [&](size_t o) -> void * { return o == SIZE_MAX ? nullptr : (void *)(b + o); };
     a.ckpt = (double *)at_off(w.ckpt);
     a.ckpt_ls = (double *)at_off(w.ckpt_ls);
@@ -298,6 +316,7 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
     a.vs_e = (uint32_t *)at_off(w.ve);
     a.vs_z = (int32_t *)at_off(w.vz);
     a.vs_fail = (int32_t *)at_off(w.vf);
+    a.vs_tl = (int32_t *)at_off(w.vt);
 }
 
 DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)

@@ -330,6 +330,299 @@ __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
     }
 }
 
+/* ---- Many series under one draw (GRID pairing, N >= 16; SURVEY §8 N1 at large
+ * K): the forward-backward itself on the matrix cores.  The series evaluated
+ * under draw s share its A, so the forward step of 16 of them is the dense
+ * product A^T [alpha_1 ... alpha_16] -- one column per series, the same
+ * operand layout and register reuse as lks_prod_kernel -- and the backward
+ * step is A [e_t .* beta_1 ... e_t .* beta_16].  One wave = (draw s, tile of
+ * 16 series), draw-fastest over the grid, so the waves writing the same
+ * gamma lines (p = s + S n: consecutive draws) run side by side.
+ *   forward   alpha_t column-renormalised by exact powers of two (exponents
+ *             summed per column: the log-likelihood), a checkpoint of the
+ *             tile every kLmChunk steps (coalesced: register kk of lane l)
+ *   backward  chunk by chunk from the end: the chunk's alphas recomputed from
+ *             its checkpoint into registers, then gamma_t = alpha .* beta / sum
+ *             (the reference's normalised-vector formula where that sum is
+ *             below 2^-960, as lk_fb_kernel) and the beta step.
+ * Outputs: loglik, gamma_tk (the hot profile); ragged T per series. ---- */
+constexpr int kLmChunk = 8;
+
+template <int RT, int KSM>
+__global__ void __launch_bounds__(256) lkm_fb_kernel(const DevArgs a)
+{
+    constexpr int KR = 16 * RT;
+    constexpr int C = kLmChunk;
+    HIP_DYNAMIC_SHARED(double, lds)
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int K = a.K;
+    const int ks = (K + 3) / 4;
+    const int64_t NT = (a.N + 15) / 16; /* series tiles */
+    const int64_t nw = a.S * NT;
+    const int64_t w = min((int64_t)blockIdx.x * (blockDim.x >> 6) + wv, nw - 1);
+    const int64_t d = w % a.S;        /* the draw */
+    const int64_t tile = w / a.S;
+    const int64_t n = min(tile * 16 + (lane & 15), a.N - 1);
+    const bool col_ok = tile * 16 + (lane & 15) < a.N;
+    const int64_t p = d + a.S * n;    /* GRID pair */
+    const int Tn = pair_len(a, n);
+    const int64_t S = a.S;
+
+    double *tab = lds + (size_t)wv * a.L * KR; /* phi[l][j], rows j >= K zero */
+    for (int idx = lane; idx < a.L * KR; idx += 64) {
+        const int l = idx / KR, j = idx - l * KR;
+        tab[idx] = j < K ? a.phi_k[d + S * ((int64_t)j + (int64_t)K * l)] : 0.0;
+    }
+    /* A operands: forward A^T[j][i] = A(i, j); backward A[j][i] = A(j, i)
+     * (row j = 16rt + (lane & 15), k = i = 4kk + (lane >> 4)) */
+    double af[RT][KSM], ab[RT][KSM];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk) {
+            const int i = 4 * kk + (lane >> 4), j = 16 * rt + (lane & 15);
+            const bool in = i < K && j < K;
+            af[rt][kk] = in ? a.A_ij[d + S * ((int64_t)i + (int64_t)K * j)] : 0.0;
+            ab[rt][kk] = in ? a.A_ij[d + S * ((int64_t)j + (int64_t)K * i)] : 0.0;
+        }
+    double pj[KSM];
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk) {
+        const int j = 4 * kk + (lane >> 4);
+        pj[kk] = j < K ? a.p_1k[d + S * j] : 0.0;
+    }
+    __syncthreads();
+
+    const int Tw = wave_max(col_ok ? Tn : 1);
+    auto xat = [&](int t) -> int { return a.x[n + a.N * (int64_t)min(max(t, 0), a.Tmax - 1)]; };
+    /* emission rows j = 4kk + (lane >> 4) of this lane's column at symbol x */
+    auto emis = [&](int x, double (&e)[KSM]) {
+        const double *row = tab + (min(max(x, 1), a.L) - 1) * KR + (lane >> 4);
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            e[kk] = row[4 * kk];
+    };
+    /* column reductions over the tile's 4 lane rows (lanes l ^ 16, l ^ 32) */
+    auto colmax = [&](double v) {
+        v = fmax(v, __shfl_xor(v, 16));
+        return fmax(v, __shfl_xor(v, 32));
+    };
+    auto colsum = [&](double v) {
+        v += __shfl_xor(v, 16);
+        return v + __shfl_xor(v, 32);
+    };
+    auto renorm = [&](double (&q)[KSM], int &ex) {
+        double mx = q[0];
+#pragma unroll
+        for (int kk = 1; kk < KSM; ++kk)
+            mx = fmax(mx, q[kk]);
+        const int e2 = __builtin_amdgcn_frexp_exp(colmax(mx));
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            q[kk] = ldexp(q[kk], -e2);
+        ex += e2;
+    };
+    auto mm = [&](const double (&A)[RT][KSM], const double (&q)[KSM], double (&out)[KSM]) {
+        lks_d4 acc[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+            acc[rt] = lks_d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            if (kk < ks) {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+                    acc[rt] = lks_mfma(A[rt][kk], q[kk], acc[rt]);
+            }
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            out[kk] = acc[kk >> 2][kk & 3];
+    };
+    /* checkpoints: [wave][chunk][kk][64 lanes] */
+    const int nck = (Tw + C - 1) / C;
+    double *ck = a.ckpt + (size_t)w * (size_t)((a.Tmax + C - 1) / C) * KSM * 64;
+    auto ck_at = [&](int c, int kk) -> double & { return ck[((size_t)c * KSM + kk) * 64 + lane]; };
+
+    /* ---- forward ---- */
+    double q[KSM], e[KSM];
+    int ex = 0;
+    emis(xat(0), e);
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk)
+        q[kk] = pj[kk] * e[kk]; /* hmm-multinom.stan:31 */
+    renorm(q, ex);
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk)
+        ck_at(0, kk) = q[kk];
+    /* observations a block of kXb steps ahead (one load per step and lane,
+     * issued a block before use: a one-step prefetch waited an HBM round trip
+     * per step) */
+    constexpr int kXb = 16;
+    int xb[kXb], xnb[kXb];
+#pragma unroll
+    for (int v = 0; v < kXb; ++v)
+        xb[v] = xat(v);
+    for (int t = 1; t < Tw; ++t) {
+        if (t % kXb == 0) { /* wave-uniform */
+#pragma unroll
+            for (int v = 0; v < kXb; ++v)
+                xb[v] = xnb[v];
+        }
+        if (t % kXb == 1 || t == 1) {
+#pragma unroll
+            for (int v = 0; v < kXb; ++v)
+                xnb[v] = xat((t / kXb + 1) * kXb + v);
+        }
+        int x = xb[0];
+#pragma unroll
+        for (int v = 1; v < kXb; ++v)
+            x = (t % kXb == v) ? xb[v] : x;
+        double dq[KSM];
+        mm(af, q, dq);
+        emis(x, e);
+        const bool on = t < Tn;
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            dq[kk] *= e[kk];
+        int e2 = 0;
+        renorm(dq, e2);
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            q[kk] = on ? dq[kk] : q[kk];
+        ex += on ? e2 : 0;
+        if (t % C == 0) {
+#pragma unroll
+            for (int kk = 0; kk < KSM; ++kk)
+                ck_at(t / C, kk) = q[kk];
+        }
+    }
+    {
+        double sq = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            sq += q[kk];
+        sq = colsum(sq);
+        if ((lane >> 4) == 0 && col_ok && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+            a.loglik[p] = log(sq) + kLn2 * ex;
+    }
+    if (!((a.outputs & HHMM_OUT_GAMMA) && a.gamma))
+        return;
+
+    /* ---- backward: beta_T = 1 (unbeta_tk[T] = 1, Q1) ---- */
+    double be[KSM];
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk)
+        be[kk] = (4 * kk + (lane >> 4) < K) ? 1.0 : 0.0;
+    int xs[C], xsn[C];
+    double ckn[KSM];
+#pragma unroll
+    for (int u = 0; u < C; ++u)
+        xsn[u] = xat((nck - 1) * C + u);
+#pragma unroll
+    for (int kk = 0; kk < KSM; ++kk)
+        ckn[kk] = ck_at(nck - 1, kk);
+    for (int c = nck - 1; c >= 0; --c) {
+        const int t0 = c * C;
+        double al[C][KSM];
+#pragma unroll
+        for (int u = 0; u < C; ++u)
+            xs[u] = xsn[u];
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            al[0][kk] = ckn[kk];
+        /* the next chunk's observations and checkpoint, a chunk ahead */
+#pragma unroll
+        for (int u = 0; u < C; ++u)
+            xsn[u] = xat((c - 1) * C + u);
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk)
+            ckn[kk] = ck_at(max(c - 1, 0), kk);
+#pragma unroll
+        for (int u = 1; u < C; ++u) {
+            double dq[KSM];
+            mm(af, al[u - 1], dq);
+            emis(xs[u], e);
+#pragma unroll
+            for (int kk = 0; kk < KSM; ++kk)
+                dq[kk] *= e[kk];
+            int e2 = 0;
+            renorm(dq, e2);
+#pragma unroll
+            for (int kk = 0; kk < KSM; ++kk)
+                al[u][kk] = dq[kk];
+        }
+#pragma unroll
+        for (int u = C - 1; u >= 0; --u) {
+            const int t = t0 + u;
+            if (t >= Tw) /* wave-uniform */
+                continue;
+            const bool on = t < Tn;
+            /* gamma_t = alpha .* beta / sum, the normalised-vector form below 2^-960 */
+            double ug[KSM], sg = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < KSM; ++kk) {
+                ug[kk] = al[u][kk] * be[kk];
+                sg += ug[kk];
+            }
+            sg = colsum(sg);
+            const bool small = !(sg > 0x1p-960);
+            double rg = 1.0 / sg;
+            if (__builtin_amdgcn_readfirstlane((int)(__ballot(small) != 0))) { /* rare, wave-uniform */
+                double sa = 0.0, sb = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < KSM; ++kk) {
+                    sa += al[u][kk];
+                    sb += be[kk];
+                }
+                sa = colsum(sa);
+                sb = colsum(sb);
+                double ssum = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < KSM; ++kk) {
+                    ug[kk] = small ? (al[u][kk] / sa) * (be[kk] / sb) : ug[kk];
+                    ssum += ug[kk];
+                }
+                ssum = colsum(ssum);
+                rg = small ? 1.0 / ssum : rg;
+            }
+            if (on && col_ok) {
+#pragma unroll
+                for (int kk = 0; kk < KSM; ++kk) {
+                    const int j = 4 * kk + (lane >> 4);
+                    if (j < K)
+                        __builtin_nontemporal_store(ug[kk] * rg, a.gamma + p + a.P * ((int64_t)t + (int64_t)a.Tout * j));
+                }
+            }
+            if (t > 0) { /* wave-uniform: the matrix product and the column
+                          * reductions run on every lane; columns past their
+                          * series' end keep beta_T */
+                /* beta_{t-1} = A (e_t .* beta_t) */
+                emis(xs[u], e);
+                double v[KSM], nb[KSM];
+#pragma unroll
+                for (int kk = 0; kk < KSM; ++kk)
+                    v[kk] = e[kk] * be[kk];
+                mm(ab, v, nb);
+                int e2 = 0;
+                renorm(nb, e2);
+#pragma unroll
+                for (int kk = 0; kk < KSM; ++kk)
+                    be[kk] = on ? nb[kk] : be[kk];
+            }
+        }
+    }
+}
+
+/* lkm_fb_kernel's domain: hmm-multinom under GRID pairing with at least 16
+ * series per draw, the hot output profile (loglik + gamma_tk), sequential in
+ * T (no scan), not switched off (HHMM_FLAG_MFMA_OFF); hhmm_kernels.hip sizes
+ * its checkpoints by the same rule (lkm_plan). */
+static inline bool lkm_ok(const DevArgs &a)
+{
+    return lkm_plan(a.model, a.K, a.N, a.pairing, a.outputs, a.flags, a.scan_cl) != 0;
+}
+
 /* LDS bytes of a launch with `threads` lanes: exchange slots + tables. */
 template <int G>
 static inline size_t lk_lds(const DevArgs &a, int threads, bool discrete)
@@ -387,6 +680,7 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         hipLaunchKernelGGL((lk_ffbs_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, f);
         e = hipGetLastError();
     }
+    const bool mfma_fb = lkm_ok(a);
     if ((out & logs) && e == hipSuccess) {
         /* the log-scale profile: every posterior output of the request from the
          * reference's log-space recursion (as fb_log_kernel at K <= 8) */
@@ -405,6 +699,13 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         if (out & (fb & ~HHMM_OUT_LOGLIK)) /* the chunks' sweeps: posteriors (the loglik is phase 2's) */
             hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)), dim3(threads),
                                lk_lds<G>(a, threads, discrete), st, a);
+        e = hipGetLastError();
+    } else if ((out & fb) && mfma_fb && e == hipSuccess) {
+        /* many series under each draw: the forward-backward on the matrix cores */
+        constexpr int RT = (KM + 15) / 16, KSM = KM / 4;
+        const int64_t waves = a.S * ((a.N + 15) / 16);
+        const size_t plds = (size_t)4 * a.L * 16 * RT * sizeof(double);
+        hipLaunchKernelGGL((lkm_fb_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
         e = hipGetLastError();
     } else if ((out & fb) && e == hipSuccess) {
         hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);

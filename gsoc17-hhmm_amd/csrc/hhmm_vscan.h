@@ -58,12 +58,14 @@ constexpr int32_t kVsTie = 1 << 30;     /* vs_k: a grid rounding tie inside the 
 #define HHMM_VS_APPROX_F32 1 /* the approximate product pass in float */
 #endif
 /* Discrete models' tie products inside the grid pass (1) or in
- * vs_prod_tie_kernel (0).  Out of line the grid pass drops from 293 to 125
- * registers, but the extra launch over every (pair, chunk, parity) lane cost
- * more at C5 than the occupancy gained: 14.17 against 13.78 ms (one box,
- * profiles/r02zl_ab_c5.log; the float approximate pass alone 13.46). */
+ * vs_prod_tie_kernel (0).  Out of line the grid pass drops from 293 VGPRs and
+ * 31k instructions to ~125 VGPRs: the first out-of-line version launched the
+ * tie kernel over every (pair, chunk, parity) lane and cost more at C5 than the
+ * occupancy gained (14.17 against 13.78 ms, profiles/r02zl_ab_c5.log); the grid
+ * pass now appends its tie chunks to a list (vs_tl: an atomic count, then
+ * lane ids g = p + P c) and the tie kernel walks only that list (round 3). */
 #ifndef HHMM_VS_TIE_INLINE
-#define HHMM_VS_TIE_INLINE 1
+#define HHMM_VS_TIE_INLINE 0
 #endif
 constexpr int32_t kVsNoGrid = -(1 << 20); /* vs_k: no finite magnitude estimate */
 constexpr int32_t kVsSeq = -(1 << 21);    /* vs_k after the exact scan: the chunk was decoded step by step */
@@ -249,37 +251,56 @@ __device__ __forceinline__ void vs_tie_product(const DevArgs &a, const VsLane &v
 /* The tie chunks' two parity products, one lane per parity, for the chunks
  * the grid pass flagged (kVsTie): Gaussian emissions (a tie shows up during
  * the pass), and discrete models when HHMM_VS_TIE_INLINE is 0. */
+constexpr int kVsTieBlocks = 512;
 template <int MODEL, int K>
 __global__ void __launch_bounds__(kBlock) vs_prod_tie_kernel(const DevArgs a)
 {
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
     constexpr int KP = (K + 1) / 2;
     HIP_DYNAMIC_SHARED(double2, lds)
-    /* lanes [0, P*nc): even entry values; [P*nc, 2*P*nc): odd ones */
-    const int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int par = g0 >= a.P * (int64_t)a.vs_nc;
+    /* work items (listed tie chunk, parity): items [0, n) even entry values,
+     * [n, 2n) odd ones; a grid of kVsTieBlocks workgroups walks them */
+    const int n = __builtin_amdgcn_readfirstlane(a.vs_tl[0]);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < 2 * (int64_t)n; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
+    const bool live = i < 2 * (int64_t)n;
+    const int par = live && i >= n;
+    const int64_t g0 = live ? a.vs_tl[1 + (par ? i - n : i)] : 0;
     VsLane v;
-    v.p = (g0 - par * a.P * (int64_t)a.vs_nc) % a.P;
-    v.c = (int)((g0 - par * a.P * (int64_t)a.vs_nc) / a.P);
+    v.p = g0 % a.P;
+    v.c = (int)(g0 / a.P);
     pair_coords(a, v.p, v.n, v.d);
     v.Tp = pair_len(a, v.n);
     v.t0 = v.c * kVsChunk;
     v.t1 = min(v.t0 + kVsChunk, v.Tp);
-    if (v.c >= a.vs_nc || v.c == 0 || v.t0 >= v.Tp)
-        return;
     const int32_t kw = a.vs_k[v.p + a.P * (int64_t)v.c];
-    if (kw == kVsNoGrid || !(kw & kVsTie) || kw < 0)
-        return;
+    const bool work = live && !(v.c >= a.vs_nc || v.c == 0 || v.t0 >= v.Tp) &&
+                      !(kw == kVsNoGrid || !(kw & kVsTie) || kw < 0);
     const int32_t kc = kw & ~kVsTie;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
-    PairParams<MODEL, K> pp;
-    load_params<MODEL, K, true>(pp, a, v.d);
-    if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, true>(slab, a, v.d);
-    const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, v.n);
-    vs_tie_product<MODEL, K>(a, v, pp, slab, sp, ldexp(1.0, 52 - kc), ldexp(1.0, kc - 52), (double)par,
-                             par ? a.vs_m1 : a.vs_m);
+    if (work) {
+        PairParams<MODEL, K> pp;
+        load_params<MODEL, K, true>(pp, a, v.d);
+        if constexpr (ModelTraits<MODEL>::kDiscrete)
+            fill_table<K, true>(slab, a, v.d);
+        const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, v.n);
+        vs_tie_product<MODEL, K>(a, v, pp, slab, sp, ldexp(1.0, 52 - kc), ldexp(1.0, kc - 52), (double)par,
+                                 par ? a.vs_m1 : a.vs_m);
+    }
+    }
+}
+
+/* A grid-pass lane whose chunk holds a rounding tie: flag it and list it for
+ * vs_prod_tie_kernel. */
+__device__ __forceinline__ void vs_list_tie(const DevArgs &a, const VsLane &v, int32_t kc)
+{
+    a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
+    if (kc >= 0) {
+        const int slot = atomicAdd(&a.vs_tl[0], 1);
+        a.vs_tl[1 + slot] = (int32_t)(v.p + a.P * (int64_t)v.c);
+    }
 }
 
 /* Chunk max-plus product M = S_{t0} (x) ... (x) S_{t1-1}, M[r][j] = best path
@@ -332,7 +353,10 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
                 vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 0.0, a.vs_m);
                 vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 1.0, a.vs_m1);
             }
-            a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
+            if (HHMM_VS_TIE_INLINE)
+                a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
+            else
+                vs_list_tie(a, v, kc);
             return;
         }
     }
@@ -418,8 +442,8 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
 #pragma unroll
         for (int j = 0; j < K; ++j)
             a.vs_m[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = (double)M[r][j];
-    if (GRID && tie)
-        a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid; /* |delta| < 1: decode it */
+    if (GRID && tie) /* a tie met during the pass (Gaussian emissions); kc < 0 (|delta| < 1): decoded step by step */
+        vs_list_tie(a, v, kc);
 }
 
 template <int K>
@@ -1024,13 +1048,14 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
     const dim3 gp((unsigned)((a.P + 63) / 64)), b64(64);
     const size_t lds_c = slab * (kBlock / 64), lds_s = vs_sp_lds<MODEL, K>(a.L) + 64 * kVsRow * sizeof(double);
     hipError_t e = hipMemsetAsync(a.vs_fail, 0, (size_t)a.P * sizeof(int32_t), st);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(a.vs_tl, 0, sizeof(int32_t), st); /* the tie list's count */
     if (e == hipSuccess) {
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, false>), gc, bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, true>), gc, bc, lds_c, st, a);
-        if (ModelTraits<MODEL>::kGauss || !HHMM_VS_TIE_INLINE)
-            hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3((unsigned)((2 * lanes + kBlock - 1) / kBlock)), bc,
-                               lds_c, st, a);
+        if (ModelTraits<MODEL>::kGauss || !HHMM_VS_TIE_INLINE) /* the listed tie chunks */
+            hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3(kVsTieBlocks), bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_scan1_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_replay_kernel<MODEL, K>), gc, bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_stitch_kernel<K>), gp, b64, 0, st, a);

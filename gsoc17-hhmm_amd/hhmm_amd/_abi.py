@@ -46,6 +46,7 @@ FLAG_FUSED = 1 << 5
 FLAG_VIT_SCAN = 1 << 6
 FLAG_VIT_SCAN_OFF = 1 << 7
 FLAG_FB_SPLIT = 1 << 16
+FLAG_MFMA_OFF = 1 << 17
 
 
 def flag_scan_chunk_log2(n):

@@ -215,6 +215,11 @@ typedef struct hhmm_draws {
  * backward sweep beside a Viterbi that reads the forward sweep's packed
  * symbols instead of x (identical results). */
 #define HHMM_FLAG_FB_SPLIT (1u << 16)
+/* K > 8 under GRID pairing with at least 16 series per draw (hmm-multinom,
+ * loglik / gamma_tk): the forward-backward runs on the matrix cores (the
+ * series under one draw share its A, so a step of 16 of them is a dense
+ * product).  This flag keeps the state-parallel VALU kernels. */
+#define HHMM_FLAG_MFMA_OFF (1u << 17)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */

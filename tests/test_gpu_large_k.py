@@ -6,7 +6,7 @@ logp_zstar and pair_status bit-exact."""
 import numpy as np
 import pytest
 
-from hhmm_amd import api, synth
+from hhmm_amd import _abi, api, synth
 from tolerances import compare_all
 
 pytestmark = pytest.mark.gpu
@@ -164,3 +164,64 @@ def test_ffbs_large_K_ragged_with_viterbi(engine, oracle):
     got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, uniforms=u, return_status=True)
     ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, uniforms=u, return_status=True, nthreads=8)
     compare_all(got, ref, pars + ["pair_status"])
+
+
+# ---- GRID batches with >= 16 series per draw: the forward-backward on the matrix cores (lkm_fb_kernel)
+
+@pytest.mark.parametrize("K", [9, 12, 16, 17, 23, 24, 32])
+@pytest.mark.parametrize("T", [1, 2, 37, 300])
+def test_mfma_grid_fb(engine, oracle, K, T):
+    data, draws = synth.hmm_multinom(N=20, S=3, T=T, K=K, L=9)
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk", "zstar_t", "logp_zstar"])
+
+
+@pytest.mark.parametrize("K", [12, 23])
+def test_mfma_grid_fb_ragged_matches_state_parallel(engine, oracle, K):
+    """Ragged series inside a tile; the matrix-core path against the oracle
+    and against the state-parallel kernels (HHMM_FLAG_MFMA_OFF) on the same
+    request (both within tolerance of each other: the sums reassociate)."""
+    import hhmm_amd
+    from tolerances import compare
+    N = 37
+    data, draws = synth.hmm_multinom(N=N, S=4, T=700, K=K, L=9)
+    data["T"] = np.random.default_rng(K).integers(1, 701, N).astype(np.int32)
+    pars = ["loglik", "gamma_tk"]
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=pars)
+    a = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine)
+    b = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=_abi.FLAG_MFMA_OFF)
+    for k in pars:
+        compare(k, a[k], b[k])
+
+
+@pytest.mark.parametrize("tiny", [1e-90, 1e-200])
+def test_mfma_grid_fb_near_impossible_runs(engine, oracle, tiny):
+    K = 23
+    data, draws = synth.hmm_multinom(N=16, S=3, T=400, K=K, L=9)
+    phi = np.array(draws["phi_k"], dtype=np.float64)
+    phi[1, :, 8] = tiny
+    phi /= phi.sum(axis=2, keepdims=True)
+    draws["phi_k"] = phi
+    x = np.array(data["x"])
+    x[:, 100:160] = 9
+    data["x"] = x
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk"])
+
+
+def test_mfma_grid_fb_disjoint_filters(engine, oracle):
+    """The gamma sum below 2^-960: the reference's normalised-vector formula."""
+    K = 12
+    data, draws = synth.hmm_multinom(N=16, S=2, T=600, K=K, L=9)
+    A = np.full((2, K, K), 1e-300)
+    for i in range(K):
+        A[:, i, i] = 1.0
+    A /= A.sum(axis=2, keepdims=True)
+    draws["A_ij"] = A
+    phi = np.full((2, K, 9), 1e-3)
+    phi[:, : K // 2, 0] = 1.0
+    phi[:, K // 2:, 1] = 1.0
+    phi /= phi.sum(axis=2, keepdims=True)
+    draws["phi_k"] = phi
+    x = np.ones((16, 600), dtype=np.int32)
+    x[:, 300:] = 2
+    data["x"] = x
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk"])

@@ -116,7 +116,11 @@ def main():
             shape = {}
             if len(sys.argv) > 3:
                 shape = json.loads(sys.argv[3])
+            bp = out / "bench_traffic.json"
+            old = json.loads(bp.read_text()) if bp.exists() else {}
             bt = {"source": f"profiles/{tag}_pmc_traffic.json", **shape, "kernels": {}}
+            if "workloads" in old:  # the evidence workloads' per-step totals (tools/workload_pmc.py)
+                bt["workloads"] = old["workloads"]
             for k, v in summ.items():
                 base = k.split("::")[-1].split("<")[0]
                 bt["kernels"][base] = {"template": k, "hbm_bytes_per_launch": v["hbm_bytes_per_launch"]}
