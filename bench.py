@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--flags", type=int, default=0, help="c3-c5 probes: hhmm_request.flags")
     ap.add_argument("--fused", action="store_true",
                     help="time the one-kernel fused sweep (HHMM_FLAG_FUSED) instead of the two-kernel schedule")
+    ap.add_argument("--schedule", default=None, choices=["step", "fused", "split", "vfb", "two"],
+                    help="c2: the request's schedule: step (library default), fused (HHMM_FLAG_FUSED), "
+                         "split (HHMM_FLAG_FB_SPLIT), vfb (HHMM_FLAG_VFB, phased sweep), two (fb_kernel || "
+                         "viterbi_kernel, HHMM_FLAG_VFB_OFF)")
     ap.add_argument("--no-sequential", action="store_true",
                     help="n2: skip the one untimed run on the sequential kernels after the timed region")
     ap.add_argument("--no-path-gather", action="store_true",
@@ -290,7 +294,8 @@ class DeviceRun:
         self.reqs = {}
         self._ws = {}
         for name, outs, flags in (("step", hot, 0), ("fused", hot, _abi.FLAG_FUSED),
-                                  ("split", hot, _abi.FLAG_FB_SPLIT),
+                                  ("split", hot, _abi.FLAG_FB_SPLIT), ("vfb", hot, _abi.FLAG_VFB),
+                                  ("two", hot, _abi.FLAG_VFB_OFF),
                                   ("fb", ["loglik", "gamma_tk"], 0), ("viterbi", ["zstar_t", "logp_zstar"], 0)):
             r = _abi.Request()
             r.abi_version = _abi.ABI_VERSION
@@ -325,6 +330,17 @@ class DeviceRun:
                                       torch.cuda.current_stream().cuda_stream)
         if st != 0:
             raise RuntimeError(self.lib.hhmm_last_error().decode())
+
+
+# C2 schedules: the kernel the roofline names, and a description
+DEFAULT_SCHEDULE = "two"  # what the library runs for the C2 request without flags
+SCHEDULE_KERNELS = {
+    "two": ("fb_kernel+viterbi_kernel", "fb_kernel || viterbi_kernel (library side stream)"),
+    "fused": ("fbv_kernel", "fused forward-backward + Viterbi sweep (one kernel, HHMM_FLAG_FUSED)"),
+    "split": ("fb_kernel+viterbi_kernel", "forward launch, then backward || packed-symbol Viterbi (HHMM_FLAG_FB_SPLIT)"),
+    "vfb": ("vfb_kernel", "phased sweep: Viterbi over x, then forward-backward over its packed symbols "
+                          "(one kernel, HHMM_FLAG_VFB)"),
+}
 
 
 def bytes_per_step(T):
@@ -421,7 +437,7 @@ def c2_workload(a, lib, rk):
     run = DeviceRun(lib, x, draws, P, T, dev)
     torch.cuda.synchronize()
     s0 = torch.cuda.current_stream()
-    name = "fused" if a.fused else "step"
+    name = a.schedule or ("fused" if a.fused else "step")
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(a.steps)]
     total = torch.zeros(1, dtype=torch.float64, device=dev)
 
@@ -455,7 +471,8 @@ def c2_workload(a, lib, rk):
     # the two halves alone (the north star's "batched forward-backward") and the
     # two-kernel schedule
     solo = {}
-    for nm in ("fb", "viterbi", "step" if a.fused else "fused"):
+    others = [nm for nm in ("step", "two", "vfb", "fused", "split") if nm != name]
+    for nm in ["fb", "viterbi"] + others:
         ts = []
         for _ in range(3):  # back to back on one stream; median of three launches
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -469,15 +486,15 @@ def c2_workload(a, lib, rk):
     if rank == 0:
         fb_b, vit_b, whole_b = bytes_per_step(T)
         units = P * T
-        dom = "fbv_kernel" if a.fused else "fb_kernel+viterbi_kernel"
-        if a.fused:
-            traffic = load_traffic("fbv_kernel", P, T)
+        sched = SCHEDULE_KERNELS[name if name != "step" else DEFAULT_SCHEDULE]
+        dom = sched[0]
+        if "+" not in dom:
+            traffic = load_traffic(dom, P, T)
         else:
             t1, t2 = load_traffic("fb_kernel", P, T), load_traffic("viterbi_kernel", P, T)
             traffic = (t1 + t2) if (t1 is not None and t2 is not None) else None
         achieved = whole_b * units / (step_ms * 1e-3)
         value = world * units * a.steps / elapsed
-        other = "step" if a.fused else "fused"
         line = {
             "metric": "series-timesteps/sec forward-backward+Viterbi (K=4) at 1/2/4/8 GPU; % HBM roofline",
             "value": value,
@@ -494,8 +511,7 @@ def c2_workload(a, lib, rk):
             "config": {"workload": "C2 hmm-multinom K=4 L=9, 1M pairs x T=1000 per GPU (zip pairing)",
                        "pairs_per_gpu": P, "T": T, "outputs": "gamma_tk zstar_t loglik logp_zstar",
                        "parallelism": f"pairs sharded over {world} GPU(s)",
-                       "schedule": ("fused forward-backward + Viterbi sweep (one kernel, HHMM_FLAG_FUSED)"
-                                    if a.fused else "fb_kernel || viterbi_kernel (library side stream)")},
+                       "schedule": sched[1]},
             "whole_step_roofline_frac": whole_b * world * units * a.steps / elapsed / (HBM_PEAK * world),
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
@@ -511,8 +527,9 @@ def c2_workload(a, lib, rk):
                               "roofline_frac": fb_b * units / (solo["fb"] * 1e-3) / HBM_PEAK},
                 "viterbi_kernel": {"ms": solo["viterbi"], "algorithmic_bytes_per_series_timestep": vit_b,
                                    "roofline_frac": vit_b * units / (solo["viterbi"] * 1e-3) / HBM_PEAK},
-                ("fused sweep (HHMM_FLAG_FUSED)" if other == "fused" else "two-kernel schedule"):
-                    {"ms": solo[other], "roofline_frac": whole_b * units / (solo[other] * 1e-3) / HBM_PEAK}},
+                **{SCHEDULE_KERNELS[nm][1]: {"ms": solo[nm],
+                                              "roofline_frac": whole_b * units / (solo[nm] * 1e-3) / HBM_PEAK}
+                   for nm in others if nm != "step"}},
         }
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(T, a.cpu_seconds, a.seed)

@@ -1351,13 +1351,90 @@ constexpr bool fbv_ok()
     return fb_big_ok<MODEL, K>() && vit_chunk(K) == fb_chunk(K);
 }
 
-template <int MODEL, int K, int MODE = FB_GAMMA | FB_PACK | FB_BIG>
-__device__ __forceinline__ void fbv_block(const DevArgs &a, uint32_t block)
+/* FB_BIG backward sweep and the Viterbi backtrack over the same kBigChunk-step
+ * blocks from the end (fbv_kernel, vfb_kernel): gamma from the recomputed
+ * filter and beta, the path from the back-pointer words, which ride the
+ * checkpoint prefetch.  z = zstar_T (0-based); invalid: the path is all zeros
+ * (pair flagged, the walk is discarded). */
+template <int MODEL, int K, int MODE>
+__device__ __forceinline__ void fbv_backward(const DevArgs &a, const FbLane<MODEL, K> &ln, int Tw_min, int Tw_max,
+                                             int z, bool invalid, bool want_z)
 {
     constexpr int C = fb_chunk(K);
     constexpr int SPW = bp_steps_per_word(K);
     constexpr int WPC = C / SPW;
     constexpr int B = kBigChunk, NW = B / 8, CPB = B / C; /* chunks per block */
+    const int64_t p = ln.p;
+    const int Tp = ln.Tp;
+    const int nfull = Tw_min / C;
+    double be[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1) */
+    int bex = 0;
+    const int nblk = (Tw_max + B - 1) / B;
+    const int nfullb = Tw_min / B;
+    const int wmax = a.Tmax / SPW;
+    auto load_blk = [&](int blk, double (&ck)[K], uint32_t (&w)[NW], uint32_t (&bw)[CPB * WPC]) {
+        const int bb = max(blk, 0);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ck[k] = get_tmp(a.ckpt + ln.Qs * ((int64_t)bb * K + k), (uint32_t)p * 8u);
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = at(a.xpk + ln.Qs * (int64_t)(bb * NW + i), (uint32_t)p * 4u);
+#pragma unroll
+        for (int i = 0; i < CPB * WPC; ++i)
+            bw[i] = get_tmp(a.bp + a.P * (int64_t)min(bb * CPB * WPC + i, wmax), (uint32_t)p * 4u);
+    };
+    double ck[K], ckn[K];
+    uint32_t w[NW], wn[NW], bw[CPB * WPC], bwn[CPB * WPC];
+    load_blk(nblk - 1, ck, w, bw);
+    for (int blk = nblk - 1; blk >= 0; --blk) {
+        load_blk(blk - 1, ckn, wn, bwn);
+        if (blk < nfullb)
+            bwd_block_big<MODEL, K, MODE, true>(a, ln, blk * B, w, ck, be, bex);
+        else
+            bwd_block_big<MODEL, K, MODE, false>(a, ln, blk * B, w, ck, be, bex);
+#pragma unroll
+        for (int cc = CPB - 1; cc >= 0; --cc) {
+            const int cidx = blk * CPB + cc;
+            int zb[C];
+            uint32_t wc[WPC];
+#pragma unroll
+            for (int i = 0; i < WPC; ++i)
+                wc[i] = bw[cc * WPC + i];
+            if (cidx < nfull)
+                vit_back_chunk<K, C, true>(Tp, cidx, wc, z, zb);
+            else
+                vit_back_chunk<K, C, false>(Tp, cidx, wc, z, zb);
+            if (want_z) {
+                if (invalid) {
+#pragma unroll
+                    for (int u = 0; u < C; ++u)
+                        zb[u] = 0;
+                }
+                vit_back_flush<C, false>(a, p, Tp, cidx, zb);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ck[k] = ckn[k];
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = wn[i];
+#pragma unroll
+        for (int i = 0; i < CPB * WPC; ++i)
+            bw[i] = bwn[i];
+    }
+}
+
+template <int MODEL, int K, int MODE = FB_GAMMA | FB_PACK | FB_BIG>
+__device__ __forceinline__ void fbv_block(const DevArgs &a, uint32_t block)
+{
+    constexpr int C = fb_chunk(K);
+    constexpr int SPW = bp_steps_per_word(K);
+    constexpr int B = kBigChunk;
     constexpr int KP = (K + 1) / 2;
     static_assert(vit_chunk(K) == C && B % C == 0, "fused sweep: one chunk size for both halves");
     HIP_DYNAMIC_SHARED(double2, lds)
@@ -1472,67 +1549,7 @@ __device__ __forceinline__ void fbv_block(const DevArgs &a, uint32_t block)
     if (invalid)
         z = 0; /* the path is all zeros (pair flagged), the walk below is discarded */
 
-    /* ---- backward sweep + backtrack, kBigChunk-step blocks from the end ---- */
-    double be[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        be[k] = 1.0; /* unbeta_tk[T] = 1 (Q1) */
-    int bex = 0;
-    const int nblk = (Tw_max + B - 1) / B;
-    const int nfullb = Tw_min / B;
-    const int wmax = a.Tmax / SPW;
-    auto load_blk = [&](int blk, double (&ck)[K], uint32_t (&w)[NW], uint32_t (&bw)[CPB * WPC]) {
-        const int bb = max(blk, 0);
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            ck[k] = get_tmp(a.ckpt + ln.Qs * ((int64_t)bb * K + k), (uint32_t)p * 8u);
-#pragma unroll
-        for (int i = 0; i < NW; ++i)
-            w[i] = at(a.xpk + ln.Qs * (int64_t)(bb * NW + i), (uint32_t)p * 4u);
-#pragma unroll
-        for (int i = 0; i < CPB * WPC; ++i)
-            bw[i] = get_tmp(a.bp + a.P * (int64_t)min(bb * CPB * WPC + i, wmax), (uint32_t)p * 4u);
-    };
-    double ck[K], ckn[K];
-    uint32_t w[NW], wn[NW], bw[CPB * WPC], bwn[CPB * WPC];
-    load_blk(nblk - 1, ck, w, bw);
-    for (int blk = nblk - 1; blk >= 0; --blk) {
-        load_blk(blk - 1, ckn, wn, bwn);
-        if (blk < nfullb)
-            bwd_block_big<MODEL, K, MODE, true>(a, ln, blk * B, w, ck, be, bex);
-        else
-            bwd_block_big<MODEL, K, MODE, false>(a, ln, blk * B, w, ck, be, bex);
-#pragma unroll
-        for (int cc = CPB - 1; cc >= 0; --cc) {
-            const int cidx = blk * CPB + cc;
-            int zb[C];
-            uint32_t wc[WPC];
-#pragma unroll
-            for (int i = 0; i < WPC; ++i)
-                wc[i] = bw[cc * WPC + i];
-            if (cidx < nfull)
-                vit_back_chunk<K, C, true>(Tp, cidx, wc, z, zb);
-            else
-                vit_back_chunk<K, C, false>(Tp, cidx, wc, z, zb);
-            if (want_z) {
-                if (invalid) {
-#pragma unroll
-                    for (int u = 0; u < C; ++u)
-                        zb[u] = 0;
-                }
-                vit_back_flush<C, false>(a, p, Tp, cidx, zb);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            ck[k] = ckn[k];
-#pragma unroll
-        for (int i = 0; i < NW; ++i)
-            w[i] = wn[i];
-#pragma unroll
-        for (int i = 0; i < CPB * WPC; ++i)
-            bw[i] = bwn[i];
-    }
+    fbv_backward<MODEL, K, MODE>(a, ln, Tw_min, Tw_max, z, invalid, want_z);
 }
 
 template <int MODEL, int K>
@@ -1542,6 +1559,284 @@ __global__ void __launch_bounds__(kBlock) fbv_kernel(const DevArgs a)
         fbv_block<MODEL, K>(a, blockIdx.x);
 }
 
+
+/* ---- phased sweep: the Viterbi first, then the forward-backward (C2's profile) ---- *
+ * One lane, one pair, three phases over ONE emission slab (so the wave keeps
+ * the single-table LDS footprint of fb_kernel / viterbi_kernel: two waves per
+ * SIMD), x read from HBM once (hmm-multinom.stan:27-132):
+ *   1. log phi in the slab: the max-plus recursion over x (viterbi_kernel's
+ *      arithmetic), writing the back-pointer words and each 8-step chunk's
+ *      symbols packed 4 bits each (the record fb_kernel's FB_PACK writes);
+ *      logp_zstar, pair_status and zstar_T as viterbi_epilogue.
+ *   2. phi in the slab: the scaled filter over the PACKED symbols (0.5 instead
+ *      of 4 B per step), loglik, 16-step checkpoints (FB_BIG).
+ *   3. the FB_BIG backward sweep with the backtrack on the same blocks
+ *      (fbv_backward).
+ * Against fb_kernel beside viterbi_kernel it moves x's second read and the
+ * forward-backward's own symbol packing (-3.5 B per series-timestep); waves
+ * in different phases share a CU the way the two kernels' waves did.  Outputs
+ * are bit-identical to the two kernels (same functions, same operation order).
+ * A wave holding a pair without the renormalisation bound lists itself after
+ * phase 1 (zstar_T parked in zstar[T-1]) for vfb_dense_kernel. */
+#ifndef HHMM_VFB_DEFAULT
+#define HHMM_VFB_DEFAULT 0 /* the phased sweep for the C2 request without flags */
+#endif
+template <int MODEL, int K>
+__device__ __forceinline__ uint32_t pack_chunk(const Obs (&cur)[8])
+{
+    uint32_t w = 0;
+#pragma unroll
+    for (int v = 0; v < 8; ++v)
+        w |= ((uint32_t)(cur[v].x - 1) & 15u) << (4 * v);
+    return w;
+}
+
+/* Phase 1: the max-plus forward over x, packing each chunk's symbols. */
+template <int MODEL, int K>
+__device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const PairParams<MODEL, K> &pp,
+                                            const double2 *slab, const SeriesPtrs &sp, int Tp, int Tw_min,
+                                            int Tw_max, double (&dl)[K], uint32_t &word)
+{
+    constexpr int CV = vit_chunk(K);
+    static_assert(CV == 8, "phased sweep: 8-step chunks");
+    const int nfull = Tw_min / CV;
+    const int nchunk = (Tw_max + CV - 1) / CV;
+    auto pack_put = [&](int c, const Obs (&cur)[CV]) {
+        if (c * CV < Tp)
+            put_tmp(a.xpk + a.P * (int64_t)c, (uint32_t)p * 4u, pack_chunk<MODEL, K>(cur));
+    };
+    Obs cur[CV];
+    load_chunk<MODEL, CV, false>(cur, sp, 0);
+    constexpr int D = kVitGroup;
+    Obs grp[D][CV];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        load_chunk<MODEL, CV, false>(grp[i], sp, (1 + i) * CV);
+    double le[K];
+    emit_log<MODEL, K>(pp, slab, a.L, cur[0], le);
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k)
+        dl[k] = dev_nan(); /* delta_tk[1, K] only (Q3, hmm-multinom.stan:105-106) */
+    dl[K - 1] = le[K - 1];
+    word = 0;
+    vit_fwd_chunk<MODEL, K, CV, false, true>(a, p, pp, slab, Tp, 0, cur, grp[0][0], le, dl, word);
+    pack_put(0, cur);
+    int c = 1;
+    for (; c + D <= nfull; c += D) {
+        Obs nxt[D][CV];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            load_chunk<MODEL, CV, false>(nxt[i], sp, (c + D + i) * CV);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c + i, grp[i],
+                                              (i + 1 < D) ? grp[i + 1 < D ? i + 1 : 0][0] : nxt[0][0], le, dl, word);
+            pack_put(c + i, grp[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int u = 0; u < CV; ++u)
+                grp[i][u] = nxt[i][u];
+    }
+#pragma unroll
+    for (int u = 0; u < CV; ++u)
+        cur[u] = grp[0][u];
+    for (; c < nchunk; ++c) {
+        Obs nxt[CV];
+        load_chunk<MODEL, CV, false>(nxt, sp, (c + 1) * CV);
+        vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
+        pack_put(c, cur);
+#pragma unroll
+        for (int u = 0; u < CV; ++u)
+            cur[u] = nxt[u];
+    }
+}
+
+/* Phase 2: the scaled filter over the packed symbols (FB_BIG checkpoints),
+ * the words a group of chunks ahead; loglik. */
+template <int MODEL, int K, int MODE>
+__device__ __forceinline__ void vfb_forward(const DevArgs &a, const FbLane<MODEL, K> &ln, int Tw_min, int Tw_max)
+{
+    constexpr int C = fb_chunk(K);
+    constexpr int MF = MODE & ~FB_PACK; /* the symbols are packed already */
+    constexpr int D = 8;                /* chunks (words) per prefetch group */
+    const int nfull = Tw_min / C;
+    const int nchunk = (Tw_max + C - 1) / C;
+    const int pkrows = (a.Tmax + C - 1) / C;
+    auto word_at = [&](int c) -> uint32_t {
+        return get_tmp(a.xpk + a.P * (int64_t)min(c, pkrows - 1), (uint32_t)ln.q * 4u);
+    };
+    auto unpack = [&](uint32_t w, Obs (&dst)[C]) {
+#pragma unroll
+        for (int v = 0; v < C; ++v) {
+            dst[v].x = (int)((w >> (4 * v)) & 15u) + 1;
+            dst[v].aux = 0;
+            dst[v].xr = 0.0;
+        }
+    };
+    auto first_obs = [&](uint32_t w) {
+        Obs o;
+        o.x = (int)(w & 15u) + 1;
+        o.aux = 0;
+        o.xr = 0.0;
+        return o;
+    };
+    double al[K], lsc = 0.0;
+    int ex = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        al[k] = 0.0;
+    uint32_t wg[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+        wg[i] = word_at(i);
+    Em<K> ecur;
+    emit_prob<MODEL, K>(ln.pp, ln.slab, ln.L, first_obs(wg[0]), ecur);
+    int c = 0;
+    for (; c + D <= nfull; c += D) {
+        uint32_t wn[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            wn[i] = word_at(c + D + i);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            Obs cur[C];
+            unpack(wg[i], cur);
+            fwd_chunk<MODEL, K, C, MF, true>(a, ln, c + i, cur, first_obs(i + 1 < D ? wg[i + 1 < D ? i + 1 : 0] : wn[0]),
+                                             ecur, al, lsc, ex);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            wg[i] = wn[i];
+    }
+    /* the rest one chunk at a time, the window rolling D words ahead */
+    for (; c < nchunk; ++c) {
+        Obs cur[C];
+        unpack(wg[0], cur);
+        const uint32_t w1 = wg[1];
+#pragma unroll
+        for (int i = 0; i + 1 < D; ++i)
+            wg[i] = wg[i + 1];
+        wg[D - 1] = word_at(c + D);
+        fwd_chunk<MODEL, K, C, MF, false>(a, ln, c, cur, first_obs(w1), ecur, al, lsc, ex);
+    }
+    if ((a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+        a.loglik[ln.p] = log(vsum<K>(al)) + (lsc + kLn2 * ex);
+}
+
+template <int MODEL, int K>
+__device__ __forceinline__ void vfb_lane(const DevArgs &a, int64_t gwave, FbLane<MODEL, K> &ln, int64_t &d)
+{
+    HIP_DYNAMIC_SHARED(double2, lds)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    constexpr int KP = (K + 1) / 2;
+    const int64_t p = min(gwave * 64 + lane, a.P - 1);
+    int64_t n;
+    pair_coords(a, p, n, d);
+    ln.p = p;
+    ln.L = a.L;
+    ln.t0 = 0;
+    ln.Tp = pair_len(a, n);
+    ln.cb = 0;
+    ln.q = p;
+    ln.Qs = a.P;
+    ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+}
+
+template <int MODEL, int K, int MODE = FB_GAMMA | FB_PACK | FB_BIG>
+__device__ __forceinline__ void vfb_block(const DevArgs &a, int64_t gwave)
+{
+    FbLane<MODEL, K> ln;
+    int64_t d;
+    vfb_lane<MODEL, K>(a, gwave, ln, d);
+    const int64_t p = ln.p;
+    const int Tp = ln.Tp;
+    const int Tw_min = wave_min(Tp);
+    const int Tw_max = wave_max(Tp);
+    double2 *slab = const_cast<double2 *>(ln.slab);
+    int z;
+    bool invalid;
+    {
+        /* ---- phase 1: Viterbi over x ---- */
+        PairParams<MODEL, K> lpp;
+        load_params<MODEL, K, true>(lpp, a, d);
+        fill_table<K, true>(slab, a, d);
+        int64_t n, dd;
+        pair_coords(a, p, n, dd);
+        const SeriesPtrs sp = series_ptrs<MODEL, false>(a, n);
+        double dl[K];
+        uint32_t word;
+        vfb_viterbi<MODEL, K>(a, p, lpp, slab, sp, Tp, Tw_min, Tw_max, dl, word);
+        constexpr int SPW = bp_steps_per_word(K);
+        if ((Tp - 1) % SPW != SPW - 1) /* partial last word */
+            put_tmp(a.bp + a.P * (int64_t)((Tp - 1) / SPW), (uint32_t)p * 4u, word);
+        const double lpz = stan_max_vec<K>(dl);
+        z = -1;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (dl[j] == lpz)
+                z = j;
+        invalid = (z < 0) || (Tp >= 2 && lpz == dev_ninf());
+        if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
+            a.logp_zstar[p] = lpz;
+        if (a.pair_status)
+            a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+        if (invalid)
+            z = 0;
+    }
+    /* ---- the slab switches to phi ---- */
+    load_params<MODEL, K, false>(ln.pp, a, d);
+    fill_table<K, false>(slab, a, d);
+    if constexpr (!(MODE & FB_RN1)) {
+        if (wave_any(!renorm_sparse_safe<MODEL, K>(ln.pp, ln.slab, a.L))) {
+            /* zstar_T parked where the backtrack writes it anyway (0: invalid) */
+            if (Tp >= 1)
+                put_out(a.zstar + a.P * (int64_t)(Tp - 1), (uint32_t)p * 4u, invalid ? 0 : z + 1);
+            if ((threadIdx.x & 63) == 0) {
+                const int slot = atomicAdd(&a.rnw[0], 1);
+                a.rnw[1 + slot] = (int32_t)gwave;
+            }
+            return;
+        }
+    }
+    /* ---- phase 2: the filter over the packed symbols ---- */
+    vfb_forward<MODEL, K, MODE>(a, ln, Tw_min, Tw_max);
+    /* ---- phase 3: gamma and the backtrack ---- */
+    fbv_backward<MODEL, K, MODE>(a, ln, Tw_min, Tw_max, z, invalid, true);
+}
+
+template <int MODEL, int K>
+__global__ void __launch_bounds__(kBlock) vfb_kernel(const DevArgs a)
+{
+    if constexpr (fbv_ok<MODEL, K>())
+        vfb_block<MODEL, K>(a, (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+}
+
+/* Phases 2-3 with per-step renormalisation for the waves vfb_kernel listed
+ * (a.rnw), zstar_T read back from zstar[T-1]. */
+template <int MODEL, int K>
+__global__ void __launch_bounds__(64) vfb_dense_kernel(const DevArgs a)
+{
+    if constexpr (fbv_ok<MODEL, K>()) {
+        constexpr int MODE = FB_GAMMA | FB_PACK | FB_BIG | FB_RN1;
+        const int nl = __builtin_amdgcn_readfirstlane(a.rnw[0]);
+        for (int i = blockIdx.x; i < nl; i += gridDim.x) {
+            const int64_t gw = __builtin_amdgcn_readfirstlane(a.rnw[1 + i]);
+            FbLane<MODEL, K> ln;
+            int64_t d;
+            vfb_lane<MODEL, K>(a, gw, ln, d);
+            const int zt = ln.Tp >= 1 ? a.zstar[ln.p + a.P * (int64_t)(ln.Tp - 1)] : 0;
+            load_params<MODEL, K, false>(ln.pp, a, d);
+            fill_table<K, false>(const_cast<double2 *>(ln.slab), a, d);
+            const int Tw_min = wave_min(ln.Tp);
+            const int Tw_max = wave_max(ln.Tp);
+            vfb_forward<MODEL, K, MODE>(a, ln, Tw_min, Tw_max);
+            fbv_backward<MODEL, K, MODE>(a, ln, Tw_min, Tw_max, zt > 0 ? zt - 1 : 0, zt <= 0, true);
+        }
+    }
+}
 
 /* ---- state-parallel Viterbi (few pairs, long T; C5) ------------------- *
  * One lane per (pair, state j): a pair's K <= 4 states sit in one lane quad.
@@ -2617,6 +2912,30 @@ static hhmm_status launch_fbv(const DevArgs &a, hipStream_t st)
     return HHMM_OK;
 }
 
+/* The phased sweep (HHMM_FLAG_VFB): vfb_kernel, then vfb_dense_kernel over the
+ * waves it listed. */
+template <int MODEL, int K>
+static hhmm_status launch_vfb(const DevArgs &a, hipStream_t st)
+{
+    LaunchShape s;
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s, "HHMM_PROBE_FB_WAVES")) {
+        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    hipError_t e = hipMemsetAsync(a.rnw, 0, sizeof(int32_t), st); /* the dense-wave list's count */
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL((vfb_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
+        hipLaunchKernelGGL((vfb_dense_kernel<MODEL, K>), dim3(kDenseBlocks), dim3(64), s.lds / (s.block.x / 64), st,
+                           a);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) {
+        set_error("vfb_kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
 /* The split schedule (HHMM_FLAG_FB_SPLIT, C2's profile): the forward sweep
  * alone (x read once: loglik, checkpoints, packed symbols), then the
  * HBM-bound backward sweep on the caller's stream beside the VALU-bound
@@ -2716,6 +3035,12 @@ static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const 
         if (vit && (out & HHMM_OUT_GAMMA) && !(out & extra) && a.xpk && a.scan_cl == 0 &&
             (a.flags & HHMM_FLAG_FUSED) && !use_vit_states(a))
             return launch_fbv<MODEL, K>(a, st);
+        const bool vfb_on = (a.flags & HHMM_FLAG_VFB) ||
+                            (HHMM_VFB_DEFAULT && !(a.flags & (HHMM_FLAG_VFB_OFF | HHMM_FLAG_FUSED | HHMM_FLAG_FB_SPLIT |
+                                                              HHMM_FLAG_NO_FUSE)));
+        if (vit && (out & HHMM_OUT_GAMMA) && (out & HHMM_OUT_ZSTAR) && a.zstar && !(out & extra) && a.xpk &&
+            a.rnw && a.scan_cl == 0 && a.vs_nc == 0 && vfb_on && !use_vit_states(a))
+            return launch_vfb<MODEL, K>(a, st);
         if (vit && (out & HHMM_OUT_GAMMA) && !(out & extra) && a.xpk && a.scan_cl == 0 && a.vs_nc == 0 &&
             (a.flags & HHMM_FLAG_FB_SPLIT) && !(a.flags & HHMM_FLAG_NO_FUSE) && !use_vit_states(a))
             return launch_split<MODEL, K>(a, st);

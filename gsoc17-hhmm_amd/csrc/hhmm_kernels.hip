@@ -163,7 +163,7 @@ int lkm_plan(int model, int K, int64_t N, int pairing, uint32_t outputs, uint32_
     const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
                         HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
     if (model != HHMM_MODEL_HMM_MULTINOM || K <= kMaxK || K > kMaxKLarge || pairing != HHMM_PAIR_GRID || N < 16 ||
-        scan_cl > 0 || (flags & HHMM_FLAG_MFMA_OFF) || !(outputs & fb) ||
+        scan_cl > 0 || !(flags & HHMM_FLAG_LKM_MFMA) || !(outputs & fb) ||
         (outputs & fb & ~(HHMM_OUT_LOGLIK | HHMM_OUT_GAMMA)))
         return 0;
     return K <= 16 ? 4 : (K <= 24 ? 6 : 8);

@@ -616,7 +616,7 @@ __global__ void __launch_bounds__(256) lkm_fb_kernel(const DevArgs a)
 
 /* lkm_fb_kernel's domain: hmm-multinom under GRID pairing with at least 16
  * series per draw, the hot output profile (loglik + gamma_tk), sequential in
- * T (no scan), not switched off (HHMM_FLAG_MFMA_OFF); hhmm_kernels.hip sizes
+ * T (no scan), asked for (HHMM_FLAG_LKM_MFMA, opt-in); hhmm_kernels.hip sizes
  * its checkpoints by the same rule (lkm_plan). */
 static inline bool lkm_ok(const DevArgs &a)
 {

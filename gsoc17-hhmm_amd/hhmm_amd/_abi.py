@@ -46,7 +46,9 @@ FLAG_FUSED = 1 << 5
 FLAG_VIT_SCAN = 1 << 6
 FLAG_VIT_SCAN_OFF = 1 << 7
 FLAG_FB_SPLIT = 1 << 16
-FLAG_MFMA_OFF = 1 << 17
+FLAG_LKM_MFMA = 1 << 17
+FLAG_VFB = 1 << 18
+FLAG_VFB_OFF = 1 << 19
 
 
 def flag_scan_chunk_log2(n):

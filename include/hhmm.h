@@ -215,11 +215,21 @@ typedef struct hhmm_draws {
  * backward sweep beside a Viterbi that reads the forward sweep's packed
  * symbols instead of x (identical results). */
 #define HHMM_FLAG_FB_SPLIT (1u << 16)
-/* K > 8 under GRID pairing with at least 16 series per draw (hmm-multinom,
- * loglik / gamma_tk): the forward-backward runs on the matrix cores (the
- * series under one draw share its A, so a step of 16 of them is a dense
- * product).  This flag keeps the state-parallel VALU kernels. */
-#define HHMM_FLAG_MFMA_OFF (1u << 17)
+/* Opt-in: K > 8 under GRID pairing with at least 16 series per draw
+ * (hmm-multinom, loglik / gamma_tk): the forward-backward on the matrix cores
+ * (the series under one draw share its A, so a step of 16 of them is a dense
+ * product).  Measured 3x slower than the state-parallel VALU
+ * kernels at N1 (117 vs 41 ms): a wave's 16 series write gamma at a stride of
+ * S pairs, so every store is a partial line.  Off by default. */
+#define HHMM_FLAG_LKM_MFMA (1u << 17)
+/* The C2 profile (hmm-multinom, K = 4, gamma_tk (+ loglik) with zstar_t, lane
+ * decoder) as one phased sweep per pair: the Viterbi over x (packing the
+ * symbols), then the forward-backward over the packed symbols with the
+ * backtrack in its backward sweep (identical results). */
+#define HHMM_FLAG_VFB (1u << 18)
+/* Forbids the phased sweep where it is the default (the C2 request then runs
+ * fb_kernel beside viterbi_kernel on the library's side stream). */
+#define HHMM_FLAG_VFB_OFF (1u << 19)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */

@@ -83,14 +83,16 @@ def test_c1_full_size(engine, oracle):
 # ---- C2: hmm-multinom K=4, L=9, T=1000 ---------------------------------------------------
 
 @pytest.mark.parametrize("flags", [0, _abi.FLAG_VIT_LANES, _abi.FLAG_VIT_LANES | _abi.FLAG_FUSED,
-                                   _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT],
-                         ids=["auto", "lane", "lane-fused", "lane-split"])
+                                   _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT, _abi.FLAG_VIT_LANES | _abi.FLAG_VFB],
+                         ids=["auto", "lane", "lane-fused", "lane-split", "lane-vfb"])
 def test_c2_slice(engine, oracle, flags):
     """A 4096-pair zip slice; `lane` forces the lane-per-pair decoder the full
     1M-pair batch dispatches to (P >= 131072); `lane-fused` the same as the
     one-kernel forward-backward + Viterbi sweep (HHMM_FLAG_FUSED); `lane-split`
     as the split schedule (HHMM_FLAG_FB_SPLIT: forward launch, then backward
-    beside a Viterbi decoding the packed symbols)."""
+    beside a Viterbi decoding the packed symbols); `lane-vfb` as the phased
+    sweep (HHMM_FLAG_VFB: the Viterbi over x, then the forward-backward over
+    its packed symbols, one kernel)."""
     data, draws = synth.hmm_multinom(N=4096, S=4096, T=1000, K=4, L=9)
     got, ref = gpu_and_oracle(engine, oracle, "hmm-multinom", data, draws, HOT, pairing="zip", flags=flags)
     compare_all(got, ref, HOT + ["pair_status"])
@@ -140,11 +142,11 @@ def test_c2_full_batch(engine, oracle):
     got = {"loglik": ll[ii].cpu().numpy(), "logp_zstar": lz[ii].cpu().numpy(),
            "zstar_t": zs[:, ii].T.cpu().numpy(), "gamma_tk": g[:, :, ii].permute(2, 1, 0).cpu().numpy()}
     compare_all(got, ref, HOT)
-    # the fused sweep and the split schedule give the same bits
+    # the fused sweep, the split schedule and the phased sweep give the same bits
     z1, ll1, lz1 = zs.clone(), ll.clone(), lz.clone()
     gs1 = g[:, :, ii].clone()
     gsum1 = g.sum(dim=(0, 1))
-    for req in ("fused", "split"):
+    for req in ("fused", "split", "vfb"):
         zs.fill_(0)
         g.fill_(0.0)
         run.launch(req)

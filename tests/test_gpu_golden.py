@@ -23,6 +23,7 @@ SCHEDULES = {
     "vscan": _abi.FLAG_VIT_SCAN,
     "vit-lanes": _abi.FLAG_VIT_LANES,
     "vit-states": _abi.FLAG_VIT_STATES,
+    "vfb": _abi.FLAG_VIT_LANES | _abi.FLAG_VFB,
 }
 
 

@@ -14,9 +14,9 @@ pytestmark = pytest.mark.gpu
 PARS = ["loglik", "alpha_tk", "beta_tk", "ungamma_tk", "gamma_tk", "zstar_t", "logp_zstar"]
 
 
-def run_both(engine, oracle, model, data, draws, pars=PARS, pairing="grid"):
+def run_both(engine, oracle, model, data, draws, pars=PARS, pairing="grid", flags=0):
     import hhmm_amd
-    got = hhmm_amd.gqs(model, data, draws, pars=pars, pairing=pairing, lib=engine, return_status=True)
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, pairing=pairing, lib=engine, return_status=True, flags=flags)
     ref = oracle.gqs(model, data, draws, pars=pars, pairing=pairing, return_status=True, nthreads=8)
     compare_all(got, ref, pars + ["pair_status"])
     assert got["status"] == ref["status"]
@@ -166,19 +166,22 @@ def test_ffbs_large_K_ragged_with_viterbi(engine, oracle):
     compare_all(got, ref, pars + ["pair_status"])
 
 
-# ---- GRID batches with >= 16 series per draw: the forward-backward on the matrix cores (lkm_fb_kernel)
+# ---- GRID batches with >= 16 series per draw: the forward-backward on the matrix cores (lkm_fb_kernel,
+# opt-in HHMM_FLAG_LKM_MFMA)
+MF = _abi.FLAG_LKM_MFMA
 
 @pytest.mark.parametrize("K", [9, 12, 16, 17, 23, 24, 32])
 @pytest.mark.parametrize("T", [1, 2, 37, 300])
 def test_mfma_grid_fb(engine, oracle, K, T):
     data, draws = synth.hmm_multinom(N=20, S=3, T=T, K=K, L=9)
-    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk", "zstar_t", "logp_zstar"])
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk", "zstar_t", "logp_zstar"],
+             flags=MF)
 
 
 @pytest.mark.parametrize("K", [12, 23])
 def test_mfma_grid_fb_ragged_matches_state_parallel(engine, oracle, K):
     """Ragged series inside a tile; the matrix-core path against the oracle
-    and against the state-parallel kernels (HHMM_FLAG_MFMA_OFF) on the same
+    and against the state-parallel kernels (the default) on the same
     request (both within tolerance of each other: the sums reassociate)."""
     import hhmm_amd
     from tolerances import compare
@@ -186,9 +189,9 @@ def test_mfma_grid_fb_ragged_matches_state_parallel(engine, oracle, K):
     data, draws = synth.hmm_multinom(N=N, S=4, T=700, K=K, L=9)
     data["T"] = np.random.default_rng(K).integers(1, 701, N).astype(np.int32)
     pars = ["loglik", "gamma_tk"]
-    run_both(engine, oracle, "hmm-multinom", data, draws, pars=pars)
-    a = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine)
-    b = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=_abi.FLAG_MFMA_OFF)
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=pars, flags=MF)
+    a = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=MF)
+    b = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine)
     for k in pars:
         compare(k, a[k], b[k])
 
@@ -204,7 +207,7 @@ def test_mfma_grid_fb_near_impossible_runs(engine, oracle, tiny):
     x = np.array(data["x"])
     x[:, 100:160] = 9
     data["x"] = x
-    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk"])
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk"], flags=MF)
 
 
 def test_mfma_grid_fb_disjoint_filters(engine, oracle):
@@ -224,4 +227,4 @@ def test_mfma_grid_fb_disjoint_filters(engine, oracle):
     x = np.ones((16, 600), dtype=np.int32)
     x[:, 300:] = 2
     data["x"] = x
-    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk"])
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["loglik", "gamma_tk"], flags=MF)

@@ -245,16 +245,19 @@ def test_viterbi_layouts_ragged(engine, oracle, model, layout):
     compare_all(got, ref, pars + ["pair_status"])
 
 
+@pytest.mark.parametrize("sched", ["split", "vfb"])
 @pytest.mark.parametrize("T", [1, 2, 9, 37, 130])
-def test_split_schedule(engine, oracle, T):
+def test_split_schedule(engine, oracle, T, sched):
     """HHMM_FLAG_FB_SPLIT (hmm-multinom K = 4, gamma + path in one request):
     the forward launch packs the symbols, the Viterbi decodes them beside the
     backward launch -- bit-exact paths, gamma / loglik within tolerance, at
-    series lengths around the 8-step chunk and 16-step block sizes."""
+    series lengths around the 8-step chunk and 16-step block sizes.  `vfb`:
+    the phased sweep (HHMM_FLAG_VFB), whose Viterbi packs the symbols its
+    forward-backward reads."""
     import hhmm_amd
     pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
     data, draws = synth.hmm_multinom(N=70, S=70, T=T, K=4, L=9)
-    flags = _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT
+    flags = _abi.FLAG_VIT_LANES | (_abi.FLAG_FB_SPLIT if sched == "split" else _abi.FLAG_VFB)
     got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=flags, pairing="zip",
                        return_status=True)
     ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True)
@@ -298,7 +301,8 @@ def _near_impossible_runs(tiny, K=4, N=192, which=(70,)):
 
 @pytest.mark.parametrize("tiny", [1e-30, 1e-70, 1e-90, 1e-200])
 @pytest.mark.parametrize("flags", [_abi.FLAG_VIT_LANES, _abi.FLAG_VIT_LANES | _abi.FLAG_FUSED,
-                                   _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT], ids=["default", "fused", "split"])
+                                   _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT, _abi.FLAG_VIT_LANES | _abi.FLAG_VFB],
+                         ids=["default", "fused", "split", "vfb"])
 def test_gamma_profile_near_impossible_runs(engine, oracle, tiny, flags):
     """The gamma profile renormalises every 4 steps (FB_BIG, kBigRenorm) only
     in waves whose pairs bound the 4-step shrink (renorm_sparse_safe: the
@@ -354,7 +358,8 @@ def test_unsupported_shape_leaves_no_kernel_running(engine, oracle):
     compare_all(got, ref, pars + ["pair_status"])
 
 
-def test_split_schedule_ragged(engine, oracle):
+@pytest.mark.parametrize("sched", ["split", "vfb"])
+def test_split_schedule_ragged(engine, oracle, sched):
     """Ragged lengths inside one wave: a lane's packed rows past its own end
     are padding the decoder never consumes."""
     import hhmm_amd
@@ -362,7 +367,7 @@ def test_split_schedule_ragged(engine, oracle):
     N = 130
     data, draws = synth.hmm_multinom(N=N, S=N, T=300, K=4, L=9)
     data["T"] = np.random.default_rng(5).integers(1, 301, N).astype(np.int32)
-    flags = _abi.FLAG_VIT_LANES | _abi.FLAG_FB_SPLIT
+    flags = _abi.FLAG_VIT_LANES | (_abi.FLAG_FB_SPLIT if sched == "split" else _abi.FLAG_VFB)
     got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=flags, pairing="zip",
                        return_status=True)
     ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True)
@@ -382,6 +387,27 @@ def test_viterbi_states_backtrack_groups(engine, oracle, model):
     got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, flags=_abi.FLAG_VIT_STATES, return_status=True)
     ref = oracle.gqs(model, data, draws, pars=pars, return_status=True)
     compare_all(got, ref, pars + ["pair_status"])
+
+
+def test_vfb_invalid_backpointer(engine, oracle):
+    """The phased sweep (HHMM_FLAG_VFB) on the all -inf delta_T pair: flagged,
+    the path zeroed, gamma / loglik as the oracle; with a near-impossible
+    symbol in another pair of the wave, so the wave takes the per-step
+    renormalisation kernel (zstar_T parked in zstar[T-1])."""
+    import hhmm_amd
+    pars = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
+    data, draws = synth.hmm_multinom(N=3, S=3, T=40, K=4, L=9)
+    draws["phi_k"][0, :, 8] = 0.0
+    draws["phi_k"][2, :, 7] = 1e-200
+    draws["phi_k"] /= draws["phi_k"].sum(axis=2, keepdims=True)
+    data["x"][0, 7] = 9
+    data["x"][2, 10:20] = 8
+    for flags in (_abi.FLAG_VIT_LANES | _abi.FLAG_VFB,):
+        got = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine, flags=flags, pairing="zip",
+                           return_status=True)
+        ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, pairing="zip", return_status=True)
+        assert ref["pair_status"][0] == 1
+        compare_all(got, ref, pars + ["pair_status"])
 
 
 @pytest.mark.parametrize("layout", ["lanes", "states"])
