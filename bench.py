@@ -333,7 +333,7 @@ class DeviceRun:
 
 
 # C2 schedules: the kernel the roofline names, and a description
-DEFAULT_SCHEDULE = "two"  # what the library runs for the C2 request without flags
+DEFAULT_SCHEDULE = "vfb"  # what the library runs for the C2 request without flags (HHMM_VFB_DEFAULT)
 SCHEDULE_KERNELS = {
     "two": ("fb_kernel+viterbi_kernel", "fb_kernel || viterbi_kernel (library side stream)"),
     "fused": ("fbv_kernel", "fused forward-backward + Viterbi sweep (one kernel, HHMM_FLAG_FUSED)"),

@@ -17,7 +17,9 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
+#include <algorithm>
 
 #include "hhmm_internal.h"
 #include "build_id.h" /* HHMM_SOURCE_HASH (Makefile) */
@@ -265,12 +267,14 @@ static int64_t npairs(const hhmm_request *r)
 }
 
 /* One array of the request: where it lives and how many elements. */
+enum ArrayClass { SERIES = 0, DRAWS = 1, PAIRS = 2 }; /* leading (fastest) dimension N, S or P */
 struct ArrayDesc {
     const void *host;
     void **dev_slot; /* field in the device copy of the request/result */
     size_t elems;
     size_t esize;
     bool output;
+    int cls;         /* ArrayClass */
 };
 
 #define REQUIRE(cond, ...)                                                                          \
@@ -415,41 +419,43 @@ static void describe(const hhmm_request *r, const hhmm_result *o, hhmm_request *
     const size_t K = (size_t)d.K, L = (size_t)(d.L > 0 ? d.L : 0), M = (size_t)(d.M > 0 ? d.M : 0);
     const size_t P = (size_t)npairs(r);
     const uint32_t out = r->outputs;
-    auto in = [&](const void *h, const void **slot, size_t n, size_t es) {
+    /* the class follows from the leading dimension of the element count */
+    auto cls_of = [&](size_t lead) { return lead == 0 ? (int)SERIES : lead == 1 ? (int)DRAWS : (int)PAIRS; };
+    auto in = [&](const void *h, const void **slot, size_t n, size_t es, int lead) {
         if (h)
-            v.push_back({h, (void **)slot, n, es, false});
+            v.push_back({h, (void **)slot, n, es, false, cls_of((size_t)lead)});
     };
     auto ou = [&](uint32_t bit, void *h, void **slot, size_t n, size_t es) {
         if ((out & bit) && h)
-            v.push_back({h, slot, n, es, true});
+            v.push_back({h, slot, n, es, true, PAIRS});
         else
             *slot = nullptr;
     };
-    in(d.T, (const void **)&dr->data.T, N, 4);
-    in(d.x_int, (const void **)&dr->data.x_int, N * Tm, 4);
-    in(d.x_real, (const void **)&dr->data.x_real, N * Tm, 8);
-    in(d.g, (const void **)&dr->data.g, N * Tm, 4);
-    in(d.sign, (const void **)&dr->data.sign, N * Tm, 4);
-    in(d.u, (const void **)&dr->data.u, N * Tm * M, 8);
-    in(d.T_oos, (const void **)&dr->data.T_oos, N, 4);
-    in(d.x_oos, (const void **)&dr->data.x_oos, N * To, 4);
-    in(d.sign_oos, (const void **)&dr->data.sign_oos, N * To, 4);
+    in(d.T, (const void **)&dr->data.T, N, 4, 0);
+    in(d.x_int, (const void **)&dr->data.x_int, N * Tm, 4, 0);
+    in(d.x_real, (const void **)&dr->data.x_real, N * Tm, 8, 0);
+    in(d.g, (const void **)&dr->data.g, N * Tm, 4, 0);
+    in(d.sign, (const void **)&dr->data.sign, N * Tm, 4, 0);
+    in(d.u, (const void **)&dr->data.u, N * Tm * M, 8, 0);
+    in(d.T_oos, (const void **)&dr->data.T_oos, N, 4, 0);
+    in(d.x_oos, (const void **)&dr->data.x_oos, N * To, 4, 0);
+    in(d.sign_oos, (const void **)&dr->data.sign_oos, N * To, 4, 0);
     dr->data.hyperparams = nullptr;
-    in(w.p_1k, (const void **)&dr->draws.p_1k, S * K, 8);
-    in(w.A_ij, (const void **)&dr->draws.A_ij, S * K * K, 8);
-    in(w.phi_k, (const void **)&dr->draws.phi_k, S * K * L, 8);
-    in(w.mu_k, (const void **)&dr->draws.mu_k, S * K, 8);
-    in(w.sigma_k, (const void **)&dr->draws.sigma_k, S * K, 8);
-    in(w.w_km, (const void **)&dr->draws.w_km, S * K * M, 8);
-    in(w.b_km, (const void **)&dr->draws.b_km, S * K * M, 8);
-    in(w.s_k, (const void **)&dr->draws.s_k, S * K, 8);
-    in(w.lambda_kl, (const void **)&dr->draws.lambda_kl, S * K * L, 8);
-    in(w.mu_kl, (const void **)&dr->draws.mu_kl, S * K * L, 8);
-    in(w.s_kl, (const void **)&dr->draws.s_kl, S * K * L, 8);
-    in(w.p_11, (const void **)&dr->draws.p_11, S, 8);
-    in(w.A_row, (const void **)&dr->draws.A_row, S * 4, 8);
-    in(r->ffbs_u, (const void **)&dr->ffbs_u, P * Tm, 8);
-    in(r->hat_rand, (const void **)&dr->hat_rand, P * Tm * 3, 8);
+    in(w.p_1k, (const void **)&dr->draws.p_1k, S * K, 8, 1);
+    in(w.A_ij, (const void **)&dr->draws.A_ij, S * K * K, 8, 1);
+    in(w.phi_k, (const void **)&dr->draws.phi_k, S * K * L, 8, 1);
+    in(w.mu_k, (const void **)&dr->draws.mu_k, S * K, 8, 1);
+    in(w.sigma_k, (const void **)&dr->draws.sigma_k, S * K, 8, 1);
+    in(w.w_km, (const void **)&dr->draws.w_km, S * K * M, 8, 1);
+    in(w.b_km, (const void **)&dr->draws.b_km, S * K * M, 8, 1);
+    in(w.s_k, (const void **)&dr->draws.s_k, S * K, 8, 1);
+    in(w.lambda_kl, (const void **)&dr->draws.lambda_kl, S * K * L, 8, 1);
+    in(w.mu_kl, (const void **)&dr->draws.mu_kl, S * K * L, 8, 1);
+    in(w.s_kl, (const void **)&dr->draws.s_kl, S * K * L, 8, 1);
+    in(w.p_11, (const void **)&dr->draws.p_11, S, 8, 1);
+    in(w.A_row, (const void **)&dr->draws.A_row, S * 4, 8, 1);
+    in(r->ffbs_u, (const void **)&dr->ffbs_u, P * Tm, 8, 2);
+    in(r->hat_rand, (const void **)&dr->hat_rand, P * Tm * 3, 8, 2);
     const size_t Tz = (r->model == HHMM_MODEL_TAYAL_LITE) ? To : Tm;
     ou(HHMM_OUT_LOGLIK, o->loglik, (void **)&dq->loglik, P, 8);
     ou(HHMM_OUT_UNALPHA, o->unalpha_tk, (void **)&dq->unalpha_tk, P * Tm * K, 8);
@@ -489,6 +495,252 @@ static hhmm_status check_device()
     return HHMM_OK;
 }
 
+static hhmm_status check_arch(int dev)
+{
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return hip_fail(hipGetLastError(), "hipGetDeviceProperties");
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error("device %d is %s, this build targets gfx950", dev, prop.gcnArchName);
+        return HHMM_ERR_NO_DEVICE;
+    }
+    return HHMM_OK;
+}
+
+/* ---------------- device set (hhmm_init / hhmm_init_devices) ---------------- */
+struct DevSet {
+    std::mutex mu;
+    std::vector<int> devs; /* ordinals HHMM_DEVICE_SET shards over (repeats allowed); empty: {0} */
+};
+static DevSet &devset()
+{
+    static DevSet d;
+    return d;
+}
+
+/* One shard of a host request: per array class (series, draws, pairs) the
+ * first element, the element count and the caller's leading extent.  An
+ * array of class c with e elements is then `e / lead` rows of `cnt` elements,
+ * at a pitch of `lead` in the caller's buffer and packed in the shard's
+ * device copy -- which is exactly the [N', ...] / [S', ...] / [P', ...]
+ * layout of the sub-request (every array is series-, draw- or pair-fastest). */
+struct Shard {
+    int64_t off[3], cnt[3], lead[3];
+};
+
+static Shard whole_shard(const hhmm_request *r)
+{
+    const int64_t N = r->data.n_series, S = r->draws.n_draws, P = npairs(r);
+    return Shard{{0, 0, 0}, {N, S, P}, {N, S, P}};
+}
+
+/* Splits a request over `n` shards: contiguous series ranges (ZIP / BLOCK take
+ * the series' own draws, GRID all draws); a GRID request with fewer series
+ * than shards splits its draws instead (pairs p = s + S*n with s in the
+ * range: rows of S' pairs at a pitch of S). */
+static std::vector<Shard> make_shards(const hhmm_request *r, int n)
+{
+    const int64_t N = r->data.n_series, S = r->draws.n_draws, P = npairs(r);
+    std::vector<Shard> v;
+    const bool by_draws = r->pairing == HHMM_PAIR_GRID && N < n;
+    const int64_t units = by_draws ? S : N;
+    const int64_t ns = std::min<int64_t>(n, units);
+    for (int64_t i = 0; i < ns; ++i) {
+        const int64_t a = units * i / ns, b = units * (i + 1) / ns;
+        Shard sh;
+        if (by_draws) {
+            sh = Shard{{0, a, a}, {N, b - a, b - a}, {N, S, S}};
+        } else if (r->pairing == HHMM_PAIR_ZIP) {
+            sh = Shard{{a, a, a}, {b - a, b - a, b - a}, {N, S, P}};
+        } else if (r->pairing == HHMM_PAIR_BLOCK) {
+            const int64_t B = S / N;
+            sh = Shard{{a, B * a, B * a}, {b - a, B * (b - a), B * (b - a)}, {N, S, P}};
+        } else { /* GRID by series */
+            sh = Shard{{a, 0, S * a}, {b - a, S, S * (b - a)}, {N, S, P}};
+        }
+        v.push_back(sh);
+    }
+    return v;
+}
+
+/* Host <-> device copy of one array's shard: rows of cnt elements at a pitch
+ * of lead on the host, packed on the device. */
+static hipError_t copy_shard(void *dev, const void *host, const ArrayDesc &a, const Shard &sh, bool to_device)
+{
+    const size_t es = a.esize, lead = (size_t)sh.lead[a.cls], cnt = (size_t)sh.cnt[a.cls];
+    const size_t rows = a.elems / lead;
+    char *h = (char *)host + (size_t)sh.off[a.cls] * es;
+    if (cnt == lead)
+        return to_device ? hipMemcpy(dev, h, rows * cnt * es, hipMemcpyHostToDevice)
+                         : hipMemcpy(h, dev, rows * cnt * es, hipMemcpyDeviceToHost);
+    return to_device ? hipMemcpy2D(dev, cnt * es, h, lead * es, cnt * es, rows, hipMemcpyHostToDevice)
+                     : hipMemcpy2D(h, lead * es, dev, cnt * es, cnt * es, rows, hipMemcpyDeviceToHost);
+}
+
+/* Runs one shard of a host request on the current device: uploads its slices,
+ * launches, downloads its output slices in place.  status: the caller's
+ * [P] host array, written at the shard's pairs; *failures counts them. */
+static hhmm_status run_on_device(const hhmm_request *req, hhmm_result *res, const Shard &sh, int32_t *status,
+                                 int64_t *failures)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipGetDevice");
+    hhmm_request dreq = *req;
+    hhmm_result dres = *res;
+    dres.pair_status = nullptr;
+    std::vector<ArrayDesc> arrays;
+    describe(req, res, &dreq, &dres, arrays);
+    dreq.data.n_series = sh.cnt[SERIES];
+    dreq.draws.n_draws = sh.cnt[DRAWS];
+    const int64_t P = npairs(&dreq);
+    if (P < 1) {
+        set_error("internal: shard describes no pairs");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    const bool ragged = req->data.T != nullptr || req->data.T_oos != nullptr;
+
+    std::vector<void *> owned;
+    auto cleanup = [&]() {
+        for (void *p : owned)
+            pool_put(p);
+    };
+    for (auto &a : arrays) {
+        const size_t bytes = a.elems / (size_t)sh.lead[a.cls] * (size_t)sh.cnt[a.cls] * a.esize;
+        void *dp = pool_get(dev, bytes);
+        if (!dp) {
+            cleanup();
+            set_error("device %d: allocation of %zu bytes failed", dev, bytes);
+            return HHMM_ERR_OUT_OF_MEMORY;
+        }
+        owned.push_back(dp);
+        *a.dev_slot = dp;
+        /* inputs always; outputs too when padded steps must round-trip untouched */
+        if (!a.output || ragged) {
+            e = copy_shard(dp, a.host, a, sh, true);
+            if (e != hipSuccess) {
+                cleanup();
+                return hip_fail(e, "hipMemcpy H2D");
+            }
+        }
+    }
+    void *dstatus = pool_get(dev, (size_t)P * sizeof(int32_t));
+    if (!dstatus) {
+        cleanup();
+        set_error("device %d: allocation failed (pair_status)", dev);
+        return HHMM_ERR_OUT_OF_MEMORY;
+    }
+    owned.push_back(dstatus);
+    (void)hipMemset(dstatus, 0, (size_t)P * sizeof(int32_t));
+    dres.pair_status = (int32_t *)dstatus;
+
+    const size_t wsb = workspace_bytes(dreq.model, dreq.data.K, dreq.data.L, dreq.data.T_max, dreq.data.T_oos_max, P,
+                                       dreq.outputs, (uint32_t)dreq.flags, dreq.data.n_series, dreq.pairing);
+    void *ws = pool_get(dev, wsb);
+    if (!ws) {
+        cleanup();
+        set_error("device %d: workspace allocation of %zu bytes failed", dev, wsb);
+        return HHMM_ERR_OUT_OF_MEMORY;
+    }
+    owned.push_back(ws);
+
+    hhmm_status s = launch_all(&dreq, &dres, P, ws, nullptr);
+    if (s != HHMM_OK) {
+        /* a failed launch may follow one that is still running: drain this
+         * request's streams before its pooled buffers can be handed to another
+         * request; a sticky device error from an earlier fault is reported
+         * beside the launch error instead of being buried under it */
+        e = sync_request(nullptr);
+        cleanup();
+        if (e != hipSuccess) {
+            std::string first = hhmm_last_error();
+            set_error("%s; draining the request's streams then failed: %s", first.c_str(), hipGetErrorString(e));
+        }
+        return s;
+    }
+    e = sync_request(nullptr);
+    if (e != hipSuccess) {
+        cleanup();
+        return hip_fail(e, "kernel execution");
+    }
+    for (auto &a : arrays) {
+        if (!a.output)
+            continue;
+        e = copy_shard(*a.dev_slot, a.host, a, sh, false);
+        if (e != hipSuccess) {
+            cleanup();
+            return hip_fail(e, "hipMemcpy D2H");
+        }
+    }
+    /* pair_status: [P] in the caller's layout (a PAIRS array of P elements) */
+    ArrayDesc st{status, nullptr, (size_t)npairs(req), sizeof(int32_t), true, PAIRS};
+    e = copy_shard(dstatus, status, st, sh, false);
+    cleanup();
+    if (e != hipSuccess)
+        return hip_fail(e, "hipMemcpy D2H (status)");
+    const size_t lead = (size_t)sh.lead[PAIRS], cnt = (size_t)sh.cnt[PAIRS], rows = (size_t)npairs(req) / lead;
+    int64_t f = 0;
+    for (size_t r = 0; r < rows; ++r)
+        for (size_t i = 0; i < cnt; ++i)
+            f += status[(size_t)sh.off[PAIRS] + r * lead + i] != 0;
+    *failures = f;
+    return HHMM_OK;
+}
+
+/* HHMM_DEVICE_SET: one host thread per shard, each on its device of the set
+ * (hhmm_init / hhmm_init_devices), writing its slices of the caller's
+ * outputs; the first failing shard's error is returned (device
+ * set {GPU 0..7}, one host thread per GPU; §8e: contiguous series ranges). */
+static hhmm_status run_sharded(const hhmm_request *req, hhmm_result *res)
+{
+    std::vector<int> devs;
+    {
+        std::lock_guard<std::mutex> g(devset().mu);
+        devs = devset().devs.empty() ? std::vector<int>{0} : devset().devs;
+    }
+    const std::vector<Shard> shards = make_shards(req, (int)devs.size());
+    const int64_t P = npairs(req);
+    std::vector<int32_t> status((size_t)P, 0);
+    std::vector<hhmm_status> st(shards.size(), HHMM_OK);
+    std::vector<std::string> msg(shards.size());
+    std::vector<int64_t> fails(shards.size(), 0);
+    auto work = [&](size_t i) {
+        hipError_t e = hipSetDevice(devs[i]);
+        if (e != hipSuccess) {
+            st[i] = hip_fail(e, "hipSetDevice");
+        } else {
+            st[i] = run_on_device(req, res, shards[i], status.data(), &fails[i]);
+        }
+        if (st[i] != HHMM_OK)
+            msg[i] = hhmm_last_error(); /* thread-local: carried to the caller's thread */
+    };
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < shards.size(); ++i)
+        th.emplace_back(work, i);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    work(0);
+    for (auto &t : th)
+        t.join();
+    (void)hipSetDevice(cur);
+    for (size_t i = 0; i < shards.size(); ++i)
+        if (st[i] != HHMM_OK) {
+            set_error("shard %zu (device %d): %s", i, devs[i], msg[i].c_str());
+            return st[i];
+        }
+    if (res->pair_status)
+        memcpy(res->pair_status, status.data(), (size_t)P * sizeof(int32_t));
+    int64_t failures = 0;
+    for (int64_t f : fails)
+        failures += f;
+    if (failures) {
+        set_error("%lld pair(s) hit an unset Viterbi back-pointer (Stan would throw)", (long long)failures);
+        return HHMM_WARN_PAIR_FAILURES;
+    }
+    return HHMM_OK;
+}
+
 } // namespace hhmm
 
 using namespace hhmm;
@@ -517,15 +769,14 @@ hhmm_status hhmm_init(int ndev)
         set_error("%d devices requested, %d visible", ndev, n);
         return HHMM_ERR_NO_DEVICE;
     }
+    std::vector<int> d;
     for (int i = 0; i < (ndev > 0 ? ndev : 1); ++i) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, i) != hipSuccess)
-            return hip_fail(hipGetLastError(), "hipGetDeviceProperties");
-        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-            set_error("device %d is %s, this build targets gfx950", i, prop.gcnArchName);
-            return HHMM_ERR_NO_DEVICE;
-        }
+        if ((s = check_arch(i)) != HHMM_OK)
+            return s;
+        d.push_back(i);
     }
+    std::lock_guard<std::mutex> g(devset().mu);
+    devset().devs = d; /* HHMM_DEVICE_SET shards over devices 0 .. ndev-1 */
     return HHMM_OK;
 }
 
@@ -583,6 +834,8 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
     }
     if ((s = check_device()) != HHMM_OK)
         return s;
+    if (req->device == HHMM_DEVICE_SET)
+        return run_sharded(req, res);
     int dev = req->device;
     if (dev < 0) {
         if (hipGetDevice(&dev) != hipSuccess)
@@ -591,104 +844,54 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
     hipError_t e = hipSetDevice(dev);
     if (e != hipSuccess)
         return hip_fail(e, "hipSetDevice");
-
     const int64_t P = npairs(req);
-    hhmm_request dreq = *req;
-    hhmm_result dres = *res;
-    /* pair_status is always produced on the device to decide the return code */
-    std::vector<int32_t> status_host;
-    int32_t *status_user = res->pair_status;
-    dres.pair_status = nullptr;
-
-    std::vector<ArrayDesc> arrays;
-    describe(req, res, &dreq, &dres, arrays);
-    const bool ragged = req->data.T != nullptr || req->data.T_oos != nullptr;
-
-    std::vector<void *> owned;
-    auto cleanup = [&]() {
-        for (void *p : owned)
-            pool_put(p);
-    };
-    for (auto &a : arrays) {
-        void *dp = pool_get(dev, a.elems * a.esize);
-        if (!dp) {
-            cleanup();
-            set_error("device allocation of %zu bytes failed", a.elems * a.esize);
-            return HHMM_ERR_OUT_OF_MEMORY;
-        }
-        owned.push_back(dp);
-        *a.dev_slot = dp;
-        /* inputs always; outputs too when padded steps must round-trip untouched */
-        if (!a.output || ragged) {
-            e = hipMemcpy(dp, a.host, a.elems * a.esize, hipMemcpyHostToDevice);
-            if (e != hipSuccess) {
-                cleanup();
-                return hip_fail(e, "hipMemcpy H2D");
-            }
-        }
-    }
-    void *dstatus = pool_get(dev, (size_t)P * sizeof(int32_t));
-    if (!dstatus) {
-        cleanup();
-        set_error("device allocation failed (pair_status)");
-        return HHMM_ERR_OUT_OF_MEMORY;
-    }
-    owned.push_back(dstatus);
-    (void)hipMemset(dstatus, 0, (size_t)P * sizeof(int32_t));
-    dres.pair_status = (int32_t *)dstatus;
-
-    size_t wsb = workspace_bytes(req->model, req->data.K, req->data.L, req->data.T_max, req->data.T_oos_max, P, req->outputs,
-                                 (uint32_t)req->flags, req->data.n_series, req->pairing);
-    void *ws = pool_get(dev, wsb);
-    if (!ws) {
-        cleanup();
-        set_error("workspace allocation of %zu bytes failed", wsb);
-        return HHMM_ERR_OUT_OF_MEMORY;
-    }
-    owned.push_back(ws);
-
-    s = launch_all(&dreq, &dres, P, ws, nullptr);
-    if (s != HHMM_OK) {
-        /* a failed launch may follow one that is still running: drain this
-         * request's streams before its pooled buffers can be handed to another
-         * request; a sticky device error from an earlier fault is reported
-         * beside the launch error instead of being buried under it */
-        e = sync_request(nullptr);
-        cleanup();
-        if (e != hipSuccess) {
-            std::string first = hhmm_last_error();
-            set_error("%s; draining the request's streams then failed: %s", first.c_str(), hipGetErrorString(e));
-        }
-        return s;
-    }
-    e = sync_request(nullptr);
-    if (e != hipSuccess) {
-        cleanup();
-        return hip_fail(e, "kernel execution");
-    }
-    for (auto &a : arrays) {
-        if (!a.output)
-            continue;
-        e = hipMemcpy((void *)a.host, *a.dev_slot, a.elems * a.esize, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) {
-            cleanup();
-            return hip_fail(e, "hipMemcpy D2H");
-        }
-    }
-    status_host.resize((size_t)P);
-    e = hipMemcpy(status_host.data(), dstatus, (size_t)P * sizeof(int32_t), hipMemcpyDeviceToHost);
-    cleanup();
-    if (e != hipSuccess)
-        return hip_fail(e, "hipMemcpy D2H (status)");
+    std::vector<int32_t> status((size_t)P, 0);
     int64_t failures = 0;
-    for (int64_t p = 0; p < P; ++p)
-        failures += status_host[(size_t)p] != 0;
-    if (status_user)
-        memcpy(status_user, status_host.data(), (size_t)P * sizeof(int32_t));
+    s = run_on_device(req, res, whole_shard(req), status.data(), &failures);
+    if (s != HHMM_OK)
+        return s;
+    if (res->pair_status)
+        memcpy(res->pair_status, status.data(), (size_t)P * sizeof(int32_t));
     if (failures) {
         set_error("%lld pair(s) hit an unset Viterbi back-pointer (Stan would throw)", (long long)failures);
         return HHMM_WARN_PAIR_FAILURES;
     }
+    return HHMM_OK;
+}
+
+int hhmm_device_set(int32_t *ordinals, int capacity)
+{
+    std::lock_guard<std::mutex> g(devset().mu);
+    const std::vector<int> d = devset().devs.empty() ? std::vector<int>{0} : devset().devs;
+    for (int i = 0; i < (int)d.size() && i < capacity; ++i)
+        if (ordinals)
+            ordinals[i] = d[(size_t)i];
+    return (int)d.size();
+}
+
+hhmm_status hhmm_init_devices(const int32_t *ordinals, int n)
+{
+    hhmm_status s = check_device();
+    if (s != HHMM_OK)
+        return s;
+    if (!ordinals || n < 1) {
+        set_error("hhmm_init_devices needs n >= 1 ordinals");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    int vis = 0;
+    (void)hipGetDeviceCount(&vis);
+    std::vector<int> d;
+    for (int i = 0; i < n; ++i) {
+        if (ordinals[i] < 0 || ordinals[i] >= vis) {
+            set_error("device ordinal %d not visible (%d devices)", ordinals[i], vis);
+            return HHMM_ERR_NO_DEVICE;
+        }
+        if ((s = check_arch(ordinals[i])) != HHMM_OK)
+            return s;
+        d.push_back(ordinals[i]);
+    }
+    std::lock_guard<std::mutex> g(devset().mu);
+    devset().devs = d;
     return HHMM_OK;
 }
 

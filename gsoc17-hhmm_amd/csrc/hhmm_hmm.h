@@ -1579,7 +1579,7 @@ __global__ void __launch_bounds__(kBlock) fbv_kernel(const DevArgs a)
  * A wave holding a pair without the renormalisation bound lists itself after
  * phase 1 (zstar_T parked in zstar[T-1]) for vfb_dense_kernel. */
 #ifndef HHMM_VFB_DEFAULT
-#define HHMM_VFB_DEFAULT 0 /* the phased sweep for the C2 request without flags */
+#define HHMM_VFB_DEFAULT 1 /* the phased sweep for the C2 request without flags */
 #endif
 template <int MODEL, int K>
 __device__ __forceinline__ uint32_t pack_chunk(const Obs (&cur)[8])

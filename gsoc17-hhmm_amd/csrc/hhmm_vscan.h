@@ -62,10 +62,13 @@ constexpr int32_t kVsTie = 1 << 30;     /* vs_k: a grid rounding tie inside the 
  * 31k instructions to ~125 VGPRs: the first out-of-line version launched the
  * tie kernel over every (pair, chunk, parity) lane and cost more at C5 than the
  * occupancy gained (14.17 against 13.78 ms, profiles/r02zl_ab_c5.log); the grid
- * pass now appends its tie chunks to a list (vs_tl: an atomic count, then
- * lane ids g = p + P c) and the tie kernel walks only that list (round 3). */
+ * pass can append its tie chunks to a list (vs_tl: an atomic count, then
+ * lane ids g = p + P c) for the tie kernel to walk (round 3), but that too
+ * measured slower at C5: 15.21 against 13.52 ms inline, interleaved on one box
+ * (profiles/r03j_ab_c5.log).  Inline stays the default; Gaussian models
+ * always use the list. */
 #ifndef HHMM_VS_TIE_INLINE
-#define HHMM_VS_TIE_INLINE 0
+#define HHMM_VS_TIE_INLINE 1
 #endif
 constexpr int32_t kVsNoGrid = -(1 << 20); /* vs_k: no finite magnitude estimate */
 constexpr int32_t kVsSeq = -(1 << 21);    /* vs_k after the exact scan: the chunk was decoded step by step */

@@ -49,6 +49,7 @@ FLAG_FB_SPLIT = 1 << 16
 FLAG_LKM_MFMA = 1 << 17
 FLAG_VFB = 1 << 18
 FLAG_VFB_OFF = 1 << 19
+DEVICE_SET = -2  # hhmm_request.device: shard over the device set (HHMM_DEVICE_SET)
 
 
 def flag_scan_chunk_log2(n):
@@ -230,6 +231,11 @@ def declare(lib):
     lib.hhmm_init.argtypes = [C.c_int]
     lib.hhmm_init.restype = C.c_int
     lib.hhmm_shutdown.restype = C.c_int
+    if hasattr(lib, "hhmm_init_devices"):  # absent from libraries built before the device set (A/B variants)
+        lib.hhmm_init_devices.argtypes = [C.POINTER(C.c_int32), C.c_int]
+        lib.hhmm_init_devices.restype = C.c_int
+        lib.hhmm_device_set.argtypes = [C.POINTER(C.c_int32), C.c_int]
+        lib.hhmm_device_set.restype = C.c_int
     lib.hhmm_run.argtypes = [RP, SP]
     lib.hhmm_run.restype = C.c_int
     lib.hhmm_workspace_size.argtypes = [RP, C.POINTER(C.c_size_t)]

@@ -239,7 +239,7 @@ typedef struct hhmm_request {
     hhmm_data data;
     hhmm_draws draws;
     const double *ffbs_u;      /* [P, T_max] uniforms in (0,1) for HHMM_OUT_FFBS */
-    int32_t device;            /* HIP device ordinal for hhmm_run; -1 = current */
+    int32_t device;            /* HIP device ordinal for hhmm_run; -1 = current; HHMM_DEVICE_SET = the set */
     int32_t flags;             /* HHMM_FLAG_* (0 = defaults) */
     const double *hat_rand;    /* [P, T_max, 3] for HHMM_OUT_HATZ/HATL/HATX: uniform (hatz),
                                 * uniform (hatl), standard normal (hatx) at p + P*(t + T_max*c) */
@@ -282,8 +282,20 @@ int64_t hhmm_num_pairs(const hhmm_request *req);
  * host data).  hhmm_run calls it; exposed for the R shim and tests. */
 hhmm_status hhmm_validate(const hhmm_request *req, const hhmm_result *res, int host_pointers);
 
-/* Optional explicit init: verifies that ndev gfx950 devices are visible. */
+/* hhmm_request.device: shard the request over the device set, one host thread
+ * per device; each writes its slice of the caller's outputs (hhmm_run only). */
+#define HHMM_DEVICE_SET (-2)
+
+/* Explicit init: verifies that ndev gfx950 devices are visible and makes
+ * devices 0 .. ndev-1 the device set. */
 hhmm_status hhmm_init(int ndev);
+
+/* The device set as explicit ordinals (a device may repeat: two shards on one
+ * GPU run in two threads).  Replaces the set hhmm_init made. */
+hhmm_status hhmm_init_devices(const int32_t *ordinals, int n);
+
+/* Writes up to `capacity` ordinals of the device set; returns its size. */
+int hhmm_device_set(int32_t *ordinals, int capacity);
 
 /* Releases the device pool (R finaliser / process exit). */
 hhmm_status hhmm_shutdown(void);

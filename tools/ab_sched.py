@@ -3,6 +3,10 @@
 device with one library (bench.DeviceRun's prepared requests):
 
   python tools/ab_sched.py [--lib path/to/libhhmm.so] [--rounds 7] [--steps 3] two vfb fused split
+  python tools/ab_sched.py --lib new=lib/libhhmm.so --lib base=lib/variants/libhhmm_base.so new:vfb base:vfb
+
+(a schedule may name its library: NAME:schedule with --lib NAME=path; a bare
+schedule runs on the first library)
 
 Rounds run A B C A B C ...; each round times `steps` back-to-back requests
 with HIP events on the launch stream (ms per request: median and min over
@@ -27,24 +31,34 @@ import hhmm_amd  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("schedules", nargs="+")
-    ap.add_argument("--lib", default=None)
+    ap.add_argument("--lib", action="append", default=[])
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=1_000_000)
     ap.add_argument("--T", type=int, default=1000)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    lib = hhmm_amd.load_library(a.lib) if a.lib else hhmm_amd.load_library()
-    assert lib.hhmm_init(1) == 0
+    libs = {}
+    for spec in a.lib or ["default=" + str(hhmm_amd.api.LIB_PATH)]:
+        name, path = spec.split("=", 1)
+        libs[name] = hhmm_amd.load_library(path)
+        assert libs[name].hhmm_init(1) == 0
+    first = next(iter(libs))
     x, draws = bench.make_batch(a.pairs, a.T, 9000, dev)
-    run = bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev)
+    runs = {n: bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev) for n, lib in libs.items()}
+
+    def split(nm):
+        return nm.split(":", 1) if ":" in nm else (first, nm)
+
     s0 = torch.cuda.current_stream()
     ref = None
     same = {}
     for nm in a.schedules:
+        ln, sc = split(nm)
+        run = runs[ln]
         for v in run.out.values():
             v.zero_()
-        run.launch(nm)
+        run.launch(sc)
         torch.cuda.synchronize()
         snap = {k: v.clone() for k, v in run.out.items()}
         if ref is None:
@@ -57,8 +71,9 @@ def main():
         for nm in a.schedules:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s0)
+            ln, sc = split(nm)
             for _ in range(a.steps):
-                run.launch(nm)
+                runs[ln].launch(sc)
             e1.record(s0)
             torch.cuda.synchronize()
             times[nm].append(e0.elapsed_time(e1) / a.steps)
