@@ -895,6 +895,96 @@ hhmm_status hhmm_init_devices(const int32_t *ordinals, int n)
     return HHMM_OK;
 }
 
+/* ---- one series split over ranks along T (include/hhmm.h hhmm_segment) ---- */
+static hhmm_status segment_check(const hhmm_request *req, const hhmm_segment *seg, hhmm_request &r2)
+{
+    if (!req || !seg) {
+        set_error("NULL argument");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    const int m = req->model;
+    if (!(m == HHMM_MODEL_HMM_GAUSS || m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ||
+          m == HHMM_MODEL_TAYAL) ||
+        req->data.K > kMaxK) {
+        set_error("segment windows: the HMM family at K <= %d (hmm, hmm-multinom, semisup, tayal)", kMaxK);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const uint32_t ok = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
+    if (req->outputs & ~ok) {
+        set_error("segment windows: outputs 0x%x have no segment form (loglik, alpha_tk, beta_tk, ungamma_tk, "
+                  "gamma_tk only; the Viterbi and FFBS stay sequential per pair)", req->outputs & ~ok);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    if (req->data.T) {
+        set_error("segment windows: every series spans the whole window (data.T must be NULL)");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    if (req->abi_version != HHMM_ABI_VERSION || npairs(req) < 1 || req->data.T_max < 1 || req->data.K < 1 ||
+        (is_discrete(m) && (req->data.L < 1 || !req->data.x_int)) || (m == HHMM_MODEL_HMM_GAUSS && !req->data.x_real)) {
+        set_error("segment windows: malformed request (abi, pairs, T_max, K, L or observations)");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    r2 = *req;
+    r2.flags = (req->flags & ~(int32_t)HHMM_FLAG_SCAN_OFF) | (int32_t)HHMM_FLAG_SCAN_FORCE;
+    return HHMM_OK;
+}
+
+hhmm_status hhmm_segment_workspace_size(const hhmm_request *req, size_t *bytes)
+{
+    hhmm_segment dummy{1, 1, nullptr, nullptr, nullptr};
+    hhmm_request r2;
+    hhmm_status s = segment_check(req, &dummy, r2);
+    if (s != HHMM_OK)
+        return s;
+    return hhmm_workspace_size(&r2, bytes);
+}
+
+static hhmm_status segment_run(const hhmm_request *req, hhmm_result *res, const hhmm_segment *seg, void *ws,
+                               size_t wsb, void *stream, int phase)
+{
+    hhmm_request r2;
+    hhmm_status s = segment_check(req, seg, r2);
+    if (s != HHMM_OK)
+        return s;
+    hhmm_result empty;
+    memset(&empty, 0, sizeof(empty));
+    hhmm_result *rr = res ? res : &empty;
+    if (phase == 1) {
+        if (!seg->summary) {
+            set_error("segment summary: seg->summary is NULL");
+            return HHMM_ERR_INVALID_ARGUMENT;
+        }
+    } else {
+        if ((!seg->first && !seg->enter) || (!seg->last && !seg->leave)) {
+            set_error("segment finish: a window that is not first needs enter, one that is not last needs leave");
+            return HHMM_ERR_INVALID_ARGUMENT;
+        }
+        if ((s = validate(&r2, rr, false)) != HHMM_OK)
+            return s;
+    }
+    if ((s = check_device()) != HHMM_OK)
+        return s;
+    size_t need = 0;
+    hhmm_workspace_size(&r2, &need);
+    if (wsb < need || !ws) {
+        set_error("workspace of %zu bytes < %zu required (hhmm_segment_workspace_size)", wsb, need);
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    return launch_all(&r2, rr, npairs(&r2), ws, (hipStream_t)stream, seg, phase);
+}
+
+hhmm_status hhmm_segment_summary_device(const hhmm_request *req, const hhmm_segment *seg, void *workspace,
+                                        size_t workspace_bytes_, void *stream)
+{
+    return segment_run(req, nullptr, seg, workspace, workspace_bytes_, stream, 1);
+}
+
+hhmm_status hhmm_segment_finish_device(const hhmm_request *req, hhmm_result *res, const hhmm_segment *seg,
+                                       void *workspace, size_t workspace_bytes_, void *stream)
+{
+    return segment_run(req, res, seg, workspace, workspace_bytes_, stream, 2);
+}
+
 hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n)
 {
     hhmm_status s = check_device();

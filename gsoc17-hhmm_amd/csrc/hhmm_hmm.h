@@ -630,6 +630,7 @@ struct FbLane {
     int cb;      /* t0 / C: first checkpoint row */
     int64_t q;   /* checkpoint column (the pair, or the scan lane) */
     int64_t Qs;  /* checkpoint row stride */
+    bool noinit = false; /* step 0 is not the series' first (a segment window's chunk 0) */
 };
 
 /* One forward chunk [t0, t0+C).  FULLC: every lane of the wave has all C
@@ -647,7 +648,7 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
         emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, (u + 1 < C) ? cur[u + 1 < C ? u + 1 : 0] : nxt0,
                                            enx);
         if (FULLC || t < ln.Tp) {
-            if (u == 0 && c == 0) {
+            if (u == 0 && c == 0 && !ln.noinit) {
                 fwd_init<MODEL, K>(al, ln.pp, ecur, cur[0], lsc, ex);
             } else {
                 lsc += ecur.m;
@@ -2453,7 +2454,7 @@ __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
     int fex = 0, qex = 0;
     double lsc = 0.0;
     int tb = t0;
-    if (c == 0) { /* chunk 0 enters from the model's init vector f_0 (every row) */
+    if (c == 0 && !a.seg_nofirst) { /* chunk 0 enters from the model's init vector f_0 (every row) */
         const Obs o0 = load_obs<MODEL, AUX>(sp, 0);
         Em<K> em;
         emit_prob<MODEL, K>(pp, slab, a.L, o0, em);
@@ -2555,10 +2556,40 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
     auto mx = [&](int c, int f) { return a.sc_mx[p + a.P * (int64_t)(c * 3 + f)]; };
 
     double f[K];
+    double sc;
+    if (!a.seg_nofirst) {
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-        f[j] = a.sc_mf[p + a.P * (int64_t)j];
-    double sc = mx(0, 1) + kLn2 * mx(0, 0);
+        for (int j = 0; j < K; ++j)
+            f[j] = a.sc_mf[p + a.P * (int64_t)j];
+        sc = mx(0, 1) + kLn2 * mx(0, 0);
+    } else {
+        /* a segment window: chunk 0 enters from the caller's state, which then
+         * goes through chunk 0's product like every later chunk */
+        double e[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            e[j] = a.seg_enter[p + a.P * (int64_t)j];
+        const double esc = a.seg_enter[p + a.P * (int64_t)K];
+        if (l0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                a.sc_st[p + a.P * (int64_t)k] = e[k];
+            a.sc_sl[p] = esc;
+        }
+        double m0[K][K];
+        load_mat<K>(a.sc_mf, a, 0, p, m0);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            double acc = e[0] * m0[0][j];
+#pragma unroll
+            for (int ii = 1; ii < K; ++ii)
+                acc = fma(e[ii], m0[ii][j], acc);
+            f[j] = acc;
+        }
+        int e2 = 0;
+        renorm<K>(f, e2);
+        sc = esc + mx(0, 1) + kLn2 * (mx(0, 0) + e2);
+    }
     double m[K][K], x3[3];
     scan_fetch<K>(a.sc_mf, a, p, min(1 + lane, max(ncp - 1, 0)), m, x3);
     for (int cb = 1; cb < ncp; cb += 64) {
@@ -2592,19 +2623,21 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
         }
         __syncthreads();
     }
-    if (l0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+    if (l0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
         a.loglik[p] = log(vsum<K>(f)) + sc;
     if constexpr (BWD) {
         double b[K];
+        /* beta at the last step: unbeta_tk[T] = 1 (Q1), or a segment window's
+         * beta leaving it (the caller's) */
+        double bsc = a.seg_nolast ? a.seg_leave[p + a.P * (int64_t)K] : 0.0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            b[k] = 1.0; /* unbeta_tk[T] = 1 (Q1) */
+            b[k] = a.seg_nolast ? a.seg_leave[p + a.P * (int64_t)k] : 1.0;
             if (l0)
                 a.sc_be[p + a.P * (int64_t)((ncp - 1) * K + k)] = b[k];
         }
         if (l0)
-            a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = 0.0;
-        double bsc = 0.0;
+            a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = bsc;
         /* blocks of 64 chunks from the top down: lane l holds chunk top - l */
         scan_fetch<K>(a.sc_qb, a, p, min(max(ncp - 1 - lane, 1), ncp - 1), m, x3);
         for (int ct = ncp - 1; ct >= 1; ct -= 64) {
@@ -2638,6 +2671,78 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
             __syncthreads();
         }
     }
+}
+
+/* Segment summary (hhmm_segment): one lane per pair multiplies its window's
+ * chunk products in order, SF = F_0 F_1 ... and SQ = Q_0 Q_1 ..., each
+ * renormalised by an exact power of two after every product, the exponents
+ * and the Gaussian log scales summed alongside (the K x K
+ * summary a rank contributes to the all-gather). */
+template <int K>
+__device__ __forceinline__ void mat_mul_acc(double (&S)[K][K], const double (&M)[K][K])
+{
+    double R[K][K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            double acc = S[i][0] * M[0][j];
+#pragma unroll
+            for (int l = 1; l < K; ++l)
+                acc = fma(S[i][l], M[l][j], acc);
+            R[i][j] = acc;
+        }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            S[i][j] = R[i][j];
+}
+
+template <int MODEL, int K, bool BWD>
+__global__ void __launch_bounds__(kBlock) seg_summary_kernel(const DevArgs a)
+{
+    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int ncp = (pair_len(a, n) + a.scan_cl - 1) / a.scan_cl;
+    double SF[K][K], SQ[K][K], M[K][K];
+    load_mat<K>(a.sc_mf, a, 0, p, SF);
+    if constexpr (BWD)
+        load_mat<K>(a.sc_qb, a, 0, p, SQ);
+    double fex = a.sc_mx[p], lsc = a.sc_mx[p + a.P], qex = a.sc_mx[p + 2 * a.P];
+    for (int c = 1; c < ncp; ++c) {
+        int e = 0;
+        load_mat<K>(a.sc_mf, a, c, p, M);
+        mat_mul_acc<K>(SF, M);
+        renorm_mat<K>(SF, e);
+        fex += a.sc_mx[p + a.P * (int64_t)(c * 3 + 0)] + e;
+        lsc += a.sc_mx[p + a.P * (int64_t)(c * 3 + 1)];
+        if constexpr (BWD) {
+            e = 0;
+            load_mat<K>(a.sc_qb, a, c, p, M);
+            mat_mul_acc<K>(SQ, M);
+            renorm_mat<K>(SQ, e);
+            qex += a.sc_mx[p + a.P * (int64_t)(c * 3 + 2)] + e;
+        }
+    }
+    if constexpr (!BWD) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                SQ[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            a.seg_sum[p + a.P * (int64_t)(i * K + j)] = SF[i][j];
+            a.seg_sum[p + a.P * (int64_t)(K * K + i * K + j)] = SQ[i][j];
+        }
+    a.seg_sum[p + a.P * (int64_t)(2 * K * K + 0)] = fex;
+    a.seg_sum[p + a.P * (int64_t)(2 * K * K + 1)] = lsc;
+    a.seg_sum[p + a.P * (int64_t)(2 * K * K + 2)] = qex;
 }
 
 /* Phase 3: the forward-backward sweep of one (pair, T-chunk). */
@@ -2676,16 +2781,19 @@ __global__ void __launch_bounds__(kBlock) fb_scan_kernel(const DevArgs a)
         fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
     const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
     const bool live = ln.t0 < Tpair;
+    /* a segment window's chunk 0 enters from the state scan_bound_kernel stored */
+    const bool entered = c > 0 || a.seg_nofirst;
+    ln.noinit = a.seg_nofirst != 0;
     double al[K], be[K];
     double lsa = 0.0, lsb = 0.0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        al[k] = (c > 0 && live) ? a.sc_st[p + a.P * (int64_t)(c * K + k)] : 0.0;
+        al[k] = (entered && live) ? a.sc_st[p + a.P * (int64_t)(c * K + k)] : 0.0;
         be[k] = 1.0;
         if (fb_base(MODE) != FB_FWD && live)
             be[k] = a.sc_be[p + a.P * (int64_t)(c * K + k)];
     }
-    if (c > 0 && live)
+    if (entered && live)
         lsa = a.sc_sl[p + a.P * (int64_t)c];
     if (fb_base(MODE) != FB_FWD && live)
         lsb = a.sc_bl[p + a.P * (int64_t)c];
@@ -2974,12 +3082,68 @@ static hhmm_status launch_split(const DevArgs &a, hipStream_t st)
     return join_stream(st, vs);
 }
 
+/* The two calls of a segment window (hhmm_segment; the T-scan of
+ * launch_fb_scan split at its exchange point). */
+template <int MODEL, int K>
+static hhmm_status launch_segment(const DevArgs &a, hipStream_t st)
+{
+    LaunchShape s;
+    if (!shape_for(a, ModelTraits<MODEL>::kDiscrete, s)) {
+        set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    const bool bwd = needs_backward(MODEL, a.outputs);
+    if (a.seg_phase == 1) {
+        const int64_t G = a.P * (int64_t)a.scan_nc;
+        const dim3 gridG((unsigned)((G + s.block.x - 1) / s.block.x));
+        const dim3 gridP((unsigned)((a.P + kBlock - 1) / kBlock));
+        if (bwd) {
+            hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, true>), gridG, s.block, s.lds, st, a);
+            hipLaunchKernelGGL((seg_summary_kernel<MODEL, K, true>), gridP, dim3(kBlock), 0, st, a);
+        } else {
+            hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, false>), gridG, s.block, s.lds, st, a);
+            hipLaunchKernelGGL((seg_summary_kernel<MODEL, K, false>), gridP, dim3(kBlock), 0, st, a);
+        }
+    } else {
+        const int64_t G3 = scan_lanes_per_chunk(a.P) * (int64_t)a.scan_nc;
+        const dim3 gridG3((unsigned)((G3 + s.block.x - 1) / s.block.x));
+        const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
+        if (bwd) {
+            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64),
+                               64 * scan_row<K>() * sizeof(double), st, a);
+            if (a.outputs & extra)
+                hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
+            else
+                hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_GAMMA>), gridG3, s.block, s.lds, st, a);
+        } else {
+            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64),
+                               64 * scan_row<K>() * sizeof(double), st, a);
+            if (a.outputs & (HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA))
+                hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
+        }
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("segment launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
 template <int MODEL, int K>
 static hhmm_status run_model_k(const DevArgs &a, const hhmm_request *req, const hhmm_result *res,
                                hipStream_t st)
 {
     hhmm_status s = HHMM_OK;
     const uint32_t out = a.outputs;
+    if (a.seg_phase) {
+        if constexpr (MODEL == HHMM_MODEL_TAYAL_LITE) {
+            set_error("segment windows: tayal-lite has no backward pass to split (use hhmm-tayal2009)");
+            return HHMM_ERR_UNSUPPORTED;
+        } else {
+            return launch_segment<MODEL, K>(a, st);
+        }
+    }
     if (MODEL == HHMM_MODEL_TAYAL_LITE) {
         /* in-sample forward: alpha_tk / unalpha_tk / loglik (hhmm-tayal2009-lite.stan:50-92) */
         if (out & (HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA)) {

@@ -80,6 +80,13 @@ struct DevArgs {
     int32_t *vs_fail;   /* [P]          a replayed chunk disagreed: decode again sequentially */
     int32_t *vs_tl;     /* [1 + P*nc]   chunks with a grid rounding tie: count, then p + P c */
     const int32_t *vs_redo; /* state-parallel decoder: only pairs with vs_redo[p] != 0 (null: all) */
+    /* one time window of a series split over ranks (hhmm_segment; 0: a whole series) */
+    int32_t seg_phase;      /* 1: summary call, 2: finish call */
+    int32_t seg_nofirst;    /* the window does not start at t = 1: chunk 0 enters from seg_enter */
+    int32_t seg_nolast;     /* the window does not end at T: beta leaves as seg_leave, no loglik */
+    double *seg_sum;        /* [2K^2 + 3][P] */
+    const double *seg_enter;/* [K + 1][P] */
+    const double *seg_leave;/* [K + 1][P] */
 };
 
 /* Phase-3 lanes of the T-scan per T-chunk: P rounded up to whole waves. */
@@ -122,8 +129,8 @@ size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, u
 void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags);
 
 /* Launches every kernel the request needs on `stream` (device pointers). */
-hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws,
-                       hipStream_t stream);
+hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws, hipStream_t st,
+                       const hhmm_segment *seg = nullptr, int seg_phase = 0);
 
 /* HMM family, one translation unit per model / K range (hhmm_m_*.hip). */
 hhmm_status run_gauss_lo(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);

@@ -379,11 +379,23 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
     return a;
 }
 
-hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws,
-                       hipStream_t st)
+hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws, hipStream_t st,
+                       const hhmm_segment *seg, int seg_phase)
 {
     DevArgs a = make_args(req, res, P);
     bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max, (uint32_t)req->flags);
+    if (seg) {
+        a.seg_phase = seg_phase;
+        a.seg_nofirst = !seg->first;
+        a.seg_nolast = !seg->last;
+        a.seg_sum = seg->summary;
+        a.seg_enter = seg->enter;
+        a.seg_leave = seg->leave;
+        if (a.scan_cl <= 0) {
+            set_error("segment: the request has no T-scan plan (HMM family, K <= 8, probability-space outputs)");
+            return HHMM_ERR_UNSUPPORTED;
+        }
+    }
     const bool lo = a.K <= 4;
     if (a.K > kMaxK) {
         if (req->model != HHMM_MODEL_HMM_GAUSS && req->model != HHMM_MODEL_HMM_MULTINOM) {

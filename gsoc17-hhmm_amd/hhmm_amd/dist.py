@@ -147,3 +147,41 @@ def _all_max(v, dev, group):
     t = torch.tensor([v], dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return int(t.item())
+
+
+def gqs_tsplit(model, data, draws, pars, group=None, pairing="grid", lib=None):
+    """One batch whose series are split along T over the ranks (SURVEY.md §8e:
+    a single very long series -- C5's shape when pairs are few).  Rank r holds
+    the steps [t0, t1) of every series (segment.windows); it computes its
+    window's K x K summaries on its GPU (hhmm_segment_summary_device),
+    all-gathers them (2K^2 + 3 doubles per pair and rank -- RCCL over xGMI
+    under nccl), chains them into the state entering and beta leaving its
+    window, and finishes its window (phases 2-3 of the T-scan).
+
+    Returns (window, outputs, loglik): window = (t0, t1); outputs = the
+    window's requested [P, t1 - t0, ...] arrays (P-first, as api.PreparedRequest
+    lays them out); loglik = the whole series' log-likelihood per pair (every
+    rank computes it from the same gathered summaries)."""
+    import torch
+    import torch.distributed as dist
+
+    from . import api, segment
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    x = np.atleast_2d(np.asarray(data["x_t" if "x_t" in data else "x"]))
+    wins = segment.windows(x.shape[-1], world)
+    t0, t1 = wins[rank]
+    lib = lib or api.load_library()
+    win = segment.SegmentWindow(lib, model, segment.slice_time(data, t0, t1), draws,
+                                list(dict.fromkeys(["loglik"] + list(pars))), rank == 0, rank == world - 1,
+                                pairing)
+    s = win.summary()
+    torch.cuda.synchronize(win.dev)
+    dev = default_device(group)
+    s = s.to(dev)
+    gathered = [torch.empty_like(s) for _ in range(world)]
+    dist.all_gather(gathered, s, group=group)
+    enter, leave, loglik = segment.boundaries([g.cpu().numpy() for g in gathered], win.K)
+    out = win.finish(enter[rank], leave[rank])
+    return (t0, t1), out, loglik

@@ -312,6 +312,43 @@ hhmm_status hhmm_workspace_size(const hhmm_request *req, size_t *bytes);
 hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res,
                             void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---- One series split over ranks along T -----------------
+ * A rank holds one time window [t0, t1) of every pair's series: the request's
+ * data arrays hold the window's steps only ([N, T_window], T = NULL: every
+ * series spans the whole window), and its scan runs in two calls on the same
+ * workspace (hhmm_segment_workspace_size) and stream:
+ *   hhmm_segment_summary_device  the window's chunk products (the T-scan's
+ *       phase 1) and their ordered products: per pair the forward product SF
+ *       (K x K, row vector times SF maps the state entering the window to the
+ *       state leaving it; the first window's rows all hold the state leaving
+ *       it), the backward product SQ (SQ times beta leaving the window is
+ *       beta entering it), their power-of-two exponents and the Gaussian log
+ *       scale: summary[p + P*f], f = 0 .. 2K^2 + 2 in the order
+ *       SF (row-major), SQ (row-major), SF exponent, log scale, SQ exponent.
+ *   hhmm_segment_finish_device  given the forward state entering the window
+ *       (`enter`, [P, K + 1]: K probabilities up to scale, then their log
+ *       scale; unused for the first window) and beta leaving it (`leave`,
+ *       likewise; unused for the last window), the scan's phases 2 and 3:
+ *       loglik (last window only), alpha_tk, beta_tk, ungamma_tk, gamma_tk of
+ *       the window's steps.
+ * The caller all-gathers the ranks' summaries (K x K per pair: 2K^2 + 3
+ * doubles) and chains them (hhmm_amd.segment.boundaries; dist.gqs_tsplit).
+ * HMM family at K <= 8 (hmm, hmm-multinom, semisup, tayal); the Viterbi and
+ * FFBS stay sequential per pair (no segment form). */
+typedef struct hhmm_segment {
+    int32_t first;           /* the window starts at the series' first step */
+    int32_t last;            /* the window ends at the series' last step */
+    double *summary;         /* summary call: [P, 2K^2 + 3] out */
+    const double *enter;     /* finish call, first = 0: [P, K + 1] */
+    const double *leave;     /* finish call, last = 0: [P, K + 1] */
+} hhmm_segment;
+
+hhmm_status hhmm_segment_workspace_size(const hhmm_request *req, size_t *bytes);
+hhmm_status hhmm_segment_summary_device(const hhmm_request *req, const hhmm_segment *seg, void *workspace,
+                                        size_t workspace_bytes, void *stream);
+hhmm_status hhmm_segment_finish_device(const hhmm_request *req, hhmm_result *res, const hhmm_segment *seg,
+                                       void *workspace, size_t workspace_bytes, void *stream);
+
 /* Self-test hooks: the device's correctly rounded log / exp over n host
  * doubles (the transcendentals every exact Viterbi input goes through), and
  * the deterministic log / exp of the FFBS contract (hhmm_detmath.h). */

@@ -1,0 +1,116 @@
+"""GPU: one series split along T over ranks (include/hhmm.h hhmm_segment;
+SURVEY.md §8e "single very long series": each GPU scans its T-chunk, the K x K
+chunk summaries are all-gathered, each GPU fixes up its prefix).
+
+The windows' results, stitched along T, must equal the whole series: the
+engine's sequential sweep and the oracle (loglik from the chained summaries,
+alpha / beta / gamma per step) within tests/tolerances.py.  First in one
+process, window by window (R = 1, 2, 3, 5 windows of unequal length), then
+over two gloo ranks on the box's GPU through dist.gqs_tsplit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from hhmm_amd import synth
+from tolerances import compare
+
+pytestmark = pytest.mark.gpu
+
+PARS = ["loglik", "alpha_tk", "beta_tk", "gamma_tk"]
+
+
+def _windows_in_one_process(engine, model, data, draws, R, pars=PARS, pairing="grid"):
+    from hhmm_amd import segment
+    T = np.atleast_2d(data["x"]).shape[-1]
+    wins = segment.windows(T, R)
+    runs = [segment.SegmentWindow(engine, model, segment.slice_time(data, t0, t1), draws, pars, i == 0,
+                                  i == R - 1, pairing) for i, (t0, t1) in enumerate(wins)]
+    sums = [w.summary().cpu().numpy() for w in runs]
+    enter, leave, loglik = segment.boundaries(sums, runs[0].K)
+    outs = [w.finish(enter[i], leave[i]) for i, w in enumerate(runs)]
+    stitched = {k: np.concatenate([o[k] for o in outs], axis=1) for k in pars if k != "loglik"}
+    stitched["loglik"] = loglik
+    last = outs[-1]["loglik"]  # the last window's own loglik (phase 2 from its entering state)
+    return stitched, last
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 5])
+@pytest.mark.parametrize("model", ["hmm-multinom", "hmm", "hhmm-tayal2009", "hmm-multinom-semisup"])
+def test_segments_equal_the_whole_series(engine, oracle, model, R):
+    import hhmm_amd
+    # T = 1001: past ~1500 steps the Tayal masks drive alpha and beta onto
+    # different states (Q6) and gamma's smallest components (~1e-164) carry the
+    # T-scan's own ~1e-8 relative reassociation error, before they underflow to
+    # NaN in the reference's formula near t = 2000; the scan's
+    # own tests stop at T = 1000 for the same reason (tests/test_gpu_scan.py)
+    data, draws = synth.GENERATORS[model](N=2, S=3, T=1001)
+    got, last = _windows_in_one_process(engine, model, data, draws, R)
+    ref = oracle.gqs(model, data, draws, pars=PARS)
+    whole = hhmm_amd.gqs(model, data, draws, pars=PARS, lib=engine)
+    compare("loglik", got["loglik"], ref["loglik"])
+    compare("loglik", last, ref["loglik"])
+    for k in ("alpha_tk", "beta_tk", "gamma_tk"):
+        compare(k, got[k], whole[k])
+        compare(k, got[k], ref[k])
+
+
+def test_segments_long_series_few_pairs(engine, oracle):
+    """Few pairs, long T: 4 pairs of one series of 2e5 steps over 4 windows,
+    against the oracle."""
+    data, draws = synth.GENERATORS["hmm-multinom"](N=1, S=4, T=200_000)
+    got, _ = _windows_in_one_process(engine, "hmm-multinom", data, draws, 4, pars=["loglik", "gamma_tk"])
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=["loglik", "gamma_tk"])
+    compare("loglik", got["loglik"], ref["loglik"])
+    compare("gamma_tk", got["gamma_tk"], ref["gamma_tk"])
+
+
+def test_segment_rejects_viterbi_outputs(engine):
+    from hhmm_amd import segment
+    data, draws = synth.hmm_multinom(N=1, S=2, T=50)
+    with pytest.raises(ValueError, match="no segment form"):
+        segment.SegmentWindow(engine, "hmm-multinom", data, draws, ["loglik", "zstar_t"], True, True)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, out_dir):
+    import sys
+    import pathlib
+    repo = pathlib.Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(repo / "gsoc17-hhmm_amd")]
+    import torch
+    import torch.distributed as dist
+    from hhmm_amd import dist as hdist
+    torch.cuda.set_device(0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data, draws = synth.GENERATORS["hmm"](N=2, S=3, T=4000)
+        (t0, t1), out, loglik = hdist.gqs_tsplit("hmm", data, draws, ["loglik", "gamma_tk"])
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), t0=t0, t1=t1, gamma=out["gamma_tk"], loglik=loglik)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_gqs_tsplit(engine, oracle, tmp_path):
+    """dist.gqs_tsplit at world size 2 over gloo, both ranks on the box's GPU:
+    each rank's window of gamma and the loglik every rank chains from the
+    gathered summaries, against the oracle's whole series."""
+    port = _free_port()
+    mp.spawn(_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    data, draws = synth.GENERATORS["hmm"](N=2, S=3, T=4000)
+    ref = oracle.gqs("hmm", data, draws, pars=["loglik", "gamma_tk"])
+    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
+    assert int(parts[0]["t1"]) == int(parts[1]["t0"]) and int(parts[1]["t1"]) == 4000
+    compare("loglik", parts[0]["loglik"], ref["loglik"])
+    compare("loglik", parts[1]["loglik"], ref["loglik"])
+    gamma = np.concatenate([p["gamma"] for p in parts], axis=1)
+    compare("gamma_tk", gamma, ref["gamma_tk"])
