@@ -143,6 +143,8 @@ hhmm_status run_tayal(const DevArgs &a, const hhmm_request *req, const hhmm_resu
 hhmm_status run_tayal_lite(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);
 /* hmm / hmm-multinom at kMaxK < K <= kMaxKLarge (hhmm_m_large.hip) */
 hhmm_status run_large(const DevArgs &a, hipStream_t st);
+/* the IOHMM programs at kMaxK < K <= kMaxKLarge (hhmm_io_large.hip) */
+hhmm_status run_large_iohmm(const DevArgs &a, hipStream_t st);
 
 /* IOHMM family (iohmm-reg / -mix / -hmix / -hmix-lite), hhmm_iohmm.hip. */
 hhmm_status launch_iohmm(const DevArgs &a, hipStream_t stream);

@@ -231,6 +231,8 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
         }
         if (outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR))
             w.bp = take((size_t)P * K * (size_t)((Tmax + 15) & ~15));
+        if (is_iohmm_model(model) && (outputs & HHMM_OUT_UNBETA))
+            w.lam = take((size_t)Tmax * P * d);
         w.total = off + 256;
         return w;
     }
@@ -398,12 +400,14 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
     }
     const bool lo = a.K <= 4;
     if (a.K > kMaxK) {
-        if (req->model != HHMM_MODEL_HMM_GAUSS && req->model != HHMM_MODEL_HMM_MULTINOM) {
-            set_error("K = %d: the device path of model %d supports K <= %d", a.K, req->model, kMaxK);
-            return HHMM_ERR_UNSUPPORTED;
-        }
         if (a.K > kMaxKLarge) {
             set_error("K = %d: the device path supports K <= %d", a.K, kMaxKLarge);
+            return HHMM_ERR_UNSUPPORTED;
+        }
+        if (is_iohmm_model(req->model))
+            return run_large_iohmm(a, st);
+        if (req->model != HHMM_MODEL_HMM_GAUSS && req->model != HHMM_MODEL_HMM_MULTINOM) {
+            set_error("K = %d: the device path of model %d supports K <= %d", a.K, req->model, kMaxK);
             return HHMM_ERR_UNSUPPORTED;
         }
         return run_large(a, st);

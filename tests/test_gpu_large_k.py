@@ -95,10 +95,11 @@ def test_gamma_only_large_K_disjoint_filters(engine, oracle):
 
 
 def test_large_K_unsupported_outputs(engine):
-    """The IOHMM programs stop at K = 8 on the device (unsupported, with a message)."""
+    """Past the state capacity (K > 32) every program is unsupported, with a
+    message (the IOHMM programs at 8 < K <= 32: tests/test_gpu_iohmm_large_k.py)."""
     import hhmm_amd
-    data, draws = synth.iohmm_reg(N=1, S=2, T=10, K=12, M=4)
-    with pytest.raises(api.HHMMError):
+    data, draws = synth.iohmm_reg(N=1, S=2, T=10, K=33, M=4)
+    with pytest.raises(api.HHMMError, match="K <= 32"):
         hhmm_amd.gqs("iohmm-reg", data, draws, pars=["loglik"], lib=engine)
 
 
