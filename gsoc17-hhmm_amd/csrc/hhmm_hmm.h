@@ -462,7 +462,10 @@ constexpr bool fb_big(int mode) { return (mode & FB_BIG) != 0; }
 constexpr int fb_rp(int mode);
 constexpr int kFwdGroup = 4;  /* forward chunks per observation prefetch group */
 constexpr int kVitGroup = 2;  /* Viterbi chunks per observation prefetch group */
-constexpr int kBigChunk = 16; /* checkpoint interval of FB_BIG (a multiple of fb_chunk(K) = 8) */
+#ifndef HHMM_BIG_CHUNK
+#define HHMM_BIG_CHUNK 16
+#endif
+constexpr int kBigChunk = HHMM_BIG_CHUNK; /* checkpoint interval of FB_BIG (a multiple of fb_chunk(K) = 8) */
 /* Phases of one forward-backward launch: both sweeps (the default), or the
  * split schedule's two launches (HHMM_FLAG_FB_SPLIT): the forward sweep
  * (loglik, checkpoints, packed symbols) and then the backward sweep, with the
@@ -519,7 +522,10 @@ __device__ __forceinline__ bool wave_any(bool v)
 {
     return __builtin_amdgcn_readfirstlane((int)(__ballot(v) != 0)) != 0;
 }
-constexpr int kGroup = 2;     /* pass 1 keeps every kGroup-th state (32 steps / groups of 4 need
+#ifndef HHMM_BIG_GROUP
+#define HHMM_BIG_GROUP 2
+#endif
+constexpr int kGroup = HHMM_BIG_GROUP; /* pass 1 keeps every kGroup-th state (32 steps / groups of 4 need
                                * ~300 VGPRs: occupancy 1) */
 
 

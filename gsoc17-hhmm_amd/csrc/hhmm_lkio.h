@@ -26,8 +26,10 @@
  * loglik, alpha, beta, ungamma, gamma, unalpha, oblik_tk, oblik_t, A_ij /
  * logA_ij and the Viterbi; unbeta adds a second pass over the stored log c_t.
  * Back-pointers and the backtrack are lk_viterbi_kernel's ([P][T_b/16][K][16]
- * bytes, one 16-byte store per lane and block).  FFBS and the fitted-output
- * draws stay at K <= 8 (HHMM_ERR_UNSUPPORTED).
+ * bytes, one 16-byte store per lane and block).  FFBS (IO_DET, its own sweep):
+ * the transition does not depend on the next state, so each draw z_{t-1} =
+ * cat(v_{t-1} .* th_t, u_{t-1}) is formed in the forward sweep from the
+ * exchanged weights.  The fitted-output draws stay at K <= 8.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -38,6 +40,31 @@
 namespace hhmm {
 
 constexpr int kLkioMmax = 8; /* inputs per step on the device path (as the lane kernels' MMAX) */
+
+/* ffbs_cat over the first K entries of a KM-capacity vector (the same
+ * sequential sum and running-sum comparison; -1 when the sum is not a
+ * positive finite number) */
+template <int KM>
+__device__ __forceinline__ int lkio_cat(const double (&w)[KM], int K, double u)
+{
+    double sum = w[0];
+#pragma unroll
+    for (int i = 1; i < KM; ++i)
+        if (i < K)
+            sum = sum + w[i];
+    const double us = u * sum;
+    int b = 0;
+    double cum = w[0];
+#pragma unroll
+    for (int i = 1; i < KM; ++i) {
+        if (i < K) {
+            const bool step = (b == i - 1) & (us > cum);
+            b = step ? i : b;
+            cum = step ? cum + w[i] : cum;
+        }
+    }
+    return ((sum > 0.0) & __builtin_isfinite(sum)) ? b : -1;
+}
 
 template <int FAM, int G, int KM, int MATH>
 __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
@@ -144,11 +171,74 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
     uint32_t wd0 = 0u, wd1 = 0u, wd2 = 0u, wd3 = 0u;
     double vx[KM];
     double x, xn, u[MMAX], un[MMAX];
+    double vprev = 0.0, uprev = 0.5; /* FFBS (IO_DET): v_{t-1}, the uniform of step t - 1 */
     load(0, x, u);
     const int Tw = wave_max(Tp);
 #pragma unroll 1
     for (int t = 0; t < Tw; ++t) {
         load(t + 1, xn, un);
+        if constexpr (MATH == IO_DET) {
+            /* FFBS (oracle ffbs_contract): the K-vector transition
+             * does not depend on the next state, so z_{t-1} = cat(v_{t-1} .* th_t,
+             * u_{t-1}) with v the contract's emission factor (p .* e_0 at t = 0)
+             * and th_t the softmax numerators -- iohmm_sweep's IO_DET arithmetic */
+            if (t < Tp) {
+                double e;
+                if constexpr (FAM == IO_REG) {
+                    const double o = on ? emission(x, u) : dev_ninf();
+                    double m = grp_max<G>(o);
+                    if (m == dev_ninf())
+                        m = 0.0;
+                    e = on ? hhmm_det_exp(o - m) : 0.0;
+                } else { /* io_mix_factor: the largest summand over every state and component */
+                    double acc[kIoLmax];
+                    double mx = dev_ninf();
+#pragma unroll
+                    for (int l = 0; l < kIoLmax; ++l) {
+                        acc[l] = dev_ninf();
+                        if (l < L) {
+                            const double z = (x - mix[(l * 4 + 0) * G + j]) * mix[(l * 4 + 1) * G + j];
+                            const double z2 = z * z;
+                            acc[l] = mix[(l * 4 + 2) * G + j] + (mix[(l * 4 + 3) * G + j] + (-0.5 * z2));
+                            if (acc[l] > mx)
+                                mx = acc[l];
+                        }
+                    }
+                    double mm = grp_max<G>(on ? mx : dev_ninf());
+                    if (mm == dev_ninf())
+                        mm = 0.0;
+                    double sum = 0.0;
+#pragma unroll
+                    for (int l = 0; l < kIoLmax; ++l)
+                        if (l < L && acc[l] != dev_ninf())
+                            sum += hhmm_det_exp(acc[l] - mm);
+                    e = on ? sum : 0.0;
+                }
+                if (t == 0) {
+                    vprev = on ? pj * e : 0.0;
+                } else {
+                    const double v = on ? sse_dot<MMAX>(u, w, M) : 0.0;
+                    grp_exchange<G, KM>(xch, 0, j, v, vx);
+                    double mx = vx[0];
+#pragma unroll
+                    for (int i = 1; i < KM; ++i)
+                        if (i < K && vx[i] > mx)
+                            mx = vx[i];
+                    const double th = on ? hhmm_det_exp(v - mx) : 0.0;
+                    grp_exchange<G, KM>(xch, 1, j, vprev * th, vx);
+                    const int z = lkio_cat<KM>(vx, K, uprev);
+                    if (j == 0)
+                        a.z_ffbs[p + a.P * (int64_t)(t - 1)] = z + 1;
+                    vprev = on ? e : 0.0;
+                }
+                uprev = a.ffbs_u[p + a.P * (int64_t)t];
+            }
+            x = xn;
+#pragma unroll
+            for (int m2 = 0; m2 < MMAX; ++m2)
+                u[m2] = un[m2];
+            continue;
+        }
         if (t < Tp) { /* group-uniform */
             const double o = on ? emission(x, u) : dev_ninf();
             double A, lA = 0.0;
@@ -259,6 +349,13 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
         for (int m2 = 0; m2 < MMAX; ++m2)
             u[m2] = un[m2];
     }
+    if constexpr (MATH == IO_DET) { /* z_{T-1} = cat(v_{T-1}, u_{T-1}) */
+        grp_exchange<G, KM>(xch, 2, j, vprev, vx);
+        const int z = lkio_cat<KM>(vx, K, uprev);
+        if (j == 0)
+            a.z_ffbs[p + a.P * (int64_t)(Tp - 1)] = z + 1;
+        return;
+    }
     if ((out & HHMM_OUT_LOGLIK) && a.loglik) { /* target += log_sum_exp(unalpha_tk[T]) (iohmm-reg.stan:120) */
         const double fs = grp_sum<G>(f);
         if (j == 0)
@@ -334,11 +431,18 @@ static hhmm_status launch_lkio_g(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_UNSUPPORTED;
     }
     const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
-    const bool vit = (a.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) != 0;
+    if (a.outputs & HHMM_OUT_FFBS) { /* the draws in their own sweep (the contract's arithmetic) */
+        DevArgs f = a;
+        f.outputs = HHMM_OUT_FFBS;
+        hipLaunchKernelGGL((lkio_kernel<FAM, G, KM, IO_DET>), grid, dim3(kBlock), lds, st, f);
+    }
+    DevArgs b = a;
+    b.outputs &= ~HHMM_OUT_FFBS;
+    const bool vit = (b.outputs & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR)) != 0;
     if (vit)
-        hipLaunchKernelGGL((lkio_kernel<FAM, G, KM, IO_CR>), grid, dim3(kBlock), lds, st, a);
-    else
-        hipLaunchKernelGGL((lkio_kernel<FAM, G, KM, IO_LIBM>), grid, dim3(kBlock), lds, st, a);
+        hipLaunchKernelGGL((lkio_kernel<FAM, G, KM, IO_CR>), grid, dim3(kBlock), lds, st, b);
+    else if (b.outputs)
+        hipLaunchKernelGGL((lkio_kernel<FAM, G, KM, IO_LIBM>), grid, dim3(kBlock), lds, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("lkio_kernel launch: %s", hipGetErrorString(e));
@@ -350,9 +454,9 @@ static hhmm_status launch_lkio_g(const DevArgs &a, hipStream_t st)
 template <int FAM>
 static hhmm_status launch_lkio(const DevArgs &a, hipStream_t st)
 {
-    constexpr uint32_t kNo = HHMM_OUT_FFBS | HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
+    constexpr uint32_t kNo = HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
     if (a.outputs & kNo) {
-        set_error("K = %d: FFBS and the fitted-output draws of the IOHMM programs run at K <= %d", a.K, kMaxK);
+        set_error("K = %d: the fitted-output draws of the IOHMM programs run at K <= %d", a.K, kMaxK);
         return HHMM_ERR_UNSUPPORTED;
     }
     if (a.M > kLkioMmax || (FAM == IO_MIX && a.L > kIoLmax)) {

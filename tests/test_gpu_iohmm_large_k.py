@@ -77,10 +77,27 @@ def test_iohmm_large_K_softmax_regimes(engine, oracle, scale):
     run_both(engine, oracle, "iohmm-reg", data, draws, pars)
 
 
-def test_iohmm_large_K_ffbs_unsupported(engine):
+@pytest.mark.parametrize("K", [9, 16, 23, 32])
+@pytest.mark.parametrize("model", ["iohmm-reg", "iohmm-mix", "iohmm-hmix"])
+def test_iohmm_large_K_ffbs(engine, oracle, model, K):
+    """FFBS draws at large K (the contract's IO_DET arithmetic, its own sweep),
+    bit-exact with the oracle, beside the posterior and Viterbi outputs of
+    the same request; ragged T."""
+    import hhmm_amd
+    N, S, T = 3, 4, 150
+    data, draws = synth.GENERATORS[model](N=N, S=S, T=T, K=K, M=4)
+    data["T"] = np.array([150, 1, 77], dtype=np.int32)
+    u = synth.ffbs_uniforms(N * S, T)
+    pars = ["loglik", "gamma_tk", "z_ffbs", "zstar_t", "logp_zstar"]
+    got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, uniforms=u, return_status=True)
+    ref = oracle.gqs(model, data, draws, pars=pars, uniforms=u, return_status=True, nthreads=8)
+    compare_all(got, ref, pars + ["pair_status"])
+
+
+def test_iohmm_large_K_fitted_draws_unsupported(engine):
     import hhmm_amd
     from hhmm_amd.api import HHMMError
     data, draws = synth.iohmm_reg(N=1, S=2, T=20, K=12, M=4)
-    u = synth.ffbs_uniforms(2, 20)
-    with pytest.raises(HHMMError, match="FFBS"):
-        hhmm_amd.gqs("iohmm-reg", data, draws, pars=["loglik", "z_ffbs"], lib=engine, uniforms=u)
+    hr = np.random.default_rng(1).random((2, 20, 3))
+    with pytest.raises(HHMMError, match="fitted-output"):
+        hhmm_amd.gqs("iohmm-reg", data, draws, pars=["loglik", "hatz_t"], lib=engine, hat_rand=hr)
