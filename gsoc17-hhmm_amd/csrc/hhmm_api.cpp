@@ -106,7 +106,7 @@ static void pool_put(void *ptr)
 /* ---------------- side streams (one per device) ---------------- */
 struct SideStreams {
     std::mutex mu;
-    std::map<int, std::pair<hipStream_t, hipEvent_t>> by_dev; /* stream, fork event */
+    std::map<int, std::pair<hipStream_t, hipEvent_t>> by_dev; /* key dev * 2 + high priority: stream, fork event */
     std::map<int, hipEvent_t> join_ev;
 };
 static SideStreams &side_streams()
@@ -123,19 +123,30 @@ hhmm_status fork_stream(hipStream_t st, hipStream_t *side)
         return HHMM_ERR_HIP;
     }
     SideStreams &ss = side_streams();
+    /* The side pass (the decoder beside the forward-backward) runs on a
+     * high-priority stream: at C5 its chain of V-scan kernels is the critical
+     * path, and the forward-backward scan's waves fill in around it (13.37 ->
+     * 12.71 ms interleaved on one box, profiles/r03s_ab_c5_side_prio.log).
+     * Probe knob HHMM_PROBE_SIDE_PRIO=0: a normal-priority side stream. */
+    const char *pk = getenv("HHMM_PROBE_SIDE_PRIO");
+    const int hi = (pk && pk[0] == '0') ? 0 : 1;
+    const int key = dev * 2 + hi;
     std::lock_guard<std::mutex> g(ss.mu);
-    auto it = ss.by_dev.find(dev);
+    auto it = ss.by_dev.find(key);
     if (it == ss.by_dev.end()) {
         hipStream_t s2 = nullptr;
         hipEvent_t ev = nullptr, ej = nullptr;
-        if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
+        int lo_p = 0, hi_p = 0;
+        if (hi)
+            (void)hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
+        if (hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, hi ? hi_p : 0) != hipSuccess ||
             hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ej, hipEventDisableTiming) != hipSuccess) {
             set_error("side stream creation failed");
             return HHMM_ERR_HIP;
         }
-        it = ss.by_dev.emplace(dev, std::make_pair(s2, ev)).first;
-        ss.join_ev[dev] = ej;
+        it = ss.by_dev.emplace(key, std::make_pair(s2, ev)).first;
+        ss.join_ev[key] = ej;
     }
     if (hipEventRecord(it->second.second, st) != hipSuccess ||
         hipStreamWaitEvent(it->second.first, it->second.second, 0) != hipSuccess) {
@@ -155,7 +166,10 @@ hhmm_status join_stream(hipStream_t st, hipStream_t side)
     }
     SideStreams &ss = side_streams();
     std::lock_guard<std::mutex> g(ss.mu);
-    hipEvent_t ej = ss.join_ev[dev];
+    hipEvent_t ej = nullptr;
+    for (int hi = 0; hi < 2 && !ej; ++hi) /* the side stream is the one `side` names */
+        if (ss.by_dev.count(dev * 2 + hi) && ss.by_dev[dev * 2 + hi].first == side)
+            ej = ss.join_ev[dev * 2 + hi];
     if (!ej || hipEventRecord(ej, side) != hipSuccess || hipStreamWaitEvent(st, ej, 0) != hipSuccess) {
         set_error("stream join failed");
         return HHMM_ERR_HIP;
@@ -173,17 +187,19 @@ static hipError_t sync_request(hipStream_t st)
     if (hipGetDevice(&dev) != hipSuccess)
         return e;
     SideStreams &ss = side_streams();
-    hipStream_t side = nullptr;
-    {
-        std::lock_guard<std::mutex> g(ss.mu);
-        auto it = ss.by_dev.find(dev);
-        if (it != ss.by_dev.end())
-            side = it->second.first;
-    }
-    if (side) {
-        hipError_t e2 = hipStreamSynchronize(side);
-        if (e == hipSuccess)
-            e = e2;
+    for (int hi = 0; hi < 2; ++hi) {
+        hipStream_t side = nullptr;
+        {
+            std::lock_guard<std::mutex> g(ss.mu);
+            auto it = ss.by_dev.find(dev * 2 + hi);
+            if (it != ss.by_dev.end())
+                side = it->second.first;
+        }
+        if (side) {
+            hipError_t e2 = hipStreamSynchronize(side);
+            if (e == hipSuccess)
+                e = e2;
+        }
     }
     return e;
 }

@@ -6,7 +6,8 @@ device with one library (bench.DeviceRun's prepared requests):
   python tools/ab_sched.py --lib new=lib/libhhmm.so --lib base=lib/variants/libhhmm_base.so new:vfb base:vfb
 
 (a schedule may name its library: NAME:schedule with --lib NAME=path; a bare
-schedule runs on the first library)
+schedule runs on the first library; NAME:schedule@VAR=VAL,... sets environment
+variables around that schedule's launches, e.g. the HHMM_PROBE_* knobs)
 
 Rounds run A B C A B C ...; each round times `steps` back-to-back requests
 with HIP events on the launch stream (ms per request: median and min over
@@ -15,6 +16,7 @@ with the first one's (gamma, loglik, zstar, logp_zstar on the whole batch).
 """
 import argparse
 import json
+import os
 import pathlib
 import sys
 
@@ -48,17 +50,35 @@ def main():
     runs = {n: bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev) for n, lib in libs.items()}
 
     def split(nm):
-        return nm.split(":", 1) if ":" in nm else (first, nm)
+        """NAME:schedule@VAR=VAL,... -> (library, schedule, environment around its launches)"""
+        env = {}
+        if "@" in nm:
+            nm, ev = nm.split("@", 1)
+            env = dict(kv.split("=", 1) for kv in ev.split(","))
+        ln, sc = nm.split(":", 1) if ":" in nm else (first, nm)
+        return ln, sc, env
+
+    def launch(nm):
+        ln, sc, env = split(nm)
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            runs[ln].launch(sc)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
 
     s0 = torch.cuda.current_stream()
     ref = None
     same = {}
     for nm in a.schedules:
-        ln, sc = split(nm)
-        run = runs[ln]
+        run = runs[split(nm)[0]]
         for v in run.out.values():
             v.zero_()
-        run.launch(sc)
+        launch(nm)
         torch.cuda.synchronize()
         snap = {k: v.clone() for k, v in run.out.items()}
         if ref is None:
@@ -71,9 +91,8 @@ def main():
         for nm in a.schedules:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s0)
-            ln, sc = split(nm)
             for _ in range(a.steps):
-                runs[ln].launch(sc)
+                launch(nm)
             e1.record(s0)
             torch.cuda.synchronize()
             times[nm].append(e0.elapsed_time(e1) / a.steps)

@@ -3,7 +3,10 @@
 c4, c5, n1), in ONE process on ONE device (cross-box numbers are not
 comparable):
 
-  python tools/ab_workload.py --workload c3 NAME=path/to/libhhmm.so [NAME=...] [--rounds 5] [--steps 3]
+  python tools/ab_workload.py --workload c3 NAME=path/to/libhhmm.so[@VAR=VAL,...] [NAME=...] [--rounds 5] [--steps 3]
+
+(@VAR=VAL sets environment variables around that variant's requests: the HHMM_PROBE_* knobs;
+#FLAGS, after the path, gives that variant's request flags instead of --flags)
 
 Every variant gets the same synthetic request (bench.prepare_other); rounds
 run A B C A B C ..., each round `steps` back-to-back requests timed with HIP
@@ -12,6 +15,7 @@ variant's (integer outputs bit for bit, float outputs to 1e-12 relative).
 """
 import argparse
 import json
+import os
 import pathlib
 import sys
 
@@ -37,12 +41,34 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     runs = {}
+    envs = {}
     for v in a.variants:
         name, path = v.split("=", 1)
-        runs[name] = bench.prepare_other(a, hhmm_amd.load_library(path), dev, 0)
+        va = a
+        if "#" in path:  # NAME=lib.so#FLAGS: this variant's request flags (hhmm_request.flags)
+            path, fl = path.split("#", 1)
+            va = argparse.Namespace(**vars(a))
+            va.flags = int(fl, 0)
+        if "@" in path:  # NAME=lib.so@VAR=VAL,VAR=VAL: environment set around this variant's requests
+            path, ev = path.split("@", 1)
+            envs[name] = dict(kv.split("=", 1) for kv in ev.split(","))
+        runs[name] = bench.prepare_other(va, hhmm_amd.load_library(path), dev, 0)
+
+    def step(n):
+        env = envs.get(n, {})
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            runs[n]["step"]()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     ref = None
     for n, w in runs.items():
-        w["step"]()
+        step(n)
         torch.cuda.synchronize()
         outs = {k: t.cpu() for k, t in w["outs"].items()}
         if ref is None:
@@ -62,7 +88,7 @@ def main():
             torch.cuda.synchronize()
             ev[0].record()
             for _ in range(a.steps):
-                w["step"]()
+                step(n)
             ev[1].record()
             torch.cuda.synchronize()
             times[n].append(ev[0].elapsed_time(ev[1]) / a.steps)
