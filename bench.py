@@ -60,8 +60,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true",
-                    help="skip the 64-pair oracle check of the timed data (run after warmup, outside the "
-                         "timed region)")
+                    help="skip the 64-pair oracle check of the timed data (outside the timed region)")
+    ap.add_argument("--check-at", default="after", choices=["after", "before"],
+                    help="C2: the oracle check on the last timed step's outputs (after) or between the warmup "
+                         "and the timed steps (before: the device idles while the host checks)")
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "n1", "n2", "f1"],
                     help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
                          "printed as its own line: c1 hmm Gaussian K=3 T=500, c3 iohmm-reg grid, c4 iohmm-hmix "
@@ -461,7 +463,10 @@ def c2_workload(a, lib, rk):
         if not a.no_check and rank == 0:
             checked.append(check_slice(run, x, draws, P, T))
 
-    elapsed_rank, elapsed, per_rank = timed_region(rk, step, a.steps, a.warmup, before_timing=check)
+    elapsed_rank, elapsed, per_rank = timed_region(rk, step, a.steps, a.warmup,
+                                                   before_timing=check if a.check_at == "before" else None)
+    if a.check_at == "after":  # the outputs of the last timed step: the same inputs, the same request
+        check()
     checked = checked[0] if checked else None
     step_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     rank_step_ms = [v[0] for v in rk.gather([step_ms])]
@@ -824,8 +829,8 @@ def features_workload(a, lib, rk):
 
 def check_slice(run, x, draws, P, T):
     """Compares 64 pairs of the data the timed steps ran on (the first 32 and
-    32 spread over the batch) with the oracle, after warmup and outside the
-    timed region (test infrastructure; raises on a mismatch)."""
+    32 spread over the batch) with the oracle, outside the timed region (test
+    infrastructure; raises on a mismatch)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     sys.path.insert(0, str(ROOT / "tests"))
     import pyoracle

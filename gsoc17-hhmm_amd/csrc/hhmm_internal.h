@@ -102,7 +102,10 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
 /* T-parallel exact Viterbi (hhmm_vscan.h): V-chunks of kVsChunk steps (a whole
  * number of back-pointer words at K = 2 and 4); returns the chunk count per
  * pair of a Viterbi over Tv steps, 0 when the sequential decoders run. */
-constexpr int kVsChunk = 512;
+#ifndef HHMM_VS_CHUNK
+#define HHMM_VS_CHUNK 512 /* build knob: steps per V-chunk */
+#endif
+constexpr int kVsChunk = HHMM_VS_CHUNK;
 int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t flags);
 
 /* Large K under GRID pairing (hhmm_lkscan.h lkm_fb_kernel): the k-steps of

@@ -54,3 +54,14 @@ def test_world_size_mismatch_fails_loudly():
                        capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_c2_line_finds_its_pmc_traffic():
+    """The default C2 line's roofline.traffic comes from the committed PMC
+    record of its dominant kernel at the bench shape (a record without the
+    shape keys silently gave traffic = null)."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    dom = bench.SCHEDULE_KERNELS[bench.DEFAULT_SCHEDULE][0]
+    t = bench.load_traffic(dom, 1_000_000, 1000)
+    assert t is not None and 40.0e9 < t < 60.0e9, (dom, t)
