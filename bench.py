@@ -127,13 +127,21 @@ class Ranks:
             raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={self.world} ranks")
         self.stub = a.stub
         self.dist = None
+        # rehearsal knobs for a one-GPU box (never set by the driver): the
+        # ranks share the visible devices (local rank modulo their count) and
+        # talk over gloo, since RCCL refuses two ranks on one device
+        self.backend = os.environ.get("HHMM_BENCH_BACKEND", "gloo" if self.stub else "nccl")
+        self.gpu = self.local
+        if not self.stub and os.environ.get("HHMM_BENCH_SHARE_DEVICES"):
+            self.gpu = self.local % max(1, torch.cuda.device_count())
         if self.world > 1:
             import torch.distributed as dist
             if not self.stub:
-                torch.cuda.set_device(self.local)
-            dist.init_process_group("gloo" if self.stub else "nccl")
+                torch.cuda.set_device(self.gpu)
+            dist.init_process_group(self.backend)
             self.dist = dist
-        self.dev = torch.device("cpu") if self.stub else torch.device("cuda", self.local)
+        self.dev = torch.device("cpu") if self.stub else torch.device("cuda", self.gpu)
+        self.cdev = torch.device("cpu") if self.backend == "gloo" else self.dev  # where collectives run
 
     def sync(self):
         if not self.stub:
@@ -145,12 +153,17 @@ class Ranks:
 
     def all_reduce_sum(self, t):
         if self.dist:
-            self.dist.all_reduce(t)
+            if t.device != self.cdev:
+                h = t.to(self.cdev)
+                self.dist.all_reduce(h)
+                t.copy_(h)
+            else:
+                self.dist.all_reduce(t)
         return t
 
     def gather(self, values):
         """Per-rank float vectors -> list over ranks (every rank gets it)."""
-        t = torch.tensor(values, dtype=torch.float64, device=self.dev)
+        t = torch.tensor(values, dtype=torch.float64, device=self.cdev)
         if not self.dist:
             return [t.tolist()]
         out = [torch.empty_like(t) for _ in range(self.world)]
