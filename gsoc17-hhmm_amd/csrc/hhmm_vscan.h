@@ -775,10 +775,105 @@ constexpr size_t vs_sp_lds(int L)
            64 * sizeof(double);
 }
 
+/* Max-plus product of two K x K matrices, C = A (x) B (approximate scan). */
+template <int K>
+__device__ __forceinline__ void vs_mp_mul(const double (&A)[K][K], const double (&B)[K][K], double (&C)[K][K])
+{
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            double b = A[i][0] + B[0][j];
+#pragma unroll
+            for (int k = 1; k < K; ++k)
+                b = fmax(b, A[i][k] + B[k][j]);
+            C[i][j] = b;
+        }
+}
+
+template <int K>
+__device__ __forceinline__ void vs_mp_shfl_up(const double (&A)[K][K], int d, double (&Q)[K][K])
+{
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            Q[i][j] = __shfl_up(A[i][j], d, 64);
+}
+
+/* One block of the approximate scan with the wave's lanes in parallel: lane l
+ * holds chunk cb + l's approximate product (identity past the pair's last
+ * chunk); a Hillis-Steele max-plus prefix over the 64 lanes gives every lane
+ * the delta entering its chunk from the block's entry `dl` (uniform), whose
+ * binade it stores; `dl` leaves as the block's exit.  The approximate scan
+ * only predicts each chunk's grid (the exact scan checks every prediction),
+ * so the reassociated sums are harmless; the serial walk spent ~1,200 cycles
+ * of dependent latency per chunk on its one wave. */
+template <int K>
+__device__ __forceinline__ void vs_scan0_block(const DevArgs &a, int64_t p, int cb, int ncp, const VsBlock<K> &b,
+                                               double (&dl)[K])
+{
+    const int lane = threadIdx.x & 63;
+    const bool live = cb + lane < ncp;
+    double P[K][K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            P[i][j] = live ? b.m[i][j] : (i == j ? 0.0 : dev_ninf());
+#pragma unroll
+    for (int d = 1; d < 64; d *= 2) {
+        double Q[K][K], R[K][K];
+        vs_mp_shfl_up<K>(P, d, Q);
+        vs_mp_mul<K>(Q, P, R);
+        if (lane >= d) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    P[i][j] = R[i][j];
+        }
+    }
+    /* exclusive prefix: the product of the chunks before this lane's */
+    double E[K][K];
+    vs_mp_shfl_up<K>(P, 1, E);
+    double din[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        if (lane == 0) {
+            din[j] = dl[j];
+        } else {
+            double v = dl[0] + E[0][j];
+#pragma unroll
+            for (int r = 1; r < K; ++r)
+                v = fmax(v, dl[r] + E[r][j]);
+            din[j] = v;
+        }
+    }
+    if (live) {
+        const double hi = vs_hi<K>(din);
+        a.vs_k[p + a.P * (int64_t)(cb + lane)] = (hi > dev_ninf() && hi != 0.0) ? vs_binade(hi) : kVsNoGrid;
+    }
+    /* the block's exit: dl (x) the inclusive prefix of lane 63 (identity past ncp) */
+    double out[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double v = dl[0] + __shfl(P[0][j], 63, 64);
+#pragma unroll
+        for (int r = 1; r < K; ++r)
+            v = fmax(v, dl[r] + __shfl(P[r][j], 63, 64));
+        out[j] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        dl[j] = out[j];
+}
+
 /* One wave per pair: chunk 0 exactly (row 1 of vs_d), then the approximate
  * scan over the approximate chunk products: k_c = binade of the largest
- * finite delta entering chunk c. */
-template <int MODEL, int K>
+ * finite delta entering chunk c.  PAR: the lane-parallel prefix per block of
+ * 64 chunks (vs_scan0_block); else the serial walk. */
+template <int MODEL, int K, bool PAR>
 __global__ void __launch_bounds__(64) vs_scan0_kernel(const DevArgs a)
 {
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
@@ -802,6 +897,14 @@ __global__ void __launch_bounds__(64) vs_scan0_kernel(const DevArgs a)
     vs_sp_steps<MODEL, K, true>(a, ln, sp, 0, min(kVsChunk, Tp), dl);
     if (l0)
         vs_store_d<K>(a, p, 1, dl);
+    if constexpr (PAR) {
+        for (int cb = 1; cb < ncp; cb += 64) {
+            const VsBlock<K> cur = nxt;
+            vs_fetch<K>(a, p, cb + 64, ncp, nxt);
+            vs_scan0_block<K>(a, p, cb, ncp, cur, dl);
+        }
+        return;
+    }
     for (int cb = 1; cb < ncp; cb += 64) {
         vs_stage<K>(nxt, blk);
         __syncthreads();
@@ -1055,7 +1158,10 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
         e = hipMemsetAsync(a.vs_tl, 0, sizeof(int32_t), st); /* the tie list's count */
     if (e == hipSuccess) {
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, false>), gc, bc, lds_c, st, a);
-        hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
+        if (getenv("HHMM_PROBE_VS_SCAN0_SERIAL")) /* probe knob: the serial approximate walk */
+            hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K, false>), dim3((unsigned)a.P), b64, lds_s, st, a);
+        else
+            hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K, true>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, true>), gc, bc, lds_c, st, a);
         if (ModelTraits<MODEL>::kGauss || !HHMM_VS_TIE_INLINE) /* the listed tie chunks */
             hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3(kVsTieBlocks), bc, lds_c, st, a);
