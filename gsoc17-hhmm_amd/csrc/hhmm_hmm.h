@@ -491,7 +491,7 @@ constexpr int fb_rp(int mode) { return (fb_big(mode) && !(mode & FB_RN1)) ? kBig
  * as with per-step renormalisation.  Pairs with a smaller b (rare symbols,
  * near-zero transitions; the reference's log space stays finite there) make
  * their wave renormalise every step (FB_RN1), the exact per-step form. */
-constexpr double kRenormSafeBound = 0x1p-39;
+constexpr double kRenormSafeBound = 1.0 / (double)(1ull << (156 / kBigRenorm)); /* 2^-39 at 4 steps */
 template <int MODEL, int K>
 __device__ __forceinline__ bool renorm_sparse_safe(const PairParams<MODEL, K> &pp, const double2 *slab, int L)
 {
