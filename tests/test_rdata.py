@@ -118,3 +118,32 @@ def test_in_sample_zigzag_count_matches_report(oracle):
     when = time[F.index_ticks(legs, price)]
     assert int(F.xts_window(when, RMD_INS).sum()) == 8386
     assert int(F.xts_window(when, RMD_OOS).sum()) > 0
+
+
+# Column sums of Table 4 ("tab:tseg-filtered-ins") of the rendered tayal2009/main.pdf:
+# main.Rmd:704-723 prints table(x.ins, state.filtered.ins) with the rows labelled by
+# expand.grid(1:9, c("U", "D")), i.e. feature codes 1..9 = U1..U9 and 10..18 = D1..D9.
+# Summed over the four states they are the in-sample count of each leg feature.
+TABLE4_U = (58, 15, 158, 810, 2155, 828, 33, 49, 17)
+TABLE4_D = (15, 72, 34, 831, 2209, 846, 181, 16, 59)
+
+
+@pytest.mark.skipif(not DATA.exists(), reason="reference tick data not present (GPU box)")
+def test_in_sample_feature_histogram_matches_report_table4(oracle):
+    """Second reference-held pin for F1, symbol by symbol: the per-feature counts
+    of the same 8386 in-sample zig-zags pin the leg coding of
+    feature-extraction.R:92-110, and the (x, sign) split of tayal2009/main.R:85-89
+    (sign = 1 for codes 1..9 = U, x = code; sign = 2 for 10..18 = D, x = code - 9)."""
+    from hhmm_amd import features as F
+    files = [DATA / "G.TO" / f"{d}.G.TO.RData" for d in RMD_DAYS]
+    price, size, time = rdata.load_ticks(files)
+    legs = oracle.extract_features(price, size, time, alpha=0.25)
+    ins = F.xts_window(time[F.index_ticks(legs, price)], RMD_INS)
+    counts = np.bincount(legs["feature"][ins], minlength=19)
+    assert counts[0] == 0 and counts.size == 19
+    assert tuple(counts[1:10]) == TABLE4_U
+    assert tuple(counts[10:19]) == TABLE4_D
+    assert sum(TABLE4_U) + sum(TABLE4_D) == 8386
+    x, sign = legs["x"][ins], legs["sign"][ins]
+    assert tuple(np.bincount(x[sign == 1], minlength=10)[1:]) == TABLE4_U
+    assert tuple(np.bincount(x[sign == 2], minlength=10)[1:]) == TABLE4_D
