@@ -196,27 +196,38 @@ def timed_region(rk, step, steps, warmup, before_timing=None):
     return elapsed, max(per_rank), per_rank
 
 
+PATH_GATHER_CAP = 512 << 20  # bytes of pinned host buffer per rank for the timed D2H
+
+
 def path_gather(rk, zs):
     """The decoded paths leave the device: this rank's zstar_t slice is copied
     into a pinned host buffer (a direct D2H per rank into its
     slice of the caller's array), all ranks at once, timed after the timed
-    region.  Returns bytes per rank and the max time over ranks."""
-    host = torch.empty(zs.shape, dtype=zs.dtype, pin_memory=True)
+    region.  At most PATH_GATHER_CAP bytes (whole time rows) are copied and the
+    time is scaled to the whole slice (a 4 GB pinned buffer per rank
+    would be 32 GB of pinned memory at 8 GPUs).  Returns bytes per rank and the
+    max time over ranks."""
+    row = zs[0].numel() * zs.element_size()
+    rows = max(1, min(zs.shape[0], PATH_GATHER_CAP // max(row, 1)))
+    src = zs[:rows]
+    host = torch.empty(src.shape, dtype=zs.dtype, pin_memory=True)
     rk.sync()
     rk.barrier()
     t0 = time.perf_counter()
-    host.copy_(zs, non_blocking=True)
+    host.copy_(src, non_blocking=True)
     rk.sync()
     dt = time.perf_counter() - t0
     rk.barrier()
-    per_rank = [v[0] for v in rk.gather([dt])]
     nbytes = zs.numel() * zs.element_size()
+    sample = src.numel() * src.element_size()
+    per_rank = [v[0] * nbytes / sample for v in rk.gather([dt])]
     ok = bool(torch.equal(host[:1], zs[:1].cpu()))
     del host
     return {"bytes_per_rank": nbytes, "ms_max_over_ranks": max(per_rank) * 1e3,
             "ms_per_rank": [x * 1e3 for x in per_rank],
             "GBps_per_rank": nbytes / max(per_rank) / 1e9,
             "GBps_aggregate": rk.world * nbytes / max(per_rank) / 1e9,
+            "sample_bytes_per_rank": sample, "scaled_from_sample": sample < nbytes,
             "destination": "pinned host buffer per rank (zstar_t [T, P] int32)", "first_row_verified": ok}
 
 

@@ -128,7 +128,7 @@ hhmm_status fork_stream(hipStream_t st, hipStream_t *side)
      * path, and the forward-backward scan's waves fill in around it (13.37 ->
      * 12.71 ms interleaved on one box, profiles/r03s_ab_c5_side_prio.log).
      * Probe knob HHMM_PROBE_SIDE_PRIO=0: a normal-priority side stream. */
-    const char *pk = getenv("HHMM_PROBE_SIDE_PRIO");
+    const char *pk = probe_env("HHMM_PROBE_SIDE_PRIO");
     const int hi = (pk && pk[0] == '0') ? 0 : 1;
     const int key = dev * 2 + hi;
     std::lock_guard<std::mutex> g(ss.mu);
@@ -301,9 +301,10 @@ struct ArrayDesc {
         }                                                                                           \
     } while (0)
 
-static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool host)
+/* o == nullptr: the request side only (the segment summary call has no result). */
+static hhmm_status validate_impl(const hhmm_request *r, const hhmm_result *o, bool host)
 {
-    REQUIRE(r && o, "request and result must be non-NULL");
+    REQUIRE(r, "request must be non-NULL");
     REQUIRE(r->abi_version == HHMM_ABI_VERSION, "abi_version %u != %u", r->abi_version, HHMM_ABI_VERSION);
     REQUIRE(r->model >= 1 && r->model <= 9, "unknown model id %d", r->model);
     REQUIRE(r->pairing == HHMM_PAIR_GRID || r->pairing == HHMM_PAIR_ZIP || r->pairing == HHMM_PAIR_BLOCK,
@@ -350,31 +351,34 @@ static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool ho
     REQUIRE((r->outputs & ~avail) == 0, "outputs 0x%x not declared by model %d (available 0x%x)",
             r->outputs & ~avail, m, avail);
     REQUIRE(r->outputs != 0, "no outputs requested");
+    static const hhmm_result none{};
+    const hhmm_result *oo = o ? o : &none;
     struct {
         uint32_t bit;
         const void *ptr;
         const char *name;
-    } outs[] = {{HHMM_OUT_LOGLIK, o->loglik, "loglik"},
-                {HHMM_OUT_UNALPHA, o->unalpha_tk, "unalpha_tk"},
-                {HHMM_OUT_ALPHA, o->alpha_tk, "alpha_tk"},
-                {HHMM_OUT_UNBETA, o->unbeta_tk, "unbeta_tk"},
-                {HHMM_OUT_BETA, o->beta_tk, "beta_tk"},
-                {HHMM_OUT_UNGAMMA, o->ungamma_tk, "ungamma_tk"},
-                {HHMM_OUT_GAMMA, o->gamma_tk, "gamma_tk"},
-                {HHMM_OUT_ZSTAR, o->zstar_t, "zstar_t"},
-                {HHMM_OUT_LOGP_ZSTAR, o->logp_zstar, "logp_zstar"},
-                {HHMM_OUT_OBLIK_TK, o->oblik_tk, "oblik_tk"},
-                {HHMM_OUT_OBLIK_T, o->oblik_t, "oblik_t"},
-                {HHMM_OUT_FFBS, o->z_ffbs, "z_ffbs"},
-                {HHMM_OUT_ALPHA_OOS, o->alpha_tk_oos, "alpha_tk_oos"},
-                {HHMM_OUT_UNALPHA_OOS, o->unalpha_tk_oos, "unalpha_tk_oos"},
-                {HHMM_OUT_LOGA, o->logA_ij, "logA_ij"},
-                {HHMM_OUT_HATPI, o->hatpi_tk, "hatpi_tk"},
-                {HHMM_OUT_HATZ, o->hatz_t, "hatz_t"},
-                {HHMM_OUT_HATL, o->hatl_t, "hatl_t"},
-                {HHMM_OUT_HATX, o->hatx_t, "hatx_t"}};
-    for (auto &e : outs)
-        REQUIRE(!(r->outputs & e.bit) || e.ptr, "output %s requested but its pointer is NULL", e.name);
+    } outs[] = {{HHMM_OUT_LOGLIK, oo->loglik, "loglik"},
+                {HHMM_OUT_UNALPHA, oo->unalpha_tk, "unalpha_tk"},
+                {HHMM_OUT_ALPHA, oo->alpha_tk, "alpha_tk"},
+                {HHMM_OUT_UNBETA, oo->unbeta_tk, "unbeta_tk"},
+                {HHMM_OUT_BETA, oo->beta_tk, "beta_tk"},
+                {HHMM_OUT_UNGAMMA, oo->ungamma_tk, "ungamma_tk"},
+                {HHMM_OUT_GAMMA, oo->gamma_tk, "gamma_tk"},
+                {HHMM_OUT_ZSTAR, oo->zstar_t, "zstar_t"},
+                {HHMM_OUT_LOGP_ZSTAR, oo->logp_zstar, "logp_zstar"},
+                {HHMM_OUT_OBLIK_TK, oo->oblik_tk, "oblik_tk"},
+                {HHMM_OUT_OBLIK_T, oo->oblik_t, "oblik_t"},
+                {HHMM_OUT_FFBS, oo->z_ffbs, "z_ffbs"},
+                {HHMM_OUT_ALPHA_OOS, oo->alpha_tk_oos, "alpha_tk_oos"},
+                {HHMM_OUT_UNALPHA_OOS, oo->unalpha_tk_oos, "unalpha_tk_oos"},
+                {HHMM_OUT_LOGA, oo->logA_ij, "logA_ij"},
+                {HHMM_OUT_HATPI, oo->hatpi_tk, "hatpi_tk"},
+                {HHMM_OUT_HATZ, oo->hatz_t, "hatz_t"},
+                {HHMM_OUT_HATL, oo->hatl_t, "hatl_t"},
+                {HHMM_OUT_HATX, oo->hatx_t, "hatx_t"}};
+    if (o)
+        for (auto &e : outs)
+            REQUIRE(!(r->outputs & e.bit) || e.ptr, "output %s requested but its pointer is NULL", e.name);
     if (r->outputs & HHMM_OUT_FFBS)
         REQUIRE(r->ffbs_u, "FFBS needs ffbs_u");
     if (r->outputs & (HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX))
@@ -422,6 +426,12 @@ static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool ho
                 REQUIRE(w.sigma_k[i] > 0.0, "sigma_k must be > 0 (real<lower=0.0001>)");
     }
     return HHMM_OK;
+}
+
+static hhmm_status validate(const hhmm_request *r, const hhmm_result *o, bool host)
+{
+    REQUIRE(r && o, "request and result must be non-NULL");
+    return validate_impl(r, o, host);
 }
 
 /* Element counts of every input / output array the request uses. */
@@ -579,18 +589,41 @@ static std::vector<Shard> make_shards(const hhmm_request *r, int n)
     return v;
 }
 
+/* One array's shard in the caller's buffer: `rows` rows of `width` bytes at a
+ * pitch of `pitch` bytes from `base`; packed (pitch = width) in the shard's copy. */
+struct ShardRows {
+    char *base;
+    size_t rows, width, pitch;
+};
+static ShardRows shard_rows(const void *host, const ArrayDesc &a, const Shard &sh)
+{
+    const size_t es = a.esize, lead = (size_t)sh.lead[a.cls], cnt = (size_t)sh.cnt[a.cls];
+    return ShardRows{(char *)host + (size_t)sh.off[a.cls] * es, a.elems / lead, cnt * es, lead * es};
+}
+
 /* Host <-> device copy of one array's shard: rows of cnt elements at a pitch
  * of lead on the host, packed on the device. */
 static hipError_t copy_shard(void *dev, const void *host, const ArrayDesc &a, const Shard &sh, bool to_device)
 {
-    const size_t es = a.esize, lead = (size_t)sh.lead[a.cls], cnt = (size_t)sh.cnt[a.cls];
-    const size_t rows = a.elems / lead;
-    char *h = (char *)host + (size_t)sh.off[a.cls] * es;
-    if (cnt == lead)
-        return to_device ? hipMemcpy(dev, h, rows * cnt * es, hipMemcpyHostToDevice)
-                         : hipMemcpy(h, dev, rows * cnt * es, hipMemcpyDeviceToHost);
-    return to_device ? hipMemcpy2D(dev, cnt * es, h, lead * es, cnt * es, rows, hipMemcpyHostToDevice)
-                     : hipMemcpy2D(h, lead * es, dev, cnt * es, cnt * es, rows, hipMemcpyDeviceToHost);
+    const ShardRows r = shard_rows(host, a, sh);
+    if (r.width == r.pitch)
+        return to_device ? hipMemcpy(dev, r.base, r.rows * r.width, hipMemcpyHostToDevice)
+                         : hipMemcpy(r.base, dev, r.rows * r.width, hipMemcpyDeviceToHost);
+    return to_device ? hipMemcpy2D(dev, r.width, r.base, r.pitch, r.width, r.rows, hipMemcpyHostToDevice)
+                     : hipMemcpy2D(r.base, r.pitch, dev, r.width, r.width, r.rows, hipMemcpyDeviceToHost);
+}
+
+/* copy_shard's host-only twin for hhmm_selftest_shards (memcpy per row). */
+static void copy_shard_host(void *packed, const void *host, const ArrayDesc &a, const Shard &sh, bool to_packed)
+{
+    const ShardRows r = shard_rows(host, a, sh);
+    for (size_t i = 0; i < r.rows; ++i) {
+        char *h = r.base + i * r.pitch, *q = (char *)packed + i * r.width;
+        if (to_packed)
+            memcpy(q, h, r.width);
+        else
+            memcpy(h, q, r.width);
+    }
 }
 
 /* Runs one shard of a host request on the current device: uploads its slices,
@@ -970,6 +1003,9 @@ static hhmm_status segment_run(const hhmm_request *req, hhmm_result *res, const 
             set_error("segment summary: seg->summary is NULL");
             return HHMM_ERR_INVALID_ARGUMENT;
         }
+        /* the request side (draw and data pointers) before any launch */
+        if ((s = validate_impl(&r2, nullptr, false)) != HHMM_OK)
+            return s;
     } else {
         if ((!seg->first && !seg->enter) || (!seg->last && !seg->leave)) {
             set_error("segment finish: a window that is not first needs enter, one that is not last needs leave");
@@ -999,6 +1035,46 @@ hhmm_status hhmm_segment_finish_device(const hhmm_request *req, hhmm_result *res
                                        void *workspace, size_t workspace_bytes_, void *stream)
 {
     return segment_run(req, res, seg, workspace, workspace_bytes_, stream, 2);
+}
+
+hhmm_status hhmm_selftest_shards(const hhmm_request *req, hhmm_result *res, int nshards)
+{
+    hhmm_status s = validate(req, res, true);
+    if (s != HHMM_OK)
+        return s;
+    if (nshards < 1) {
+        set_error("nshards must be >= 1");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    hhmm_request dreq = *req;
+    hhmm_result dres = *res;
+    std::vector<ArrayDesc> arrays;
+    describe(req, res, &dreq, &dres, arrays);
+    for (const Shard &sh : make_shards(req, nshards)) {
+        for (const ArrayDesc &a : arrays) {
+            const ShardRows r = shard_rows(a.host, a, sh);
+            std::vector<char> packed(r.rows * r.width);
+            copy_shard_host(packed.data(), a.host, a, sh, true);
+            if (!a.output) /* inputs only travel host -> shard: back into a scratch twin */
+                continue;
+            const size_t n = packed.size() / a.esize;
+            for (size_t i = 0; i < n; ++i) {
+                if (a.esize == sizeof(double)) {
+                    double v;
+                    memcpy(&v, &packed[i * 8], 8);
+                    v += 1.0;
+                    memcpy(&packed[i * 8], &v, 8);
+                } else {
+                    int32_t v;
+                    memcpy(&v, &packed[i * 4], 4);
+                    v += 1;
+                    memcpy(&packed[i * 4], &v, 4);
+                }
+            }
+            copy_shard_host(packed.data(), a.host, a, sh, false);
+        }
+    }
+    return HHMM_OK;
 }
 
 hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n)

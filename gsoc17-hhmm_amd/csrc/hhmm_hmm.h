@@ -479,6 +479,8 @@ enum FbPhase { FB_PH_BOTH = 0, FB_PH_FWD = 1, FB_PH_BWD = 2 };
 #define HHMM_BIG_RENORM 4
 #endif
 constexpr int kBigRenorm = HHMM_BIG_RENORM;
+/* the gate's bound 2^-(156 / kBigRenorm) below is a shift of at most 52 bits */
+static_assert(kBigRenorm >= 3 && kBigRenorm <= 8, "HHMM_BIG_RENORM must be 3..8");
 constexpr int fb_rp(int mode) { return (fb_big(mode) && !(mode & FB_RN1)) ? kBigRenorm : 1; }
 /* Is the kBigRenorm-step cadence safe for this pair?  Renormalisation leaves
  * the filter's max in [0.5, 1).  One forward step keeps the max at least
@@ -2831,7 +2833,7 @@ struct LaunchShape {
  * kernel's workgroups share a CU (and so leaves room for the other kernel's). */
 static size_t lds_floor(const char *name)
 {
-    const char *v = getenv(name);
+    const char *v = probe_env(name);
     return v ? (size_t)atoi(v) * 1024 : 0;
 }
 
@@ -2840,8 +2842,8 @@ static bool shape_for(const DevArgs &a, bool discrete, LaunchShape &s, const cha
     const int KP = (a.K + 1) / 2;
     size_t per_wave = discrete ? (size_t)a.L * KP * 64 * sizeof(double2) : 0;
     int waves = 4;
-    if (probe && getenv(probe)) /* probe knob (tools/ab_bench.py --env): waves per workgroup, 1..4 */
-        waves = std::min(std::max(atoi(getenv(probe)), 1), 4);
+    if (probe && probe_env(probe)) /* probe knob (tools/ab_bench.py --env): waves per workgroup, 1..4 */
+        waves = std::min(std::max(atoi(probe_env(probe)), 1), 4);
     if (per_wave > 0) {
         while (waves > 0 && per_wave * waves > kLdsLimit)
             --waves;

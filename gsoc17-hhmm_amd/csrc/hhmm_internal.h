@@ -6,11 +6,22 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "hhmm.h"
 #include "hhmm_features.h"
 
 namespace hhmm {
+
+/* Probe knobs (HHMM_PROBE_* environment variables: launch shapes, stream
+ * priority, the V-scan statistics) exist only in a build with -DHHMM_PROBES
+ * (tools/build_variant.sh); a release libhhmm.so never reads the environment,
+ * so a stray variable cannot change its schedule or synchronise it. */
+#ifdef HHMM_PROBES
+static inline const char *probe_env(const char *name) { return getenv(name); }
+#else
+static inline const char *probe_env(const char *) { return nullptr; }
+#endif
 
 /* Everything one launch needs, by value in the kernel argument segment.
  * All pointers are device pointers; layouts as in include/hhmm.h. */
@@ -58,6 +69,7 @@ struct DevArgs {
     double *lam;        /* [Tmax][P]      IOHMM: running sum of log c_t (unbeta pass) */
     uint32_t *xpk;      /* [nchunk][P]    packed symbols of each checkpoint chunk (multinom, L <= 16) */
     int32_t *rnw;       /* [waves]        FB_BIG: the wave renormalises every step (fb_dense_kernel) */
+    int32_t *io_redo;   /* [1 + P]        IOHMM: pairs whose linear filter underflowed (count, then ids) */
     /* parallel scan over T; scan_cl = 0: sequential sweeps */
     uint32_t flags;     /* hhmm_request.flags */
     int32_t scan_cl;    /* steps per T-chunk (multiple of fb_chunk(K)) */
@@ -151,6 +163,14 @@ hhmm_status run_large_iohmm(const DevArgs &a, hipStream_t st);
 
 /* IOHMM family (iohmm-reg / -mix / -hmix / -hmix-lite), hhmm_iohmm.hip. */
 hhmm_status launch_iohmm(const DevArgs &a, hipStream_t stream);
+/* The outputs the IOHMM linear-space filter produces; a pair whose filter
+ * drops below kIoWeak is listed in a.io_redo and re-run in log space by
+ * launch_iohmm_log (hhmm_iolog.hip). */
+constexpr uint32_t kIoFilt = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA | HHMM_OUT_UNBETA | HHMM_OUT_BETA |
+                             HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA | HHMM_OUT_OBLIK_T;
+constexpr uint32_t kIoBack = HHMM_OUT_UNBETA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
+constexpr double kIoWeak = 0x1p-960;
+hhmm_status launch_iohmm_log(const DevArgs &a, hipStream_t stream);
 /* Fitted-output draws hatpi / hatz / hatl / hatx (hhmm_fitted.hip). */
 hhmm_status launch_fitted(const DevArgs &a, hipStream_t stream);
 hhmm_status run_io_reg_lo(const DevArgs &a, hipStream_t st);

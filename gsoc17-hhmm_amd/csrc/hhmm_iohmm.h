@@ -428,12 +428,17 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
     constexpr int STEPB = K * BITS;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int64_t p = min((int64_t)blockIdx.x * blockDim.x + threadIdx.x, a.P - 1);
+    const int64_t pg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t p = min(pg, a.P - 1);
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
     const int M = a.M, L = a.L;
     const uint32_t out = HOT ? (a.outputs & kIoHot) : a.outputs;
+    /* the linear filter's underflow check (hhmm_iolog.hip): s_t, max f_0 and,
+     * where a backward output is read, c_t must stay above kIoWeak */
+    const bool gate = (out & kIoFilt) && a.io_redo;
+    bool weak = false;
     const bool want_vit = MATH == IO_CR && (out & (HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR));
     const bool want_ffbs = MATH == IO_DET && (out & HHMM_OUT_FFBS) && a.z_ffbs;
     const bool fixed_init = (a.model == HHMM_MODEL_IOHMM_HMIX); /* iohmm-hmix.stan:166-167 */
@@ -571,6 +576,11 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     f[k] = pp.p[k] * e[k];
+                double f0 = f[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k)
+                    f0 = fmax(f0, f[k]);
+                weak = gate && !(f0 >= kIoWeak);
             } else {
                 /* num_filter: the softmax numerators, the sum in the log scale
                  * (psum, pex) -- iohmm_sp_sweep's arithmetic, bit for bit */
@@ -587,14 +597,18 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     f[k] = e[k] * s;
+                weak |= gate && !(s >= kIoWeak);
                 /* log c_t = m + log sum_i A_t(i) e_t(i) (backward accumulator, :94) */
-                if (out & HHMM_OUT_UNBETA) {
+                if (out & kIoBack) {
                     double c = st.A[0] * e[0];
 #pragma unroll
                     for (int i = 1; i < K; ++i)
                         c = fma(st.A[i], e[i], c);
-                    lam += m + log(c);
-                    at(a.lam + a.P * (int64_t)t, (uint32_t)p * 8u) = lam;
+                    weak |= gate && !(c >= kIoWeak);
+                    if (out & HHMM_OUT_UNBETA) {
+                        lam += m + log(c);
+                        at(a.lam + a.P * (int64_t)t, (uint32_t)p * 8u) = lam;
+                    }
                 }
             }
             lsc += m;
@@ -698,6 +712,8 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
     }
     if (want_ffbs)
         at(a.z_ffbs + a.P * (int64_t)(Tp - 1), (uint32_t)p * 4u) = ffbs_cat<K>(vprev, uprev) + 1;
+    if (weak && pg < a.P) /* re-run in log space (launch_iohmm_log) */
+        a.io_redo[1 + atomicAdd(&a.io_redo[0], 1)] = (int32_t)p;
     if ((out & HHMM_OUT_LOGLIK) && a.loglik) /* target += log_sum_exp(unalpha_tk[T]) (iohmm-reg.stan:120) */
         a.loglik[p] = (log(vsum<K>(f)) + (lsc + kLn2 * ex)) - (log(psum) + kLn2 * pex);
 
@@ -768,6 +784,8 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
     const int M = a.M, L = a.L;
     const uint32_t out = a.outputs;
     const bool want_ffbs = MATH == IO_DET && (out & HHMM_OUT_FFBS) && a.z_ffbs;
+    const bool gate = (out & kIoFilt) && a.io_redo; /* iohmm_sweep's underflow check */
+    bool weak = false;
 
     /* ---- parameters: p_1k whole, state js's rows and tables ---- */
     double pk[K];
@@ -911,6 +929,11 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     f[k] = pk[k] * ee[k];
+                double f0 = f[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k)
+                    f0 = fmax(f0, f[k]);
+                weak = gate && !(f0 >= kIoWeak);
             } else {
                 double sv = f[0] * AA[0];
 #pragma unroll
@@ -919,6 +942,14 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     f[k] = ee[k] * sv;
+                weak |= gate && !(sv >= kIoWeak);
+                if (out & kIoBack) { /* the backward accumulator sum_i A_t(i) e_t(i) (numerators) */
+                    double c = AA[0] * ee[0];
+#pragma unroll
+                    for (int i = 1; i < K; ++i)
+                        c = fma(AA[i], ee[i], c);
+                    weak |= gate && !(c >= kIoWeak);
+                }
             }
             lsc += m;
             renorm<K>(f, ex);
@@ -942,6 +973,8 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
     if (live && j == 0) {
         if (want_ffbs)
             at(a.z_ffbs + a.P * (int64_t)(Tp - 1), (uint32_t)p * 4u) = ffbs_cat<K>(vprev, uprev) + 1;
+        if (weak) /* re-run in log space (launch_iohmm_log) */
+            a.io_redo[1 + atomicAdd(&a.io_redo[0], 1)] = (int32_t)p;
         if ((out & HHMM_OUT_LOGLIK) && a.loglik)
             a.loglik[p] = (log(vsum<K>(f)) + (lsc + kLn2 * ex)) - (log(psum) + kLn2 * pex);
     }

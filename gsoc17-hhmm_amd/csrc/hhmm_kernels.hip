@@ -192,7 +192,7 @@ int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t
 
 /* Offsets of every workspace region (SIZE_MAX = unused) and the total. */
 struct WsLayout {
-    size_t ckpt, ckpt_ls, xpk, rnw, bp, lam, mf, qb, mx, st, sl, be, bl, total;
+    size_t ckpt, ckpt_ls, xpk, rnw, bp, lam, ior, mf, qb, mx, st, sl, be, bl, total;
     size_t vm, vm1, vd, vk, ve, vz, vf, vt;
     int vnc;
     ScanPlan sp;
@@ -203,7 +203,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
 {
     WsLayout w;
     const size_t NONE = SIZE_MAX;
-    w.ckpt = w.ckpt_ls = w.xpk = w.rnw = w.bp = w.lam = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
+    w.ckpt = w.ckpt_ls = w.xpk = w.rnw = w.bp = w.lam = w.ior = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
     w.vm = w.vm1 = w.vd = w.vk = w.ve = w.vz = w.vf = w.vt = NONE;
     w.vnc = 0;
     size_t off = 0;
@@ -238,6 +238,8 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
             w.bp = take((size_t)P * K * (size_t)((Tmax + 15) & ~15));
         if (is_iohmm_model(model) && (outputs & HHMM_OUT_UNBETA))
             w.lam = take((size_t)Tmax * P * d);
+        if (is_iohmm_model(model) && (outputs & kIoFilt))
+            w.ior = take((size_t)(1 + P) * sizeof(int32_t));
         w.total = off + 256;
         return w;
     }
@@ -285,6 +287,8 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     }
     if (is_iohmm_model(model) && (outputs & HHMM_OUT_UNBETA))
         w.lam = take((size_t)Tmax * P * d);
+    if (is_iohmm_model(model) && (outputs & kIoFilt))
+        w.ior = take((size_t)(1 + P) * sizeof(int32_t));
     w.total = off + 256;
     return w;
 }
@@ -306,6 +310,7 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
     a.rnw = (int32_t *)at_off(w.rnw);
     a.bp = (uint32_t *)at_off(w.bp);
     a.lam = (double *)at_off(w.lam);
+    a.io_redo = (int32_t *)at_off(w.ior);
     a.scan_cl = w.sp.cl;
     a.scan_nc = w.sp.nc;
     a.sc_mf = (double *)at_off(w.mf);
@@ -386,6 +391,23 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
     return a;
 }
 
+/* An IOHMM sweep with its log-space fallback: the list of underflowed pairs
+ * is cleared, the sweep lists them, launch_iohmm_log re-runs them (all on `st`). */
+static hhmm_status run_iohmm_filtered(const DevArgs &a, hipStream_t st, hhmm_status (*sweep)(const DevArgs &, hipStream_t))
+{
+    if (a.io_redo && (a.outputs & kIoFilt)) {
+        const hipError_t e = hipMemsetAsync(a.io_redo, 0, sizeof(int32_t), st);
+        if (e != hipSuccess) {
+            set_error("hipMemsetAsync: %s", hipGetErrorString(e));
+            return HHMM_ERR_HIP;
+        }
+    }
+    const hhmm_status s = sweep(a, st);
+    if (s != HHMM_OK)
+        return s;
+    return launch_iohmm_log(a, st);
+}
+
 hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws, hipStream_t st,
                        const hhmm_segment *seg, int seg_phase)
 {
@@ -410,7 +432,7 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
             return HHMM_ERR_UNSUPPORTED;
         }
         if (is_iohmm_model(req->model))
-            return run_large_iohmm(a, st);
+            return run_iohmm_filtered(a, st, run_large_iohmm);
         if (req->model != HHMM_MODEL_HMM_GAUSS && req->model != HHMM_MODEL_HMM_MULTINOM) {
             set_error("K = %d: the device path of model %d supports K <= %d", a.K, req->model, kMaxK);
             return HHMM_ERR_UNSUPPORTED;
@@ -431,7 +453,7 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
         constexpr uint32_t kHat = HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
         hhmm_status s = HHMM_OK;
         if (a.outputs & ~kHat)
-            s = launch_iohmm(a, st);
+            s = run_iohmm_filtered(a, st, launch_iohmm);
         if (s == HHMM_OK && (a.outputs & kHat))
             s = launch_fitted(a, st);
         return s;

@@ -87,6 +87,8 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
     const bool fixed_init = (a.model == HHMM_MODEL_IOHMM_HMIX); /* iohmm-hmix.stan:166-167 */
     const bool log_A_out = (a.model == HHMM_MODEL_IOHMM_HMIX || a.model == HHMM_MODEL_IOHMM_HMIX_LITE);
     const bool need_lA = want_vit || (log_A_out && (out & HHMM_OUT_LOGA) && a.logA);
+    const bool gate = (out & kIoFilt) && a.io_redo; /* iohmm_sweep's underflow check (group-uniform) */
+    bool weak = false;
 
     /* ---- state jj's parameters ---- */
     const double pj = a.p_1k[d + S * jj];
@@ -281,15 +283,20 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
             double ua_base = 0.0, fj;
             if (t == 0) {
                 fj = on ? pj * e : 0.0;
+                weak = gate && !(grp_max<G>(fj) >= kIoWeak);
             } else {
                 const double s = grp_sum<G>(on ? f * A : 0.0);
                 ua_base = log(s) + (lsc + kLn2 * ex);
                 fj = e * s;
-                if (out & HHMM_OUT_UNBETA) { /* log c_t = m + log sum_i A_t(i) e_t(i) (:94) */
+                weak |= gate && !(s >= kIoWeak);
+                if (out & kIoBack) { /* log c_t = m + log sum_i A_t(i) e_t(i) (:94) */
                     const double c = grp_sum<G>(on ? A * e : 0.0);
-                    lam += m + log(c);
-                    if (j == 0)
-                        a.lam[p + a.P * (int64_t)t] = lam;
+                    weak |= gate && !(c >= kIoWeak);
+                    if (out & HHMM_OUT_UNBETA) {
+                        lam += m + log(c);
+                        if (j == 0)
+                            a.lam[p + a.P * (int64_t)t] = lam;
+                    }
                 }
             }
             lsc += m;
@@ -356,6 +363,8 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
             a.z_ffbs[p + a.P * (int64_t)(Tp - 1)] = z + 1;
         return;
     }
+    if (weak && j == 0 && (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G < a.P)
+        a.io_redo[1 + atomicAdd(&a.io_redo[0], 1)] = (int32_t)p; /* re-run in log space (launch_iohmm_log) */
     if ((out & HHMM_OUT_LOGLIK) && a.loglik) { /* target += log_sum_exp(unalpha_tk[T]) (iohmm-reg.stan:120) */
         const double fs = grp_sum<G>(f);
         if (j == 0)

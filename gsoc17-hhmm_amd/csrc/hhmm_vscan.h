@@ -1158,7 +1158,7 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
         e = hipMemsetAsync(a.vs_tl, 0, sizeof(int32_t), st); /* the tie list's count */
     if (e == hipSuccess) {
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, false>), gc, bc, lds_c, st, a);
-        if (getenv("HHMM_PROBE_VS_SCAN0_SERIAL")) /* probe knob: the serial approximate walk */
+        if (probe_env("HHMM_PROBE_VS_SCAN0_SERIAL")) /* probe knob: the serial approximate walk */
             hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K, false>), dim3((unsigned)a.P), b64, lds_s, st, a);
         else
             hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K, true>), dim3((unsigned)a.P), b64, lds_s, st, a);
@@ -1178,7 +1178,7 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
         hipLaunchKernelGGL((viterbi_sp_kernel<MODEL, K>), dim3((unsigned)((4 * a.P + 63) / 64)), dim3(64), lds, st, r);
         e = hipGetLastError();
     }
-    if (e == hipSuccess && getenv("HHMM_PROBE_VS_STATS")) {
+    if (e == hipSuccess && probe_env("HHMM_PROBE_VS_STATS")) {
         /* probe: chunks the exact scan decoded step by step, and replay failures */
         std::vector<int32_t> k((size_t)a.P * a.vs_nc), f((size_t)a.P);
         e = hipStreamSynchronize(st);

@@ -250,4 +250,6 @@ def declare(lib):
     lib.hhmm_selftest_det_log.restype = C.c_int
     lib.hhmm_selftest_det_exp.argtypes = [F64P, F64P, C.c_int64]
     lib.hhmm_selftest_det_exp.restype = C.c_int
+    lib.hhmm_selftest_shards.argtypes = [RP, SP, C.c_int]
+    lib.hhmm_selftest_shards.restype = C.c_int
     return lib

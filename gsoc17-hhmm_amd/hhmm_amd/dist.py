@@ -170,15 +170,29 @@ def gqs_tsplit(model, data, draws, pars, group=None, pairing="grid", lib=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     x = np.atleast_2d(np.asarray(data["x_t" if "x_t" in data else "x"]))
+    if x.shape[-1] < world:  # every rank holds the same data, so every rank raises here
+        raise ValueError(f"gqs_tsplit: T = {x.shape[-1]} is shorter than the world size {world}")
     wins = segment.windows(x.shape[-1], world)
     t0, t1 = wins[rank]
-    lib = lib or api.load_library()
-    win = segment.SegmentWindow(lib, model, segment.slice_time(data, t0, t1), draws,
-                                list(dict.fromkeys(["loglik"] + list(pars))), rank == 0, rank == world - 1,
-                                pairing)
-    s = win.summary()
-    torch.cuda.synchronize(win.dev)
     dev = default_device(group)
+    # a rank whose window fails must not leave the others waiting in all_gather:
+    # agree on success first
+    err, s, win = None, None, None
+    try:
+        lib = lib or api.load_library()
+        win = segment.SegmentWindow(lib, model, segment.slice_time(data, t0, t1), draws,
+                                    list(dict.fromkeys(["loglik"] + list(pars))), rank == 0, rank == world - 1,
+                                    pairing)
+        s = win.summary()
+        torch.cuda.synchronize(win.dev)
+    except Exception as ex:  # re-raised below, after every rank knows
+        err = ex
+    failed = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
+    dist.all_reduce(failed, op=dist.ReduceOp.MAX, group=group)
+    if err is not None:
+        raise err
+    if int(failed.item()):
+        raise RuntimeError("gqs_tsplit: the window of another rank failed")
     s = s.to(dev)
     gathered = [torch.empty_like(s) for _ in range(world)]
     dist.all_gather(gathered, s, group=group)

@@ -357,6 +357,15 @@ hhmm_status hhmm_selftest_cr_exp(const double *in, double *out, int64_t n);
 hhmm_status hhmm_selftest_det_log(const double *in, double *out, int64_t n);
 hhmm_status hhmm_selftest_det_exp(const double *in, double *out, int64_t n);
 
+/* Host-only self-test of the device-set sharding (HHMM_DEVICE_SET; no GPU
+ * used): splits the request over `nshards` shards exactly as hhmm_run does,
+ * moves every input array's slices into packed shard buffers and back, and
+ * adds 1 to every element of every requested output through the same slice
+ * copies.  A caller that zero-fills the outputs then finds each element equal
+ * to 1 iff the shards cover every output element exactly once (driven under
+ * host ASan / UBSan by tools/sanitize.sh). */
+hhmm_status hhmm_selftest_shards(const hhmm_request *req, hhmm_result *res, int nshards);
+
 #ifdef __cplusplus
 }
 #endif

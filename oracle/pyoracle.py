@@ -6,6 +6,7 @@ uses the product's request builder (hhmm_amd.api.PreparedRequest) so both
 sides see byte-identical inputs, and returns results in the same layout.
 """
 import ctypes as C
+import os
 import pathlib
 import subprocess
 import sys
@@ -29,6 +30,11 @@ def load(variant="cr"):
     if variant in _LIBS:
         return _LIBS[variant]
     name = {"cr": "liboracle.so", "libm": "liboracle_libm.so"}[variant]
+    if os.environ.get("HHMM_ORACLE_SAN") == "1":  # the ASan + UBSan build (tools/sanitize.sh)
+        name = name.replace(".so", "_san.so")
+        path = ROOT / "build" / name
+        if not path.exists():
+            subprocess.run(["make", "-s", "-C", str(ROOT), "sanitize"], check=True)
     path = ROOT / "build" / name
     if not path.exists():
         build()

@@ -175,3 +175,19 @@ def test_library_is_built_from_these_sources(engine):
     it must be this tree's (a stale or foreign build fails here)."""
     v = engine.hhmm_version().decode()
     assert v.split(" src ")[-1] == _source_hash(), (v, _source_hash())
+
+
+def test_segment_summary_validates_the_request_before_launching(engine):
+    """the summary call of a segment window checks the request side
+    (draw and data pointers) before any launch, so a NULL draw array is an
+    argument error, not a device fault -- reported even without a GPU."""
+    from hhmm_amd import segment
+    segment.declare(engine)
+    pr = _prepared("hmm")
+    pr.req.outputs = _abi.OUT["loglik"] | _abi.OUT["gamma_tk"]
+    pr.req.data.T = None
+    pr.req.draws.A_ij = None
+    seg = segment.Segment(1, 1, 0x1000, None, None)
+    st = engine.hhmm_segment_summary_device(C.byref(pr.req), C.byref(seg), None, 0, None)
+    assert st == _abi.ERR_INVALID_ARGUMENT
+    assert b"A_ij" in engine.hhmm_last_error()

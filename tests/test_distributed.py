@@ -142,3 +142,48 @@ def test_shard_range_covers_everything():
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             sizes = [e - b for b, e in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _tsplit_worker(rank, world, port, T, q):
+    import sys
+    import pathlib
+    repo = pathlib.Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(repo / "gsoc17-hhmm_amd"), str(repo / "oracle")]
+    import torch.distributed as dist
+    from hhmm_amd import dist as hdist, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        try:
+            data, draws = synth.GENERATORS["hmm"](N=1, S=3, T=T)
+            hdist.gqs_tsplit("hmm", data, draws, ["loglik", "gamma_tk"])
+            q.put((rank, "ok"))
+        except Exception as ex:  # noqa: BLE001 -- the test inspects what each rank raised
+            q.put((rank, type(ex).__name__))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("T", [1, 40])
+def test_gqs_tsplit_fails_on_every_rank_without_hanging(T):
+    """a rank whose window fails (T shorter than the world; here on
+    the CPU box also no gfx950 device) must not leave the other rank waiting in
+    all_gather.  Both ranks raise, and the test ends within the queue timeout."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tsplit_worker, args=(r, world, port, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    if T == 1:
+        assert got == {0: "ValueError", 1: "ValueError"}
+    else:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present: the windows succeed")
+        assert "ok" not in got.values() and set(got) == {0, 1}

@@ -67,13 +67,13 @@ def test_iohmm_large_K_profiles(engine, oracle, model, pars):
 def test_iohmm_large_K_softmax_regimes(engine, oracle, scale):
     """Mild to saturated transitions (one state takes A = 1 - tiny): the
     sequential softmax and the correctly rounded log A stay bit-exact.  At
-    scale 400 the linear-space filter is left out: there A_t underflows to 0
-    on every state the filter's renormalised mass sits on, so s_t = 0 and the
-    loglik is -inf, while the reference's log space keeps the states below
-    1e-308 of the max finite."""
+    scale 400 A_t underflows to 0 on every state the linear filter's
+    renormalised mass sits on (s_t = 0; tests/test_iohmm_underflow.py), and
+    the pairs' filter outputs come from the log-space re-run
+    (hhmm_iolog.hip), finite like the reference's."""
     data, draws = synth.iohmm_reg(N=2, S=6, T=120, K=16, M=4)
     draws["w_km"] = draws["w_km"] * scale
-    pars = ["zstar_t", "logp_zstar", "logA_ij"] + (["loglik"] if scale < 400 else [])
+    pars = ["zstar_t", "logp_zstar", "logA_ij", "loglik", "alpha_tk", "unbeta_tk"]
     run_both(engine, oracle, "iohmm-reg", data, draws, pars)
 
 

@@ -1,0 +1,44 @@
+"""CPU: the device-set sharding of hhmm_run (HHMM_DEVICE_SET; hhmm_api.cpp
+make_shards / shard_rows) covers every output element exactly once, for every
+pairing, with draw splits (GRID with fewer series than shards), ragged T and
+every array class (series, draws, pairs).  hhmm_selftest_shards runs the
+shard plan and the slice copies on host buffers only, so this runs without a
+GPU -- and under host ASan / UBSan in tools/sanitize.sh."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from hhmm_amd import _abi, api, synth
+
+CASES = [
+    ("hmm-multinom", "grid", dict(N=5, S=4)),
+    ("hmm-multinom", "grid", dict(N=2, S=7)),      # fewer series than shards: split the draws
+    ("hmm-multinom", "zip", dict(N=6, S=6)),
+    ("hmm-multinom", "block", dict(N=3, S=9)),
+    ("iohmm-hmix", "grid", dict(N=3, S=5)),
+    ("hhmm-tayal2009-lite", "grid", dict(N=4, S=3)),
+]
+
+
+@pytest.mark.parametrize("nshards", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("model,pairing,sizes", CASES)
+def test_shards_cover_every_output_element_once(engine, model, pairing, sizes, nshards):
+    data, draws = synth.GENERATORS[model](T=23, **sizes)
+    data["T"] = np.array([23 - 3 * (i % 4) for i in range(sizes["N"])], dtype=np.int32)
+    pars = [p for p in synth.PARS[model] if p not in ("oblik_tk",)]
+    pr = api.PreparedRequest(model, data, draws, pars, pairing)
+    for a in pr.out.values():
+        a[...] = 0
+    assert engine.hhmm_selftest_shards(C.byref(pr.req), C.byref(pr.res), nshards) == _abi.OK, \
+        engine.hhmm_last_error()
+    for name, a in pr.out.items():
+        assert np.all(a == 1), (name, np.unique(a))
+
+
+def test_shard_selftest_rejects_bad_requests(engine):
+    data, draws = synth.GENERATORS["hmm-multinom"](N=2, S=3, T=5)
+    pr = api.PreparedRequest("hmm-multinom", data, draws, ["loglik"])
+    assert engine.hhmm_selftest_shards(C.byref(pr.req), C.byref(pr.res), 0) == _abi.ERR_INVALID_ARGUMENT
+    pr.res.loglik = None
+    assert engine.hhmm_selftest_shards(C.byref(pr.req), C.byref(pr.res), 2) == _abi.ERR_INVALID_ARGUMENT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Builds libhhmm.so from a git revision (or the working tree with REV=WT) into
 # gsoc17-hhmm_amd/lib/variants/libhhmm_NAME.so, for tools/ab_bench.py.
-# Usage: tools/build_variant.sh NAME REV [extra hipcc flags...]
+# Usage: tools/build_variant.sh NAME REV [make variables, e.g. EXTRA="-DHHMM_PROBES" for the HHMM_PROBE_* knobs]
 set -e
 NAME=$1; REV=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
