@@ -420,20 +420,30 @@ def cpu_baseline(T, target_s, seed):
             "cpu_model": cpu_model()}
 
 
-def load_traffic(kernel, P, T):
+def lib_src(lib):
+    """The source hash the loaded libhhmm.so was built from (hhmm_version)."""
+    return lib.hhmm_version().decode().split(" src ")[-1]
+
+
+def load_traffic(kernel, P, T, src):
     """HBM bytes per launch of `kernel` from the committed PMC passes
     (profiles/bench_traffic.json, written by tools/prof_summary.py from
     rocprofv3 FETCH_SIZE / WRITE_SIZE, gfx950 correction applied), when they
-    were taken on this batch shape; else None."""
+    were taken on this batch shape AND on the library build now loaded
+    (`src`, VERDICT r3: evidence keyed to the build it measured).  Returns
+    (bytes or None, source note)."""
     p = ROOT / "profiles" / "bench_traffic.json"
     try:
         bt = json.loads(p.read_text())
     except Exception:
-        return None
+        return None, "no profiles/bench_traffic.json"
     if bt.get("pairs") != P or bt.get("T") != T:
-        return None
+        return None, f"PMC pass taken at pairs={bt.get('pairs')} T={bt.get('T')}, not this shape"
+    if bt.get("src") != src:
+        return None, f"PMC pass measured build src {bt.get('src')}, the loaded library is src {src}"
     k = bt.get("kernels", {}).get(kernel)
-    return k.get("hbm_bytes_per_launch") if k else None
+    note = f"{bt.get('source')} (build src {src})"
+    return (k.get("hbm_bytes_per_launch") if k else None), note
 
 
 def main():
@@ -517,10 +527,11 @@ def c2_workload(a, lib, rk):
         units = P * T
         sched = SCHEDULE_KERNELS[name if name != "step" else DEFAULT_SCHEDULE]
         dom = sched[0]
+        src = lib_src(run.lib)
         if "+" not in dom:
-            traffic = load_traffic(dom, P, T)
+            traffic, pmc_note = load_traffic(dom, P, T, src)
         else:
-            t1, t2 = load_traffic("fb_kernel", P, T), load_traffic("viterbi_kernel", P, T)
+            (t1, pmc_note), (t2, _) = load_traffic("fb_kernel", P, T, src), load_traffic("viterbi_kernel", P, T, src)
             traffic = (t1 + t2) if (t1 is not None and t2 is not None) else None
         achieved = whole_b * units / (step_ms * 1e-3)
         value = world * units * a.steps / elapsed
@@ -544,8 +555,10 @@ def c2_workload(a, lib, rk):
             "whole_step_roofline_frac": whole_b * world * units * a.steps / elapsed / (HBM_PEAK * world),
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": traffic, "algorithmic_bytes_per_series_timestep": whole_b,
+                         "traffic": traffic, "pmc_source": pmc_note,
+                         "algorithmic_bytes_per_series_timestep": whole_b,
                          "duration_ms": step_ms},
+            "library": run.lib.hhmm_version().decode(),
             "rank_ms_per_step": [x / a.steps * 1e3 for x in per_rank],
             "rank_kernel_ms": rank_step_ms,
             "path_gather": gather,
@@ -669,23 +682,30 @@ F64_PEAK = 78.6e12      # FLOP/s, MI355X fp64 vector and fp64 matrix (dense) pea
 VALU_ISSUE = 1024 * 2.4e9 / 4.0  # wave-instructions/s: 1024 SIMDs x 2.4 GHz, 4 cycles per fp64-rate VALU op
 
 
-def load_workload_pmc(name):
+def load_workload_pmc(name, src):
     """Per-step PMC totals of workload `name` (tools/pmc_workloads.sh ->
-    tools/workload_pmc.py -> profiles/bench_traffic.json["workloads"]), or {}."""
+    tools/workload_pmc.py -> profiles/bench_traffic.json["workloads"]) when
+    they were measured on the library build now loaded (`src`); else {} with
+    the reason in "source"."""
     try:
         bt = json.loads((ROOT / "profiles" / "bench_traffic.json").read_text())
-        return bt.get("workloads", {}).get(name, {}) or {}
+        pm = bt.get("workloads", {}).get(name, {}) or {}
     except Exception:
-        return {}
+        return {"source": "no profiles/bench_traffic.json"}
+    if not pm:
+        return {"source": f"no PMC pass of workload {name}"}
+    if pm.get("src") != src:
+        return {"source": f"{pm.get('source')} measured build src {pm.get('src')}, the loaded library is src {src}"}
+    return dict(pm, source=f"{pm.get('source')} (build src {src})")
 
 
-def compute_rooflines(name, B, units, dev_ms, algo_flops=None):
+def compute_rooflines(name, B, units, dev_ms, src, algo_flops=None):
     """HBM roofline of the whole request (algorithmic bytes over the live
     duration) beside the VALU and, where the request uses the matrix cores,
     the f64-MFMA ones: the committed PMC instruction counts per step over the
     same live duration.  `bound` names the larger fraction."""
     t = dev_ms * 1e-3
-    pm = load_workload_pmc(name)
+    pm = load_workload_pmc(name, src)
     hbm_frac = B * units / t / HBM_PEAK
     r = {"kernel": "whole request", "bound": "hbm", "achieved": B * units / t / 1e9, "peak": HBM_PEAK / 1e9,
          "unit": "GB/s", "frac": hbm_frac, "traffic": pm.get("hbm_bytes_per_step"),
@@ -753,8 +773,9 @@ def other_workload(a, lib, rk):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (hhmm_amd.synth generators, seeded)",
             "config": {"workload": desc, "model": model, "pairs_per_gpu": P, "T": T, "outputs": pars},
-            "roofline": compute_rooflines(a.workload, B, units, dev_ms,
+            "roofline": compute_rooflines(a.workload, B, units, dev_ms, lib_src(lib),
                                           algo_flops=(2.0 * kw["K"] ** 3 * units if a.workload == "n2" else None)),
+            "library": lib.hhmm_version().decode(),
             "rank_ms_per_step": [x / a.steps * 1e3 for x in per_rank],
             "pair_failures": int((status != 0).sum().item()),
         }

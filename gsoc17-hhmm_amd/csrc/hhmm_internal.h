@@ -170,6 +170,9 @@ constexpr uint32_t kIoFilt = HHMM_OUT_LOGLIK | HHMM_OUT_UNALPHA | HHMM_OUT_ALPHA
                              HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA | HHMM_OUT_OBLIK_T;
 constexpr uint32_t kIoBack = HHMM_OUT_UNBETA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
 constexpr double kIoWeak = 0x1p-960;
+/* t = 0: f_0 = p .* e_0 keeps every component above 2^-1074, i.e. down to
+ * 2^-834 (below the 1e-250 tolerance floor) of a max of at least 2^-240 */
+constexpr double kIoWeak0 = 0x1p-240;
 hhmm_status launch_iohmm_log(const DevArgs &a, hipStream_t stream);
 /* Fitted-output draws hatpi / hatz / hatl / hatx (hhmm_fitted.hip). */
 hhmm_status launch_fitted(const DevArgs &a, hipStream_t stream);

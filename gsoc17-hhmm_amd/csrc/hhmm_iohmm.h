@@ -580,7 +580,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 1; k < K; ++k)
                     f0 = fmax(f0, f[k]);
-                weak = gate && !(f0 >= kIoWeak);
+                weak = gate && !(f0 >= kIoWeak0);
             } else {
                 /* num_filter: the softmax numerators, the sum in the log scale
                  * (psum, pex) -- iohmm_sp_sweep's arithmetic, bit for bit */
@@ -594,10 +594,16 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                     pex += pe;
                 }
                 ua_base = log(s) + (lsc + kLn2 * ex);
+                weak |= gate && !(s >= kIoWeak);
+                /* s into [0.5, 1) first (exact): f_t = e_t * s then keeps every
+                 * emission factor e_t(j) the reference's alpha keeps (a tiny s
+                 * would flush e_t(j) * s below the subnormals) */
+                const int es = __builtin_amdgcn_frexp_exp(s);
+                ex += es;
+                const double sn = ldexp(s, -es);
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    f[k] = e[k] * s;
-                weak |= gate && !(s >= kIoWeak);
+                    f[k] = e[k] * sn;
                 /* log c_t = m + log sum_i A_t(i) e_t(i) (backward accumulator, :94) */
                 if (out & kIoBack) {
                     double c = st.A[0] * e[0];
@@ -933,16 +939,19 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
 #pragma unroll
                 for (int k = 1; k < K; ++k)
                     f0 = fmax(f0, f[k]);
-                weak = gate && !(f0 >= kIoWeak);
+                weak = gate && !(f0 >= kIoWeak0);
             } else {
                 double sv = f[0] * AA[0];
 #pragma unroll
                 for (int i = 1; i < K; ++i)
                     sv = fma(f[i], AA[i], sv);
+                weak |= gate && !(sv >= kIoWeak);
+                const int es = __builtin_amdgcn_frexp_exp(sv); /* iohmm_sweep: s into [0.5, 1) first */
+                ex += es;
+                const double sn = ldexp(sv, -es);
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    f[k] = ee[k] * sv;
-                weak |= gate && !(sv >= kIoWeak);
+                    f[k] = ee[k] * sn;
                 if (out & kIoBack) { /* the backward accumulator sum_i A_t(i) e_t(i) (numerators) */
                     double c = AA[0] * ee[0];
 #pragma unroll

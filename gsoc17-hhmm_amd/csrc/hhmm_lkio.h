@@ -283,12 +283,14 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
             double ua_base = 0.0, fj;
             if (t == 0) {
                 fj = on ? pj * e : 0.0;
-                weak = gate && !(grp_max<G>(fj) >= kIoWeak);
+                weak = gate && !(grp_max<G>(fj) >= kIoWeak0);
             } else {
                 const double s = grp_sum<G>(on ? f * A : 0.0);
                 ua_base = log(s) + (lsc + kLn2 * ex);
-                fj = e * s;
                 weak |= gate && !(s >= kIoWeak);
+                const int es = __builtin_amdgcn_frexp_exp(s); /* iohmm_sweep: s into [0.5, 1) first */
+                ex += es;
+                fj = e * ldexp(s, -es);
                 if (out & kIoBack) { /* log c_t = m + log sum_i A_t(i) e_t(i) (:94) */
                     const double c = grp_sum<G>(on ? A * e : 0.0);
                     weak |= gate && !(c >= kIoWeak);

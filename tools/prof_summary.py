@@ -26,6 +26,23 @@ from collections import defaultdict
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 
 
+def run_src(d):
+    """The libhhmm build (source hash) the profiled run loaded: the "library"
+    field of bench.py's JSON line(s) in the run's logs under `d`, or None."""
+    srcs = set()
+    for path in glob.glob(str(pathlib.Path(d) / "**" / "*.log"), recursive=True):
+        for ln in open(path, errors="replace"):
+            ln = ln.strip()
+            if ln.startswith("{") and '"library"' in ln:
+                try:
+                    srcs.add(json.loads(ln)["library"].split(" src ")[-1])
+                except Exception:
+                    pass
+    if len(srcs) > 1:
+        raise SystemExit(f"{d}: runs of different builds {sorted(srcs)}")
+    return srcs.pop() if srcs else None
+
+
 def short(name):
     if "hhmm::" in name:
         return name.split("(")[0].replace("void ", "")
@@ -109,6 +126,9 @@ def main():
                            "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
                            "correction": "FETCH_SIZE doubled (gfx950, MI355X_MICROARCH.md §HBM)"}
         if summ:
+            src = run_src(d)
+            for v in summ.values():
+                v["src"] = src
             (out / f"{tag}_pmc_traffic.json").write_text(json.dumps(summ, indent=1))
             print("wrote", out / f"{tag}_pmc_traffic.json")
             # the bench's roofline.traffic: HBM bytes per launch of each bench kernel,
@@ -118,7 +138,7 @@ def main():
                 shape = json.loads(sys.argv[3])
             bp = out / "bench_traffic.json"
             old = json.loads(bp.read_text()) if bp.exists() else {}
-            bt = {"source": f"profiles/{tag}_pmc_traffic.json", **shape, "kernels": {}}
+            bt = {"source": f"profiles/{tag}_pmc_traffic.json", "src": src, **shape, "kernels": {}}
             if "workloads" in old:  # the evidence workloads' per-step totals (tools/workload_pmc.py)
                 bt["workloads"] = old["workloads"]
             for k, v in summ.items():

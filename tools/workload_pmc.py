@@ -23,6 +23,23 @@ from collections import defaultdict
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 
 
+def run_src(d):
+    """The libhhmm build (source hash) the profiled run loaded: the "library"
+    field of bench.py's JSON line(s) in the run's logs under `d`, or None."""
+    srcs = set()
+    for path in glob.glob(str(pathlib.Path(d) / "**" / "*.log"), recursive=True):
+        for ln in open(path, errors="replace"):
+            ln = ln.strip()
+            if ln.startswith("{") and '"library"' in ln:
+                try:
+                    srcs.add(json.loads(ln)["library"].split(" src ")[-1])
+                except Exception:
+                    pass
+    if len(srcs) > 1:
+        raise SystemExit(f"{d}: runs of different builds {sorted(srcs)}")
+    return srcs.pop() if srcs else None
+
+
 def short(name):
     return name.split("(")[0].replace("void ", "") if "hhmm::" in name else None
 
@@ -68,7 +85,7 @@ def main():
             for n in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_MFMA_F64", "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_INSTS_SALU"):
                 if n in c:
                     step[n] += per_step * c[n]
-        out[d.name] = {"kernels": ks, "per_step": dict(step)}
+        out[d.name] = {"kernels": ks, "per_step": dict(step), "src": run_src(d)}
     prof = ROOT / "profiles"
     (prof / f"{tag}_workloads_pmc.json").write_text(json.dumps(out, indent=1))
     bt_path = prof / "bench_traffic.json"
@@ -76,7 +93,7 @@ def main():
     wl = bt.setdefault("workloads", {})
     for w, v in out.items():
         ps = v["per_step"]
-        wl[w] = {"source": f"profiles/{tag}_workloads_pmc.json",
+        wl[w] = {"source": f"profiles/{tag}_workloads_pmc.json", "src": v["src"],
                  "hbm_bytes_per_step": ps.get("hbm_bytes"), "valu_insts_per_step": ps.get("SQ_INSTS_VALU"),
                  "mfma_f64_insts_per_step": ps.get("SQ_INSTS_VALU_MFMA_F64"),
                  "kernel_ns_per_step": ps.get("kernel_ns")}
