@@ -234,6 +234,19 @@ __device__ __forceinline__ int wave_max(int v)
     return __builtin_amdgcn_readfirstlane(v);
 }
 
+/* XCD-aware workgroup order (cdna_hip_programming.md T1; speed only, never
+ * correctness): workgroups are dealt round-robin over the 8 XCDs, so blocks b
+ * and b + 8 share an L2.  This bijection gives each XCD a contiguous range of
+ * logical blocks, so neighbouring pairs -- whose 8-byte output stores share
+ * 128-byte lines when a group of lanes owns a pair -- are written through one
+ * L2 and leave it as whole lines. */
+__device__ __forceinline__ int64_t xcd_block()
+{
+    const int64_t nb = gridDim.x, b = blockIdx.x;
+    const int64_t x = b & 7, q = nb >> 3, r = nb & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 __device__ __forceinline__ void pair_coords(const DevArgs &a, int64_t p, int64_t &n, int64_t &d)
 {
     if (a.pairing == HHMM_PAIR_ZIP) {

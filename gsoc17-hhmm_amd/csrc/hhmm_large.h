@@ -41,6 +41,9 @@
 
 namespace hhmm {
 
+#ifndef HHMM_LK_XCD
+#define HHMM_LK_XCD 1 /* build knob: XCD-contiguous pair ranges (lk_group) */
+#endif
 constexpr int kLChunk = 8;  /* steps per forward checkpoint */
 constexpr int kLBack = 16;  /* backtrack steps per back-pointer chunk */
 /* The filters renormalise (a group max, an exact power of two) every kLRenorm
@@ -136,11 +139,23 @@ struct LkLane {
     bool dense;        /* wave-uniform: renormalise every step (kLRenormSafeBound) */
 };
 
-/* The group index of this lane's group (blockIdx.x * groups per block + group), clamped to nq - 1. */
+/* The group index of this lane's group (workgroup * groups per block + group;
+ * lk_group: clamped to nq - 1). */
+template <int G>
+__device__ __forceinline__ int64_t lk_group_raw()
+{
+#if HHMM_LK_XCD
+    /* a wave holds two or four pairs, so a gamma / alpha row's 128-byte line
+     * (16 pairs) spans 4-8 waves of 2 workgroups: keep them on one XCD */
+    return xcd_block() * (blockDim.x / G) + threadIdx.x / G;
+#else
+    return (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
+#endif
+}
 template <int G>
 __device__ __forceinline__ int64_t lk_group(int64_t nq)
 {
-    return min((int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G, nq - 1);
+    return min(lk_group_raw<G>(), nq - 1);
 }
 
 template <int MODEL, int G, int KM>
@@ -425,7 +440,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     bcur = bnxt;
     double al = 0.0, lsc = 0.0;
     int ex = 0;
-    if (t0 > 0) {
+    if (t0 > 0 || (scan && a.seg_nofirst)) { /* a segment window's chunk 0 enters too */
         al = (ln.on && t0 < t1) ? a.sc_st[sbase] : 0.0;
         lsc = t0 < t1 ? a.sc_sl[(int64_t)pq * a.scan_nc + cq] : 0.0;
     }
@@ -438,7 +453,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         int x;
         double xr, m;
         lk_get<MODEL, G>(bcur, u, x, xr);
-        if (t == 0) {
+        if (t == 0 && !a.seg_nofirst) {
             if constexpr (LkTraits<MODEL>::kGauss) {
                 /* log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k): alpha_1 = p_1k */
                 const double z = (xr - ln.mu) * ln.isig;

@@ -365,7 +365,7 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
             a.z_ffbs[p + a.P * (int64_t)(Tp - 1)] = z + 1;
         return;
     }
-    if (weak && j == 0 && (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G < a.P)
+    if (weak && j == 0 && lk_group_raw<G>() < a.P)
         a.io_redo[1 + atomicAdd(&a.io_redo[0], 1)] = (int32_t)p; /* re-run in log space (launch_iohmm_log) */
     if ((out & HHMM_OUT_LOGLIK) && a.loglik) { /* target += log_sum_exp(unalpha_tk[T]) (iohmm-reg.stan:120) */
         const double fs = grp_sum<G>(f);

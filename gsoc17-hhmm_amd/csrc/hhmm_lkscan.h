@@ -160,7 +160,10 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
                 const int t = t0[u] + s;
-                const bool on = t >= 1 && t < t1[u];
+                /* t = 0 is the init (phase 2 applies p_1k .* phi), except in a
+                 * segment window that starts inside the series: there every
+                 * step is a transition */
+                const bool on = (t >= 1 || a.seg_nofirst) && t < t1[u];
                 const int xc = min(max(xb[u][v], 1), a.L);
                 const double *row = tab + (xc - 1) * KR + (lane >> 4);
                 double nv[KSM];
@@ -262,16 +265,24 @@ __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
     /* exponent of a row: frexp exponent of the value + the row's scale; INT_MIN/2 for a zero */
     constexpr int kDead = -(1 << 29);
 
-    /* ---- forward: f_0 = p_1k .* phi[., x_1] (hmm-multinom.stan:31), then f <- f M_c ---- */
-    const int x0 = min(max(a.x[n], 1), a.L);
-    double f = on ? a.p_1k[d + S * jj] * a.phi_k[d + S * ((int64_t)jj + (int64_t)K * (x0 - 1))] : 0.0;
+    /* ---- forward: f_0 = p_1k .* phi[., x_1] (hmm-multinom.stan:31), then f <- f M_c;
+     * a segment window that starts inside the series enters from the caller's
+     * state (seg_enter: K values up to scale, then their log scale) ---- */
+    double f, lsc = 0.0;
+    if (!a.seg_nofirst) {
+        const int x0 = min(max(a.x[n], 1), a.L);
+        f = on ? a.p_1k[d + S * jj] * a.phi_k[d + S * ((int64_t)jj + (int64_t)K * (x0 - 1))] : 0.0;
+    } else {
+        f = on ? a.seg_enter[p + a.P * (int64_t)jj] : 0.0;
+        lsc = a.seg_enter[p + a.P * (int64_t)K];
+    }
     int fe = __builtin_amdgcn_frexp_exp(wmax_d(f));
     f = ldexp(f, -fe);
-    double lsc = kLn2 * fe;
+    lsc += kLn2 * fe;
     double rb[NV];
     lks_stage_load<KM>(a, p, 0, rb);
     for (int c = 0; c < ncp; ++c) {
-        if (c > 0 && on) {
+        if ((c > 0 || a.seg_nofirst) && on) {
             a.sc_st[base(c) * K + j] = f;
             if (j == 0)
                 a.sc_sl[base(c)] = lsc;
@@ -298,11 +309,13 @@ __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
         lsc += kLn2 * ((double)(em == kDead ? 0 : em) + e2);
     }
     const double sf = wsum_d(on ? f : 0.0);
-    if (j == 0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
+    if (j == 0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
         a.loglik[p] = log(sf) + lsc;
 
-    /* ---- backward: beta_T = 1 (unbeta_tk[T] = 1, Q1); b_{c-1} = M_c b_c ---- */
-    double b = on ? 1.0 : 0.0;
+    /* ---- backward: beta_T = 1 (unbeta_tk[T] = 1, Q1), or the beta leaving a
+     * segment window (the caller's; its scale cancels in the posteriors);
+     * b_{c-1} = M_c b_c ---- */
+    double b = on ? (a.seg_nolast ? a.seg_leave[p + a.P * (int64_t)jj] : 1.0) : 0.0;
     if (on && ncp > 0)
         a.sc_be[base(ncp - 1) * K + j] = b;
     lks_stage_load<KM>(a, p, ncp - 1, rb);
@@ -327,6 +340,136 @@ __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
         b = (er == kDead || em == kDead) ? 0.0 : ldexp(h, (int)sr - em);
         if (on)
             a.sc_be[base(c - 1) * K + j] = b;
+    }
+}
+
+/* ---- Segment summary at large K (include/hhmm.h hhmm_segment; SURVEY §8e,
+ * the flattened-HHMM shape: few pairs, 23 states, T = 10^6 split along T over
+ * ranks).  hmm-multinom has no masks, so the window's forward product and its
+ * backward product are the same matrix: SF = SQ = M_0 M_1 ... with
+ * M_c = diag(2^s) M'_c the chunk products of lks_prod_kernel (row exponents
+ * s).  One wave per pair: the running product S (K x K, one power-of-two
+ * exponent E) and the chunk's M' sit in LDS; lane l owns column l & 31 of S
+ * for the rows of parity l >> 5.  Each chunk scales the columns of S by
+ * 2^(s_k - max s) (exact while no entry underflows: rows more than 2^1074
+ * below the largest are dropped, as lks_bound_kernel drops them), multiplies
+ * by M'_c in state order, and renormalises by the exact power of two of the
+ * largest entry.  The first window's rows all hold the state leaving it
+ * (p_1k .* phi[., x_1] times S): the layout of the K <= 8 summary
+ * (seg_summary_kernel), so hhmm_amd.segment.boundaries chains both. ---- */
+template <int KM>
+__global__ void __launch_bounds__(64) lks_seg_summary_kernel(const DevArgs a)
+{
+    __shared__ double Sm[KM * KM];
+    __shared__ double Mt[KM * KM];
+    __shared__ double fk[KM];
+    constexpr int RH = (KM + 1) / 2; /* rows per lane */
+    constexpr int kDead = -(1 << 29);
+    const int64_t p = blockIdx.x;
+    const int l = threadIdx.x;
+    const int K = a.K, nc = a.scan_nc, cl = a.scan_cl;
+    const int col = l & 31, h = l >> 5;
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int ncp = (Tp + cl - 1) / cl;
+    const int64_t S = a.S;
+    auto base = [&](int c) { return ((int64_t)p * nc + c); };
+    auto wmax_i = [&](int v) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+            v = max(v, __shfl_xor(v, off));
+        return v;
+    };
+    auto wmax_d = [&](double v) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+            v = fmax(v, __shfl_xor(v, off));
+        return v;
+    };
+    /* the chunk's row exponents: fk[k] = 2^(s_k - smax) (0 for a dead row); returns smax */
+    auto stage = [&](int c) {
+        for (int idx = l; idx < K * K; idx += 64)
+            Mt[idx] = a.sc_mf[base(c) * K * K + idx];
+        const double s = l < K ? a.sc_mx[base(c) * K + l] : dev_ninf();
+        const int si = (s == dev_ninf()) ? kDead : (int)s;
+        const int smax = wmax_i(si);
+        if (l < K)
+            fk[l] = (si == kDead || smax == kDead) ? 0.0 : ldexp(1.0, si - smax);
+        return smax == kDead ? 0 : smax;
+    };
+    double r[RH];
+    int E = 0;
+    /* S = M_0 */
+    E = stage(0);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RH; ++q) {
+        const int i = 2 * q + h;
+        r[q] = (i < K && col < K) ? Mt[i * K + col] * fk[i] : 0.0;
+    }
+    for (int c = 1; c <= ncp; ++c) {
+        /* renormalise the new rows, then publish them */
+        double m = 0.0;
+#pragma unroll
+        for (int q = 0; q < RH; ++q)
+            m = fmax(m, r[q]);
+        const int e = __builtin_amdgcn_frexp_exp(wmax_d(m));
+        E += e;
+        __syncthreads(); /* every lane is done reading Sm and Mt */
+#pragma unroll
+        for (int q = 0; q < RH; ++q) {
+            const int i = 2 * q + h;
+            if (i < K && col < K)
+                Sm[i * K + col] = ldexp(r[q], -e);
+        }
+        if (c == ncp)
+            break;
+        E += stage(c);
+        __syncthreads();
+        /* new S[i][col] = sum_k (S[i][k] 2^(s_k - smax)) M'_c[k][col] */
+#pragma unroll
+        for (int q = 0; q < RH; ++q) {
+            const int i = 2 * q + h;
+            double acc = 0.0;
+            if (i < K && col < K)
+                for (int k = 0; k < K; ++k)
+                    acc = fma(Sm[i * K + k] * fk[k], Mt[k * K + col], acc);
+            r[q] = acc;
+        }
+    }
+    __syncthreads();
+    const int KK = K * K;
+    double *out = a.seg_sum;
+    for (int idx = l; idx < KK; idx += 64) /* SQ = the product (beta entering = SQ beta leaving) */
+        out[p + a.P * (int64_t)(KK + idx)] = Sm[idx];
+    int fex = E;
+    if (!a.seg_nofirst) {
+        /* the first window: every row holds p_1k .* phi[., x_1] (hmm-multinom.stan:31) times S */
+        const int x0 = min(max(a.x[n], 1), a.L);
+        const double f0 = (l < K) ? a.p_1k[d + S * l] * a.phi_k[d + S * ((int64_t)l + (int64_t)K * (x0 - 1))] : 0.0;
+        const int fe = __builtin_amdgcn_frexp_exp(wmax_d(f0));
+        if (l < K)
+            fk[l] = ldexp(f0, -fe);
+        __syncthreads();
+        double g = 0.0;
+        if (l < K)
+            for (int k = 0; k < K; ++k)
+                g = fma(fk[k], Sm[k * K + l], g);
+        const int e2 = __builtin_amdgcn_frexp_exp(wmax_d(l < K ? g : 0.0));
+        g = ldexp(g, -e2);
+        fex = E + fe + e2;
+        if (l < K)
+            for (int i = 0; i < K; ++i)
+                out[p + a.P * (int64_t)(i * K + l)] = g;
+    } else {
+        for (int idx = l; idx < KK; idx += 64)
+            out[p + a.P * (int64_t)idx] = Sm[idx];
+    }
+    if (l == 0) {
+        out[p + a.P * (int64_t)(2 * KK + 0)] = (double)fex;
+        out[p + a.P * (int64_t)(2 * KK + 1)] = 0.0; /* no Gaussian log scale */
+        out[p + a.P * (int64_t)(2 * KK + 2)] = (double)E;
     }
 }
 
@@ -657,6 +800,35 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_UNSUPPORTED;
     }
     const int gpb = threads / G;
+    if (a.seg_phase) {
+        /* one window of a series split over ranks along T (hhmm_segment):
+         * phase 1 + the window's summary, or phases 2 + 3 from the caller's
+         * entering state / leaving beta */
+        if (MODEL != HHMM_MODEL_HMM_MULTINOM || a.scan_cl <= 0) {
+            set_error("segment windows at K = %d > %d: hmm-multinom on the T-scan", a.K, kMaxK);
+            return HHMM_ERR_UNSUPPORTED;
+        }
+        constexpr int RT = (KM + 15) / 16, KSM = KM / 4;
+        if (a.seg_phase == 1) {
+            const int ntile = (a.scan_nc * a.K + 15) / 16;
+            const int64_t waves = a.P * (int64_t)((ntile + kLksTiles - 1) / kLksTiles);
+            const size_t plds = (size_t)4 * a.L * 16 * RT * sizeof(double);
+            hipLaunchKernelGGL((lks_prod_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
+            hipLaunchKernelGGL((lks_seg_summary_kernel<KM>), dim3((unsigned)a.P), dim3(64), 0, st, a);
+        } else {
+            hipLaunchKernelGGL((lks_bound_kernel<KM>), dim3((unsigned)a.P), dim3(64), 0, st, a);
+            const int64_t nq = a.P * (int64_t)a.scan_nc;
+            if (out & (fb & ~HHMM_OUT_LOGLIK))
+                hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)),
+                                   dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_error("large-K segment launch: %s", hipGetErrorString(e));
+            return HHMM_ERR_HIP;
+        }
+        return HHMM_OK;
+    }
     const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
     /* checkpoints use the [rows][K][P] layout of the lane kernels.  With both
      * halves requested the decoder runs on the library's side stream, forked

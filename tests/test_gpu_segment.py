@@ -57,6 +57,35 @@ def test_segments_equal_the_whole_series(engine, oracle, model, R):
         compare(k, got[k], ref[k])
 
 
+@pytest.mark.parametrize("R", [1, 2, 3])
+@pytest.mark.parametrize("K", [16, 23])
+def test_segments_large_K(engine, oracle, K, R):
+    """hmm-multinom at K > 8 (the T-split stopped at K <= 8): the
+    summaries come from the MFMA chunk products (lks_prod_kernel) chained by
+    lks_seg_summary_kernel, the finish from lks_bound_kernel + lk_fb_kernel."""
+    import hhmm_amd
+    data, draws = synth.GENERATORS["hmm-multinom"](N=2, S=3, T=3001, K=K, L=9)
+    pars = ["loglik", "alpha_tk", "beta_tk", "gamma_tk"]
+    got, last = _windows_in_one_process(engine, "hmm-multinom", data, draws, R, pars=pars)
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=pars, nthreads=6)
+    whole = hhmm_amd.gqs("hmm-multinom", data, draws, pars=pars, lib=engine)
+    compare("loglik", got["loglik"], ref["loglik"])
+    compare("loglik", last, ref["loglik"])
+    for k in ("alpha_tk", "beta_tk", "gamma_tk"):
+        compare(k, got[k], whole[k])
+        compare(k, got[k], ref[k])
+
+
+def test_segments_large_K_long_series(engine, oracle):
+    """The N2 shape scaled down: one series of 10^5 steps under 4 draws at
+    K = 23 over 3 windows."""
+    data, draws = synth.GENERATORS["hmm-multinom"](N=1, S=4, T=100_000, K=23, L=9)
+    got, _ = _windows_in_one_process(engine, "hmm-multinom", data, draws, 3, pars=["loglik", "gamma_tk"])
+    ref = oracle.gqs("hmm-multinom", data, draws, pars=["loglik", "gamma_tk"], nthreads=4)
+    compare("loglik", got["loglik"], ref["loglik"])
+    compare("gamma_tk", got["gamma_tk"], ref["gamma_tk"])
+
+
 def test_segments_long_series_few_pairs(engine, oracle):
     """Few pairs, long T: 4 pairs of one series of 2e5 steps over 4 windows,
     against the oracle."""
@@ -80,7 +109,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, out_dir):
+def _rank(rank, world, port, out_dir, model="hmm", kw=None):
     import sys
     import pathlib
     repo = pathlib.Path(__file__).resolve().parent.parent
@@ -93,21 +122,23 @@ def _rank(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        data, draws = synth.GENERATORS["hmm"](N=2, S=3, T=4000)
-        (t0, t1), out, loglik = hdist.gqs_tsplit("hmm", data, draws, ["loglik", "gamma_tk"])
+        data, draws = synth.GENERATORS[model](N=2, S=3, T=4000, **(kw or {}))
+        (t0, t1), out, loglik = hdist.gqs_tsplit(model, data, draws, ["loglik", "gamma_tk"])
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), t0=t0, t1=t1, gamma=out["gamma_tk"], loglik=loglik)
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_gqs_tsplit(engine, oracle, tmp_path):
+@pytest.mark.parametrize("model,kw", [("hmm", {}), ("hmm-multinom", {"K": 23, "L": 9})], ids=["hmm", "multinom-K23"])
+def test_two_ranks_gqs_tsplit(engine, oracle, tmp_path, model, kw):
     """dist.gqs_tsplit at world size 2 over gloo, both ranks on the box's GPU:
     each rank's window of gamma and the loglik every rank chains from the
-    gathered summaries, against the oracle's whole series."""
+    gathered summaries, against the oracle's whole series (K = 23: the large-K
+    summaries, 2K^2 + 3 = 1061 doubles per pair and rank)."""
     port = _free_port()
-    mp.spawn(_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    data, draws = synth.GENERATORS["hmm"](N=2, S=3, T=4000)
-    ref = oracle.gqs("hmm", data, draws, pars=["loglik", "gamma_tk"])
+    mp.spawn(_rank, args=(2, port, str(tmp_path), model, kw), nprocs=2, join=True)
+    data, draws = synth.GENERATORS[model](N=2, S=3, T=4000, **kw)
+    ref = oracle.gqs(model, data, draws, pars=["loglik", "gamma_tk"])
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
     assert int(parts[0]["t1"]) == int(parts[1]["t0"]) and int(parts[1]["t1"]) == 4000
     compare("loglik", parts[0]["loglik"], ref["loglik"])
