@@ -5,12 +5,13 @@ assembly file (where the VALU of the VALU-bound sweeps goes).
   hipcc -O3 -g ... --cuda-device-only -S -o k.s hhmm_io_reg_lo.hip
   python tools/isa_phases.py k.s 'iohmm_reg_kernelILi4ELi4ELi1ELb1E' [source dir, default csrc]
 
-The main loop is the largest backward branch of the kernel; every instruction
-in it is attributed to the source function its `.loc` line falls in (the
-innermost inlined function: dev_cr_exp, softmax_cr_log, io_emission, ...),
-and counted by class (f64 VALU, other VALU, SALU, LDS, VMEM).  Static counts of
-one loop iteration (the t == 0 and store branches included): compare the VALU
-total with the dynamic SQ_INSTS_VALU per wave-step of the PMC passes.
+Loops are the natural loops of the kernel's control-flow graph (basic blocks,
+dominators, back edges); every instruction in a loop body is attributed to
+the source function its `.loc` line falls in (the innermost inlined function:
+dev_cr_exp, softmax_cr_log, io_emission, ...) and counted by class (VALU, SALU,
+LDS, VMEM).  Static counts with every block of the body once (rare branches
+such as t == 0 included): compare the VALU total with the dynamic SQ_INSTS_VALU
+per wave-step of the PMC passes.
 """
 import collections
 import os
@@ -53,55 +54,120 @@ def main():
         if not pat.search(name) or name.startswith("_ZL"):
             continue
         lines = body.split("\n")
-        labels = {}
-        insts = []  # (line index, op, loc)
+        # basic blocks: split at labels and after branches / s_endpgm
+        blocks = []  # [label, [(op, text, loc)], succ labels]
+        cur = [None, []]
         loc = (0, 0)
-        for i, ln in enumerate(lines):
-            s = ln.strip()
-            if not s or s.startswith(";"):
+        order = []
+
+        def close(fall):
+            if cur[1] or cur[0] is not None:
+                blocks.append({"label": cur[0], "insts": cur[1], "fall": fall})
+
+        for ln in lines:
+            s2 = ln.strip()
+            if not s2 or s2.startswith(";"):
                 continue
-            if s.startswith(".loc"):
-                p = s.split()
-                loc = (int(p[1]), int(p[2]))
+            if s2.startswith(".loc"):
+                p2 = s2.split()
+                loc = (int(p2[1]), int(p2[2]))
                 continue
-            if s.endswith(":") and not s.startswith("."):
+            m2 = re.match(r"^(\.LBB\w+):", s2)
+            if m2:
+                close(True)
+                cur = [m2.group(1), []]
                 continue
-            if re.match(r"^\.LBB\w+:", s):
-                labels[s.split(":")[0]] = len(insts)
+            if s2.startswith(".") or s2.endswith(":"):
                 continue
-            if s.startswith("."):
-                continue
-            insts.append((s.split()[0], s, loc))
-        loops = []
-        for k, (op, s, _) in enumerate(insts):
-            if op.startswith("s_cbranch") or op == "s_branch":
-                tgt = s.split()[-1]
-                if tgt in labels and labels[tgt] <= k:
-                    loops.append((k - labels[tgt] + 1, labels[tgt], k))
+            op = s2.split()[0]
+            cur[1].append((op, s2, loc))
+            if op.startswith("s_cbranch") or op in ("s_branch", "s_endpgm", "s_setpc_b64"):
+                close(op.startswith("s_cbranch"))
+                cur = [None, []]
+        close(False)
+        idx = {b["label"]: i for i, b in enumerate(blocks) if b["label"]}
+        succ = []
+        for i, b in enumerate(blocks):
+            sc = []
+            last = b["insts"][-1] if b["insts"] else None
+            if last and (last[0].startswith("s_cbranch") or last[0] == "s_branch"):
+                tgt = last[1].split()[-1]
+                if tgt in idx:
+                    sc.append(idx[tgt])
+            if b["fall"] and i + 1 < len(blocks):
+                sc.append(i + 1)
+            succ.append(sc)
+        n_b = len(blocks)
+        pred = [[] for _ in range(n_b)]
+        for i, sc in enumerate(succ):
+            for j in sc:
+                pred[j].append(i)
+        # blocks reachable from the entry only (cold tails after s_endpgm are not)
+        reach, stack = {0}, [0]
+        while stack:
+            x = stack.pop()
+            for y in succ[x]:
+                if y not in reach:
+                    reach.add(y)
+                    stack.append(y)
+        succ = [[y for y in sc if y in reach] if i in reach else [] for i, sc in enumerate(succ)]
+        pred = [[q for q in ps if q in reach] for ps in pred]
+        # dominators (iterative; entry = block 0)
+        full = set(reach)
+        dom = [full.copy() for _ in range(n_b)]
+        dom[0] = {0}
+        changed = True
+        while changed:
+            changed = False
+            for i in range(1, n_b):
+                if i not in reach:
+                    continue
+                ps = [dom[q] for q in pred[i]]
+                nd = (set.intersection(*ps) if ps else set()) | {i}
+                if nd != dom[i]:
+                    dom[i], changed = nd, True
+        loops = []  # (size, header, body)
+        for u in range(n_b):
+            for h in succ[u]:
+                if h in dom[u]:  # back edge u -> h
+                    body, stack = {h, u}, ([u] if u != h else [])
+                    while stack:
+                        x = stack.pop()
+                        for q in pred[x]:
+                            if q not in body:
+                                body.add(q)
+                                stack.append(q)
+                    loops.append((sum(len(blocks[i]["insts"]) for i in body), h, frozenset(body)))
         if not loops:
             print(f"{name}: no loop")
             continue
-        # outermost loops (not inside a larger one), largest first
-        outer = [(n, a, b) for n, a, b in loops
-                 if not any(a2 <= a and b <= b2 and (a2, b2) != (a, b) for _, a2, b2 in loops)]
-        outer = sorted(set(outer), reverse=True)[:int(os.environ.get("ISA_LOOPS", "3"))]
+        # merge back edges into one loop per header; outermost first
+        by_h = {}
+        for n2, h, body in loops:
+            by_h[h] = by_h.get(h, frozenset()) | body
+        lps = sorted(((sum(len(blocks[i]["insts"]) for i in b), h, b) for h, b in by_h.items()), reverse=True)
         fidx = {}
-        print(f"{name}: {len(insts)} instructions; outermost loops (static, one iteration):")
-        for n, a, b in outer:
+        total = sum(len(b["insts"]) for b in blocks)
+        print(f"{name}: {total} instructions, {n_b} blocks; loops (static instructions of the body, "
+              f"every block once):")
+        for n2, h, body in lps[:int(os.environ.get("ISA_LOOPS", "3"))]:
             per = collections.defaultdict(collections.Counter)
             tot = collections.Counter()
-            for op, _, (fno, line) in insts[a:b + 1]:
-                f = files.get(fno, "?")
-                full = f if os.path.isabs(f) else os.path.join(srcdir, f)
-                if full not in fidx:
-                    fidx[full] = function_index(full)
-                fn = fidx[full](line) or "?"
-                key = f"{os.path.basename(f)}:{fn}"
-                c = classify(op)
-                c = "valu" if c.startswith("valu") else c
-                per[key][c] += 1
-                tot[c] += 1
-            print(f"  loop [{a}, {b}] = {n} instructions  {dict(tot)}")
+            for i in sorted(body):
+                for op, _, (fno, line) in blocks[i]["insts"]:
+                    f = files.get(fno, "?")
+                    full = f if os.path.isabs(f) else os.path.join(srcdir, f)
+                    if full not in fidx:
+                        fidx[full] = function_index(full)
+                    fn = fidx[full](line) or "?"
+                    key = f"{os.path.basename(f)}:{fn}"
+                    c = classify(op)
+                    c = "valu" if c.startswith("valu") else c
+                    per[key][c] += 1
+                    tot[c] += 1
+            inner = sum(1 for _, h2, b2 in lps if b2 < body)
+            print(f"  loop at block {h} ({blocks[h]['label']}): {n2} instructions in {len(body)} blocks, "
+                  f"{inner} inner loops  {dict(tot)}")
             for key, c in sorted(per.items(), key=lambda kv: -kv[1]["valu"]):
                 if c["valu"] + c["salu"] == 0:
                     continue
