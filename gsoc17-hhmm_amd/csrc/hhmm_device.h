@@ -129,6 +129,20 @@ __device__ __forceinline__ double dpp_f64(double v)
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
+/* v of lane ^ 16 through the gfx950 half-exchange v_permlane16_swap (both
+ * operands v: the first result holds the lower 16-lane row of each pair of
+ * rows in both rows, the second the upper) -- VALU moves instead of a
+ * ds_swizzle round trip through the LDS crossbar. */
+__device__ __forceinline__ double lane_xor16(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    const bool up = (threadIdx.x & 16) != 0;
+    const int l = up ? lo[0] : lo[1];
+    const int h = up ? hi[0] : hi[1];
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)h << 32) | (unsigned)l));
+}
 /* d[i] = v of lane i of this lane's quad. */
 template <int K>
 __device__ __forceinline__ void quad_gather(double v, double (&d)[K])

@@ -83,13 +83,26 @@ __device__ __forceinline__ double lk_dpp(double v)
     const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
+/* Build knob: lane ^ 16 by v_permlane16_swap (0: ds_swizzle).  N1 40.94 against
+ * 41.19 ms interleaved on one box (outputs identical; profiles/r04g_ab_n1.log).
+ * The MFMA chunk-product kernel keeps its ds_bpermute column reductions
+ * (__shfl_xor): there the VALU form measured 168.8 against 156.8 ms. */
+#ifndef HHMM_LK_PERMLANE
+#define HHMM_LK_PERMLANE 1
+#endif
 __device__ __forceinline__ double lk_xor16(double v)
 {
-    constexpr int kXor16 = 0x1F | (0x10 << 10); /* ds_swizzle bit mode: and 0x1F, or 0, xor 0x10 */
+#if HHMM_LK_PERMLANE
+    /* a VALU exchange (lane_xor16) instead of a ds_swizzle round trip through
+     * the LDS crossbar, on the dependency chain of every group reduction */
+    return lane_xor16(v);
+#else
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_swizzle((int)b, kXor16);
-    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), kXor16);
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    constexpr int kXor16 = 0x1F | (0x10 << 10); /* ds_swizzle bit mode: and 0x1F, or 0, xor 0x10 */
+    const int l = __builtin_amdgcn_ds_swizzle((int)b, kXor16);
+    const int h = __builtin_amdgcn_ds_swizzle((int)(b >> 32), kXor16);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)h << 32) | (unsigned)l));
+#endif
 }
 constexpr int kDppXor1 = 0xB1;       /* quad_perm [1,0,3,2] */
 constexpr int kDppXor2 = 0x4E;       /* quad_perm [2,3,0,1] */
