@@ -17,8 +17,9 @@
  *
  *   hhmm_det_exp: x = k ln2 + r (Cody-Waite, ln2 in two parts, k*LN2_HI exact
  *     for |k| < 2^11), |r| <= ln2/2, exp(r) by the degree-13 Taylor sum in
- *     Horner form (truncation < 2^-57), times 2^k as two exact power-of-two
- *     factors (one rounding, also for subnormal results).
+ *     Horner form (truncation < 2^-57), times 2^k by ldexp (one rounding, also
+ *     for subnormal results; the same double as two exact power-of-two
+ *     factors).
  *   hhmm_det_log: x = 2^e m, m in [sqrt(1/2), sqrt(2)); s = (m - 1) / (m + 1),
  *     log m = 2 s + s^3 (2/3 + 2/5 s^2 + ... + 2/21 s^18) (truncation < 2^-60),
  *     + e ln2 (two parts).
@@ -65,8 +66,9 @@ HHMM_MATH_FN double hhmm_det_pow2(int k)
 HHMM_MATH_FN double hhmm_det_exp(double x)
 {
     /* clamp into [-746, 710]: below, exp rounds to 0; above, to +inf -- the
-     * clamped argument still gives exactly that (NaN is selected at the end) */
-    const double xc = x < -746.0 ? -746.0 : (x > 710.0 ? 710.0 : x);
+     * clamped argument still gives exactly that (fmax / fmin take a NaN to a
+     * bound; NaN is selected at the end) */
+    const double xc = __builtin_fmin(__builtin_fmax(x, -746.0), 710.0);
     const double kd = __builtin_rint(xc * HHMM_DET_INV_LN2);
     double r = __builtin_fma(-kd, HHMM_DET_LN2_HI, xc);
     r = __builtin_fma(-kd, HHMM_DET_LN2_LO, r);
@@ -84,11 +86,12 @@ HHMM_MATH_FN double hhmm_det_exp(double x)
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     p = __builtin_fma(p, r, 1.0);
-    /* k in [-1077, 1025]: 2^k = 2^k1 2^k2 with both factors normal */
-    const int k = (int)kd;
-    const int k1 = k / 2;
-    const int k2 = k - k1;
-    const double y = (p * hhmm_det_pow2(k1)) * hhmm_det_pow2(k2);
+    /* times 2^k, k in [-1077, 1025], rounded once (also for subnormal
+     * results): ldexp is exactly RN(p 2^k) on both sides (v_ldexp_f64; C's
+     * ldexp), the same double as the two-factor product (p 2^k1) 2^k2 with
+     * k1 = k / 2 (exact, normal) of the contract's statement (DESIGN.md §5;
+     * tests/test_detmath.py restates that form and checks bit identity) */
+    const double y = __builtin_ldexp(p, (int)kd);
     return x != x ? x + x : y;
 }
 

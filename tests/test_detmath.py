@@ -42,6 +42,18 @@ def test_det_exp_oracle_matches_python_restatement(oracle):
     assert same.all(), x[~same][:5]
 
 
+def test_det_exp_subnormal_and_overflow_edges(oracle):
+    """The result's scaling by 2^k (ldexp in hhmm_detmath.h) against the
+    restatement's two exact power-of-two factors, densely where it matters:
+    the subnormal results (x in [-746, -708]) and the overflow edge."""
+    g = np.random.Generator(np.random.Philox(23))
+    x = np.concatenate([-708.0 - g.random(20000) * 38.0, 700.0 + g.random(4000) * 11.0])
+    got = oracle.det_array("exp", x)
+    want = np.array([fc.det_exp(float(v)) for v in x])
+    same = _same(got, want)
+    assert same.all(), x[~same][:5]
+
+
 def test_det_log_oracle_matches_python_restatement(oracle):
     x = _args_log()
     got = oracle.det_array("log", x)
