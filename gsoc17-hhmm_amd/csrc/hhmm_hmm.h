@@ -2516,44 +2516,144 @@ __device__ __forceinline__ void load_mat(const double *base, const DevArgs &a, i
             M[i][j] = base[p + a.P * ((int64_t)(c * K + i) * K + j)];
 }
 
-/* Phase 2: one wave per pair scans its chunk products.  The lanes fetch 64
- * chunks' products and scale words at once (lane l: chunk block + l), stage
- * them in LDS, and every lane walks the block with uniform-address LDS reads
- * while the next block's loads are in flight (all lanes compute the same
- * vectors in the same operation order; lane 0 stores).  One lane per pair
- * walking its own chunks waited a memory round trip per chunk (C5: 2.5 ms). */
-template <int K>
-constexpr int scan_row() { return (K * K + 3 + 1) & ~1; }
+/* Phase 2: one wave per pair scans its chunk products, 64 chunks per step of
+ * the walk, lane-parallel.  Lane l holds chunk cb + l's product; a
+ * Hillis-Steele prefix over the lanes (six levels of K x K products, the
+ * partner's matrix by __shfl_up) gives every lane the product of the block's
+ * chunks up to its own, and every lane applies it to the vector entering the
+ * block, so the vectors entering all 64 chunks come out at once and are
+ * stored by their own lanes.  The serial walk (one chunk per ~700 cycles of
+ * dependent latency, lane 0 storing) took 2.4 ms at C5.
+ * Products of the non-negative chunk matrices keep every entry's relative
+ * precision; the partial products carry one exact power-of-two exponent PER
+ * ROW (a row is the map from one entering state, and rows can drift apart by
+ * more than the double range over a block), as lks_bound_kernel's exponents
+ * do at large K.  The reassociated sums change the boundary vectors by a few
+ * ulps against the serial walk, far inside the 1e-9 parity tolerance. */
+constexpr int kNoExp = -(1 << 30);
 
 template <int K>
-__device__ __forceinline__ void scan_fetch(const double *base, const DevArgs &a, int64_t p, int c, double (&m)[K][K],
-                                           double (&x)[3])
+struct RowMat {
+    double m[K][K]; /* rows with max in [0.5, 1), or zero */
+    int rs[K];      /* row i of the value is 2^rs[i] m[i] */
+    double ls;      /* additive log scale (nats): the Gaussian emission shifts */
+};
+
+/* out 2^ex = f diag(2^rs) m (f any non-negative vector): the terms scaled to
+ * the largest entering exponent, out renormalised into [0.5, 1). f == 0:
+ * out = 0, ex unchanged. */
+template <int K>
+__device__ __forceinline__ void vec_rowmat(const double (&f)[K], const double (&m)[K][K], const int (&rs)[K],
+                                           double (&out)[K], int &ex)
 {
-    load_mat<K>(base, a, c, p, m);
+    int E = kNoExp;
 #pragma unroll
-    for (int f = 0; f < 3; ++f)
-        x[f] = a.sc_mx[p + a.P * (int64_t)(c * 3 + f)];
+    for (int i = 0; i < K; ++i)
+        E = (f[i] != 0.0) ? max(E, __builtin_amdgcn_frexp_exp(f[i]) + rs[i]) : E;
+    double g[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        g[i] = (f[i] != 0.0) ? ldexp(f[i], rs[i] - E) : 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double acc = g[0] * m[0][j];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            acc = fma(g[i], m[i][j], acc);
+        out[j] = acc;
+    }
+    int e2 = 0;
+    renorm<K>(out, e2);
+    ex += (E == kNoExp) ? 0 : E + e2;
+}
+
+/* A chunk product as stored by scan_prod_kernel (one exponent for the whole
+ * matrix; TR: transposed, the backward map applied to a row vector) in the
+ * row-scaled form. */
+template <int K, bool TR>
+__device__ __forceinline__ void rowmat_load(const double *base, const DevArgs &a, int c, int64_t p, int mex,
+                                            double mls, bool ident, RowMat<K> &R)
+{
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double mx = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const double v = ident ? (i == j ? 1.0 : 0.0)
+                                   : base[p + a.P * ((int64_t)(c * K + (TR ? j : i)) * K + (TR ? i : j))];
+            R.m[i][j] = v;
+            mx = fmax(mx, v);
+        }
+        const int e = __builtin_amdgcn_frexp_exp(mx); /* 0 for a zero row */
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            R.m[i][j] = ldexp(R.m[i][j], -e);
+        R.rs[i] = ident ? e : e + mex;
+    }
+    R.ls = ident ? 0.0 : mls;
+}
+
+/* R = X Y (X the earlier chunks). */
+template <int K>
+__device__ __forceinline__ void rowmat_mul(const RowMat<K> &X, const RowMat<K> &Y, RowMat<K> &R)
+{
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        int e = 0;
+        vec_rowmat<K>(X.m[i], Y.m, Y.rs, R.m[i], e);
+        R.rs[i] = X.rs[i] + e;
+    }
+    R.ls = X.ls + Y.ls;
 }
 
 template <int K>
-__device__ __forceinline__ void scan_stage(double *blk, const double (&m)[K][K], const double (&x)[3])
+__device__ __forceinline__ void rowmat_shfl_up(const RowMat<K> &S, RowMat<K> &D, int d)
 {
-    double *r = blk + (threadIdx.x & 63) * scan_row<K>();
 #pragma unroll
-    for (int i = 0; i < K; ++i)
+    for (int i = 0; i < K; ++i) {
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            r[i * K + j] = m[i][j];
+            D.m[i][j] = __shfl_up(S.m[i][j], d);
+        D.rs[i] = __shfl_up(S.rs[i], d);
+    }
+    D.ls = __shfl_up(S.ls, d);
+}
+
+/* Inclusive prefix product over the wave's lanes: P_l = M_0 M_1 ... M_l. */
+template <int K>
+__device__ __forceinline__ void rowmat_prefix(RowMat<K> &P, int lane)
+{
 #pragma unroll
-    for (int f = 0; f < 3; ++f)
-        r[K * K + f] = x[f];
+    for (int d = 1; d < 64; d <<= 1) {
+        RowMat<K> X, R;
+        rowmat_shfl_up<K>(P, X, d);
+        rowmat_mul<K>(X, P, R);
+        if (lane >= d)
+            P = R;
+    }
+}
+
+/* One block of the boundary walk: lane l holds the (row-scaled) map of the
+ * block's chunk l (identity past the walk's end); v / vsc enter the block
+ * (wave-uniform) and leave it after its last live chunk nb - 1.  Lane l
+ * returns the vector leaving its chunk, normalised, and its log scale. */
+template <int K>
+__device__ __forceinline__ void bound_block(RowMat<K> &P, int lane, int nb, double (&v)[K], double &vsc,
+                                            double (&out)[K], double &osc)
+{
+    rowmat_prefix<K>(P, lane);
+    int ex = 0;
+    vec_rowmat<K>(v, P.m, P.rs, out, ex);
+    osc = vsc + (P.ls + kLn2 * ex);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        v[k] = __shfl(out[k], nb - 1);
+    vsc = __shfl(osc, nb - 1);
 }
 
 template <int MODEL, int K, bool BWD>
 __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
 {
-    HIP_DYNAMIC_SHARED(double, blk)
-    constexpr int RW = scan_row<K>();
     const int64_t p = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const bool l0 = lane == 0;
@@ -2563,77 +2663,53 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
     const int ncp = (Tp + a.scan_cl - 1) / a.scan_cl;
     auto mx = [&](int c, int f) { return a.sc_mx[p + a.P * (int64_t)(c * 3 + f)]; };
 
+    /* ---- forward: f entering chunks c0 .. ncp-1, the loglik ---- */
     double f[K];
     double sc;
+    int c0;
     if (!a.seg_nofirst) {
+        /* chunk 0's product has every row equal to the filter leaving it */
 #pragma unroll
         for (int j = 0; j < K; ++j)
             f[j] = a.sc_mf[p + a.P * (int64_t)j];
         sc = mx(0, 1) + kLn2 * mx(0, 0);
+        c0 = 1;
     } else {
         /* a segment window: chunk 0 enters from the caller's state, which then
          * goes through chunk 0's product like every later chunk */
-        double e[K];
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            e[j] = a.seg_enter[p + a.P * (int64_t)j];
-        const double esc = a.seg_enter[p + a.P * (int64_t)K];
-        if (l0) {
+            f[j] = a.seg_enter[p + a.P * (int64_t)j];
+        sc = a.seg_enter[p + a.P * (int64_t)K];
+        c0 = 0;
+    }
+    if (l0 && c0 < ncp) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            a.sc_st[p + a.P * (int64_t)(c0 * K + k)] = f[k];
+        a.sc_sl[p + a.P * (int64_t)c0] = sc;
+    }
+    for (int cb = c0; cb < ncp; cb += 64) {
+        const int c = cb + lane;
+        const bool live = c < ncp;
+        const int cc = live ? c : ncp - 1;
+        RowMat<K> P;
+        rowmat_load<K, false>(a.sc_mf, a, cc, p, live ? (int)mx(cc, 0) : 0, live ? mx(cc, 1) : 0.0, !live, P);
+        double out[K], osc;
+        bound_block<K>(P, lane, min(ncp - cb, 64), f, sc, out, osc);
+        if (c + 1 < ncp) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                a.sc_st[p + a.P * (int64_t)k] = e[k];
-            a.sc_sl[p] = esc;
+                a.sc_st[p + a.P * (int64_t)((c + 1) * K + k)] = out[k];
+            a.sc_sl[p + a.P * (int64_t)(c + 1)] = osc;
         }
-        double m0[K][K];
-        load_mat<K>(a.sc_mf, a, 0, p, m0);
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            double acc = e[0] * m0[0][j];
-#pragma unroll
-            for (int ii = 1; ii < K; ++ii)
-                acc = fma(e[ii], m0[ii][j], acc);
-            f[j] = acc;
-        }
-        int e2 = 0;
-        renorm<K>(f, e2);
-        sc = esc + mx(0, 1) + kLn2 * (mx(0, 0) + e2);
-    }
-    double m[K][K], x3[3];
-    scan_fetch<K>(a.sc_mf, a, p, min(1 + lane, max(ncp - 1, 0)), m, x3);
-    for (int cb = 1; cb < ncp; cb += 64) {
-        scan_stage<K>(blk, m, x3);
-        __syncthreads();
-        scan_fetch<K>(a.sc_mf, a, p, min(cb + 64 + lane, ncp - 1), m, x3);
-        for (int i = 0; i < 64 && cb + i < ncp; ++i) {
-            const int c = cb + i;
-            const double *r = blk + i * RW;
-            if (l0) {
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    a.sc_st[p + a.P * (int64_t)(c * K + k)] = f[k];
-                a.sc_sl[p + a.P * (int64_t)c] = sc;
-            }
-            double nf[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                double acc = f[0] * r[j];
-#pragma unroll
-                for (int ii = 1; ii < K; ++ii)
-                    acc = fma(f[ii], r[ii * K + j], acc);
-                nf[j] = acc;
-            }
-            int e2 = 0;
-            renorm<K>(nf, e2);
-            sc += r[K * K + 1] + kLn2 * (r[K * K + 0] + e2);
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                f[j] = nf[j];
-        }
-        __syncthreads();
     }
     if (l0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
         a.loglik[p] = log(vsum<K>(f)) + sc;
+
     if constexpr (BWD) {
+        /* ---- backward: beta leaving chunks ncp-1 .. 0; chunk c's map applied
+         * to a row vector is Q_c^T, lane l holds chunk ncp-1-(block)-l ---- */
         double b[K];
         /* beta at the last step: unbeta_tk[T] = 1 (Q1), or a segment window's
          * beta leaving it (the caller's) */
@@ -2646,37 +2722,20 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
         }
         if (l0)
             a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = bsc;
-        /* blocks of 64 chunks from the top down: lane l holds chunk top - l */
-        scan_fetch<K>(a.sc_qb, a, p, min(max(ncp - 1 - lane, 1), ncp - 1), m, x3);
         for (int ct = ncp - 1; ct >= 1; ct -= 64) {
-            scan_stage<K>(blk, m, x3);
-            __syncthreads();
-            scan_fetch<K>(a.sc_qb, a, p, min(max(ct - 64 - lane, 1), ncp - 1), m, x3);
-            for (int i = 0; i < 64 && ct - i >= 1; ++i) {
-                const int c = ct - i;
-                const double *r = blk + i * RW;
-                double nb[K];
+            const int c = ct - lane;
+            const bool live = c >= 1;
+            const int cc = live ? c : 1;
+            RowMat<K> P;
+            rowmat_load<K, true>(a.sc_qb, a, cc, p, live ? (int)mx(cc, 2) : 0, live ? mx(cc, 1) : 0.0, !live, P);
+            double out[K], osc;
+            bound_block<K>(P, lane, min(ct, 64), b, bsc, out, osc);
+            if (live) {
 #pragma unroll
-                for (int rr = 0; rr < K; ++rr) {
-                    double acc = r[rr * K + 0] * b[0];
-#pragma unroll
-                    for (int ii = 1; ii < K; ++ii)
-                        acc = fma(r[rr * K + ii], b[ii], acc);
-                    nb[rr] = acc;
-                }
-                int e2 = 0;
-                renorm<K>(nb, e2);
-                bsc += r[K * K + 1] + kLn2 * (r[K * K + 2] + e2);
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    b[k] = nb[k];
-                    if (l0)
-                        a.sc_be[p + a.P * (int64_t)((c - 1) * K + k)] = b[k];
-                }
-                if (l0)
-                    a.sc_bl[p + a.P * (int64_t)(c - 1)] = bsc;
+                for (int k = 0; k < K; ++k)
+                    a.sc_be[p + a.P * (int64_t)((c - 1) * K + k)] = out[k];
+                a.sc_bl[p + a.P * (int64_t)(c - 1)] = osc;
             }
-            __syncthreads();
         }
     }
 }
@@ -2931,13 +2990,13 @@ static hhmm_status launch_fb_scan(const DevArgs &a, bool fwd_only, hipStream_t s
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     if (fwd_only) {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, false>), gridG, s.block, s.lds, st, a);
-        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64),
-                           64 * scan_row<K>() * sizeof(double), st, a);
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64), 0, st,
+                           a);
         hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
     } else {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, true>), gridG, s.block, s.lds, st, a);
-        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64),
-                           64 * scan_row<K>() * sizeof(double), st, a);
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64), 0, st,
+                           a);
         if (a.outputs & extra)
             hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
         else
@@ -3117,15 +3176,15 @@ static hhmm_status launch_segment(const DevArgs &a, hipStream_t st)
         const dim3 gridG3((unsigned)((G3 + s.block.x - 1) / s.block.x));
         const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
         if (bwd) {
-            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64),
-                               64 * scan_row<K>() * sizeof(double), st, a);
+            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64), 0,
+                               st, a);
             if (a.outputs & extra)
                 hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
             else
                 hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_GAMMA>), gridG3, s.block, s.lds, st, a);
         } else {
-            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64),
-                               64 * scan_row<K>() * sizeof(double), st, a);
+            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64), 0,
+                               st, a);
             if (a.outputs & (HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA))
                 hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
         }

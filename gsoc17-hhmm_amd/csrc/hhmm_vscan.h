@@ -923,15 +923,59 @@ __global__ void __launch_bounds__(64) vs_scan0_kernel(const DevArgs a)
     }
 }
 
+/* One chunk of the exact scan from the exact entry dl (wave-uniform): the
+ * grid product where the checks hold (a tie chunk through M0 / M1 by the
+ * entry values' parities), else step by step.  Row c + 1 of vs_d. */
+template <int MODEL, int K>
+__device__ __forceinline__ void vs_exact_chunk(const DevArgs &a, int64_t p, const SpLane<MODEL, K> &ln,
+                                               const SeriesPtrs &sp, const double *blk, int i, int c, int Tp,
+                                               double (&dl)[K])
+{
+    const bool l0 = (threadIdx.x & 63) == 0;
+    const double hi = vs_hi<K>(dl);
+    double nx[K];
+    const int32_t kc = vs_apply_lds<K>(blk, i, dl, nx);
+    const int32_t kb = (kc >= 0) ? (kc & ~kVsTie) : kc; /* ties are exact through M0 / M1 */
+    bool ok = kc != kVsNoGrid && hi > dev_ninf() && hi != 0.0 && vs_binade(hi) == kb;
+    /* every finite exit value inside the binade, 2^-40 of its width clear of the edge */
+    const double edge = -ldexp(1.0 - 0x1p-40, kb + 1);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        ok = ok && (nx[k] == dev_ninf() || nx[k] > edge);
+    if (ok) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            dl[k] = nx[k];
+    } else {
+        const int t0 = c * kVsChunk;
+        vs_sp_steps<MODEL, K, false>(a, ln, sp, t0, min(t0 + kVsChunk, Tp), dl);
+        if (l0)
+            a.vs_k[p + a.P * (int64_t)c] = kVsSeq;
+    }
+    if (l0)
+        vs_store_d<K>(a, p, c + 1, dl);
+}
+
 /* One wave per pair: the exact scan over the grid products, chunks failing
- * the checks decoded step by step.  Rows 2..ncp of vs_d. */
+ * the checks decoded step by step.  Rows 2..ncp of vs_d.
+ * Lane-parallel per block of 64 chunks (round 4): a max-plus Hillis-Steele
+ * prefix of the grid products from lane s on gives every lane a candidate
+ * entry, every lane applies its own chunk to it and makes the serial walk's
+ * checks, and a lane's candidate counts only if it is bit for bit the exit of
+ * the lane before it: so every committed exit is the serial walk's own
+ * arithmetic from a verified entry, whatever the reassociated prefix did.
+ * (Within one binade the grid sums are exact, so the candidates do match; a
+ * tie chunk, a binade crossing or a failed check ends the run.)  The first
+ * lane f that fails is walked exactly as before, then the prefix restarts at
+ * f + 1.  At C5 the serial walk took 2.4 ms, ~1,900 cycles per chunk on one
+ * wave per pair. */
 template <int MODEL, int K>
 __global__ void __launch_bounds__(64) vs_scan1_kernel(const DevArgs a)
 {
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
     HIP_DYNAMIC_SHARED(double, ldsd)
     const int64_t p = blockIdx.x;
-    const bool l0 = threadIdx.x == 0;
+    const int lane = threadIdx.x & 63;
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
@@ -947,33 +991,84 @@ __global__ void __launch_bounds__(64) vs_scan1_kernel(const DevArgs a)
     double dl[K];
     vs_load_d<K>(a, p, 1, dl);
     for (int cb = 1; cb < ncp; cb += 64) {
-        vs_stage<K>(nxt, blk);
+        const VsBlock<K> cur = nxt;
+        vs_stage<K>(cur, blk);
         __syncthreads();
         vs_fetch<K>(a, p, cb + 64, ncp, nxt);
-        for (int i = 0; i < 64 && cb + i < ncp; ++i) {
-            const int c = cb + i;
-            const double hi = vs_hi<K>(dl);
+        const int nb = min(ncp - cb, 64);
+        const int32_t kc = cur.k;
+        const bool tie = kc >= 0 && (kc & kVsTie);
+        const int32_t kb = (kc >= 0) ? (kc & ~kVsTie) : kc;
+        const double edge = -ldexp(1.0 - 0x1p-40, kb + 1);
+        int s = 0; /* the first lane of the run; dl enters its chunk */
+        while (s < nb) {
+            const bool in = lane >= s && lane < nb;
+            double P[K][K];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    P[i][j] = in ? cur.m[i][j] : (i == j ? 0.0 : dev_ninf());
+#pragma unroll
+            for (int dd = 1; dd < 64; dd *= 2) {
+                double Q[K][K], R[K][K];
+                vs_mp_shfl_up<K>(P, dd, Q);
+                vs_mp_mul<K>(Q, P, R);
+                if (lane >= dd) {
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+#pragma unroll
+                        for (int j = 0; j < K; ++j)
+                            P[i][j] = R[i][j];
+                }
+            }
+            /* candidate entry: dl (x) the product of the run's chunks before this lane's */
+            double E[K][K];
+            vs_mp_shfl_up<K>(P, 1, E);
+            double din[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                double v = dl[0] + E[0][j];
+#pragma unroll
+                for (int r = 1; r < K; ++r)
+                    v = fmax(v, dl[r] + E[r][j]);
+                din[j] = (lane == s) ? dl[j] : v;
+            }
+            /* the lane's own chunk from its candidate, in vs_apply_lds's order */
             double nx[K];
-            const int32_t kc = vs_apply_lds<K>(blk, i, dl, nx);
-            const int32_t kb = (kc >= 0) ? (kc & ~kVsTie) : kc; /* ties are exact through M0 / M1 */
-            bool ok = kc != kVsNoGrid && hi > dev_ninf() && hi != 0.0 && vs_binade(hi) == kb;
-            /* every finite exit value inside the binade, 2^-40 of its width clear of the edge */
-            const double edge = -ldexp(1.0 - 0x1p-40, kb + 1);
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                double best = din[0] + cur.m[0][j];
+#pragma unroll
+                for (int r = 1; r < K; ++r)
+                    best = fmax(best, din[r] + cur.m[r][j]);
+                nx[j] = best;
+            }
+            const double hi = vs_hi<K>(din);
+            bool ok = in && !tie && kc != kVsNoGrid && hi > dev_ninf() && hi != 0.0 && vs_binade(hi) == kb;
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 ok = ok && (nx[k] == dev_ninf() || nx[k] > edge);
-            if (ok) {
+            /* the candidate must be the previous lane's exit, bit for bit */
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const double prev = __shfl_up(nx[k], 1, 64);
+                ok = ok && (lane == s || __double_as_longlong(prev) == __double_as_longlong(din[k]));
+            }
+            const uint64_t bad = __ballot(in && !ok);
+            const int f = __builtin_amdgcn_readfirstlane(bad ? __ffsll((unsigned long long)bad) - 1 : nb);
+            if (lane >= s && lane < f)
+                vs_store_d<K>(a, p, cb + lane + 1, nx);
+            /* the exact entry of lane f: the exit of lane f - 1 (or dl) */
+            if (f > s) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    dl[k] = nx[k];
-            } else {
-                const int t0 = c * kVsChunk;
-                vs_sp_steps<MODEL, K, false>(a, ln, sp, t0, min(t0 + kVsChunk, Tp), dl);
-                if (l0)
-                    a.vs_k[p + a.P * (int64_t)c] = kVsSeq;
+                    dl[k] = __shfl(nx[k], f - 1, 64);
             }
-            if (l0)
-                vs_store_d<K>(a, p, c + 1, dl);
+            if (f == nb)
+                break;
+            vs_exact_chunk<MODEL, K>(a, p, ln, sp, blk, f, cb + f, Tp, dl);
+            s = f + 1;
         }
         __syncthreads();
     }
@@ -1040,14 +1135,27 @@ __global__ void __launch_bounds__(kBlock) vs_replay_kernel(const DevArgs a)
         a.vs_fail[v.p] = 1;
 }
 
-/* lane = pair: logp_zstar, zstar_T and pair_status (viterbi_epilogue's rules),
- * then the path state at the end of every chunk through the backtrack maps. */
+/* Composition of two backtrack maps (byte j: the entry state of the survivor
+ * ending in j): (g o h)(j) = g(h(j)). */
+__device__ __forceinline__ uint32_t vs_map_compose(uint32_t g, uint32_t h, int K)
+{
+    uint32_t r = 0;
+    for (int j = 0; j < K; ++j)
+        r |= ((g >> (8 * ((h >> (8 * j)) & 0xffu))) & 0xffu) << (8 * j);
+    return r;
+}
+
+/* One wave per pair: logp_zstar, zstar_T and pair_status (viterbi_epilogue's
+ * rules), then the path state at the end of every chunk through the backtrack
+ * maps, 64 chunks at a time from the top: lane l holds chunk top - l's map, a
+ * Hillis-Steele prefix of the compositions over the lanes gives every lane the
+ * map from the block's top state to its chunk's end state (round 4; a lane per
+ * pair walking 1,954 chunks took 0.42 ms at C5). */
 template <int K>
 __global__ void __launch_bounds__(64) vs_stitch_kernel(const DevArgs a)
 {
-    const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (p >= a.P)
-        return;
+    const int64_t p = blockIdx.x;
+    const int lane = threadIdx.x & 63;
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
@@ -1061,38 +1169,41 @@ __global__ void __launch_bounds__(64) vs_stitch_kernel(const DevArgs a)
         if (dl[j] == lp)
             z = j;
     const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
-    if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
-        a.logp_zstar[p] = lp;
-    if (a.pair_status)
-        a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+    if (lane == 0) {
+        if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
+            a.logp_zstar[p] = lp;
+        if (a.pair_status)
+            a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+    }
     if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
         return;
     if (invalid)
         z = -1;
-    /* maps prefetched G chunks at a time: the walk itself is a byte extract per chunk */
-    constexpr int G = 16;
-    uint32_t e[G], en[G];
-    int c = ncp - 1;
-    const int gl = c / G;
+    uint32_t ident = 0;
 #pragma unroll
-    for (int i = 0; i < G; ++i)
-        e[i] = a.vs_e[p + a.P * (int64_t)min(gl * G + i, ncp - 1)];
-    for (int g = gl; g >= 0; --g) {
+    for (int j = 0; j < K; ++j)
+        ident |= (uint32_t)j << (8 * j);
+    for (int top = ncp - 1; top >= 0; top -= 64) {
+        const int cc = top - lane;
+        /* lane l: the map of chunk top - l + 1 (the one applied to reach chunk
+         * top - l's end state); lane 0: the identity (the block's top state) */
+        uint32_t m = (lane > 0 && cc >= 0) ? a.vs_e[p + a.P * (int64_t)(cc + 1)] : ident;
 #pragma unroll
-        for (int i = 0; i < G; ++i)
-            en[i] = a.vs_e[p + a.P * (int64_t)max(min((g - 1) * G + i, ncp - 1), 0)];
-#pragma unroll
-        for (int i = G - 1; i >= 0; --i) {
-            const int cc = g * G + i;
-            if (cc <= c) {
-                a.vs_z[p + a.P * (int64_t)cc] = z;
-                if (z >= 0)
-                    z = (int)((e[i] >> (8 * z)) & 0xffu);
-            }
+        for (int dd = 1; dd < 64; dd *= 2) {
+            const uint32_t q = __shfl_up(m, dd, 64);
+            const uint32_t r = vs_map_compose(m, q, K);
+            m = lane >= dd ? r : m;
         }
-#pragma unroll
-        for (int i = 0; i < G; ++i)
-            e[i] = en[i];
+        /* m: the map from the top state to chunk cc's end state */
+        const int zc = z < 0 ? -1 : (int)((m >> (8 * z)) & 0xffu);
+        if (cc >= 0)
+            a.vs_z[p + a.P * (int64_t)cc] = zc;
+        /* the next block's top state: chunk top - 64's end state */
+        const int last = min(top, 63);
+        int zn = __shfl(zc, last, 64);
+        if (top - 64 >= 0 && zn >= 0)
+            zn = (int)((a.vs_e[p + a.P * (int64_t)(top - 63)] >> (8 * zn)) & 0xffu);
+        z = zn;
     }
 }
 
@@ -1167,7 +1278,7 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
             hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3(kVsTieBlocks), bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_scan1_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_replay_kernel<MODEL, K>), gc, bc, lds_c, st, a);
-        hipLaunchKernelGGL((vs_stitch_kernel<K>), gp, b64, 0, st, a);
+        hipLaunchKernelGGL((vs_stitch_kernel<K>), dim3((unsigned)a.P), b64, 0, st, a);
         if ((a.outputs & HHMM_OUT_ZSTAR) && a.zstar)
             hipLaunchKernelGGL((vs_fill_kernel<K>), gc, bc, 0, st, a);
         /* pairs whose replay disagreed with the scan: the sequential decoder */

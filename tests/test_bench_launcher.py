@@ -56,12 +56,25 @@ def test_world_size_mismatch_fails_loudly():
     assert "WORLD_SIZE=1" in (r.stderr + r.stdout)
 
 
-def test_c2_line_finds_its_pmc_traffic():
-    """The default C2 line's roofline.traffic comes from the committed PMC
-    record of its dominant kernel at the bench shape (a record without the
-    shape keys silently gave traffic = null)."""
+def test_c2_line_finds_its_pmc_traffic(tmp_path, monkeypatch):
+    """The C2 line's roofline.traffic comes from the PMC record of its dominant
+    kernel only when that record was taken at the bench shape AND on the
+    library build now loaded (evidence keyed to the build); otherwise
+    it is null with the reason.  The committed record keeps the shape keys (a
+    record without them silently gave traffic = null)."""
     sys.path.insert(0, str(REPO))
     import bench
     dom = bench.SCHEDULE_KERNELS[bench.DEFAULT_SCHEDULE][0]
-    t = bench.load_traffic(dom, 1_000_000, 1000)
-    assert t is not None and 40.0e9 < t < 60.0e9, (dom, t)
+    committed = json.loads((REPO / "profiles" / "bench_traffic.json").read_text())
+    assert committed.get("pairs") == 1_000_000 and committed.get("T") == 1000
+    assert dom in committed.get("kernels", {}), dom
+    (tmp_path / "profiles").mkdir()
+    rec = dict(committed, src="00112233aabbccdd")
+    (tmp_path / "profiles" / "bench_traffic.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    t, note = bench.load_traffic(dom, 1_000_000, 1000, "00112233aabbccdd")
+    assert t is not None and 40.0e9 < t < 60.0e9, (dom, t, note)
+    t, note = bench.load_traffic(dom, 1_000_000, 1000, "ffffffffffffffff")
+    assert t is None and "00112233aabbccdd" in note, note
+    t, note = bench.load_traffic(dom, 1_000, 1000, "00112233aabbccdd")
+    assert t is None and "shape" in note, note
