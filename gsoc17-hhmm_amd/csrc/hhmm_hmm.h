@@ -2568,19 +2568,37 @@ __device__ __forceinline__ void vec_rowmat(const double (&f)[K], const double (&
 }
 
 /* A chunk product as stored by scan_prod_kernel (one exponent for the whole
- * matrix; TR: transposed, the backward map applied to a row vector) in the
- * row-scaled form. */
+ * matrix; TR: transposed, the backward map applied to a row vector), fetched
+ * a block ahead; `ident` (past the walk's end): the identity. */
+template <int K>
+struct RawMat {
+    double m[K][K];
+    double ex, ls;
+};
+
 template <int K, bool TR>
-__device__ __forceinline__ void rowmat_load(const double *base, const DevArgs &a, int c, int64_t p, int mex,
-                                            double mls, bool ident, RowMat<K> &R)
+__device__ __forceinline__ void rawmat_fetch(const double *base, const DevArgs &a, int c, int64_t p, int xf,
+                                             RawMat<K> &R)
+{
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            R.m[i][j] = base[p + a.P * ((int64_t)(c * K + (TR ? j : i)) * K + (TR ? i : j))];
+    R.ex = a.sc_mx[p + a.P * (int64_t)(c * 3 + xf)];
+    R.ls = a.sc_mx[p + a.P * (int64_t)(c * 3 + 1)];
+}
+
+/* ... in the row-scaled form */
+template <int K>
+__device__ __forceinline__ void rowmat_from(const RawMat<K> &M, bool ident, RowMat<K> &R)
 {
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         double mx = 0.0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const double v = ident ? (i == j ? 1.0 : 0.0)
-                                   : base[p + a.P * ((int64_t)(c * K + (TR ? j : i)) * K + (TR ? i : j))];
+            const double v = ident ? (i == j ? 1.0 : 0.0) : M.m[i][j];
             R.m[i][j] = v;
             mx = fmax(mx, v);
         }
@@ -2588,9 +2606,9 @@ __device__ __forceinline__ void rowmat_load(const double *base, const DevArgs &a
 #pragma unroll
         for (int j = 0; j < K; ++j)
             R.m[i][j] = ldexp(R.m[i][j], -e);
-        R.rs[i] = ident ? e : e + mex;
+        R.rs[i] = ident ? e : e + (int)M.ex;
     }
-    R.ls = ident ? 0.0 : mls;
+    R.ls = ident ? 0.0 : M.ls;
 }
 
 /* R = X Y (X the earlier chunks). */
@@ -2663,52 +2681,57 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
     const int ncp = (Tp + a.scan_cl - 1) / a.scan_cl;
     auto mx = [&](int c, int f) { return a.sc_mx[p + a.P * (int64_t)(c * 3 + f)]; };
 
-    /* ---- forward: f entering chunks c0 .. ncp-1, the loglik ---- */
-    double f[K];
-    double sc;
-    int c0;
-    if (!a.seg_nofirst) {
-        /* chunk 0's product has every row equal to the filter leaving it */
+    /* ---- forward (blockIdx.y == 0): f entering chunks c0 .. ncp-1, the loglik ---- */
+    if (blockIdx.y == 0) {
+        double f[K];
+        double sc;
+        int c0;
+        if (!a.seg_nofirst) {
+            /* chunk 0's product has every row equal to the filter leaving it */
 #pragma unroll
-        for (int j = 0; j < K; ++j)
-            f[j] = a.sc_mf[p + a.P * (int64_t)j];
-        sc = mx(0, 1) + kLn2 * mx(0, 0);
-        c0 = 1;
-    } else {
-        /* a segment window: chunk 0 enters from the caller's state, which then
-         * goes through chunk 0's product like every later chunk */
+            for (int j = 0; j < K; ++j)
+                f[j] = a.sc_mf[p + a.P * (int64_t)j];
+            sc = mx(0, 1) + kLn2 * mx(0, 0);
+            c0 = 1;
+        } else {
+            /* a segment window: chunk 0 enters from the caller's state, which then
+             * goes through chunk 0's product like every later chunk */
 #pragma unroll
-        for (int j = 0; j < K; ++j)
-            f[j] = a.seg_enter[p + a.P * (int64_t)j];
-        sc = a.seg_enter[p + a.P * (int64_t)K];
-        c0 = 0;
-    }
-    if (l0 && c0 < ncp) {
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            a.sc_st[p + a.P * (int64_t)(c0 * K + k)] = f[k];
-        a.sc_sl[p + a.P * (int64_t)c0] = sc;
-    }
-    for (int cb = c0; cb < ncp; cb += 64) {
-        const int c = cb + lane;
-        const bool live = c < ncp;
-        const int cc = live ? c : ncp - 1;
-        RowMat<K> P;
-        rowmat_load<K, false>(a.sc_mf, a, cc, p, live ? (int)mx(cc, 0) : 0, live ? mx(cc, 1) : 0.0, !live, P);
-        double out[K], osc;
-        bound_block<K>(P, lane, min(ncp - cb, 64), f, sc, out, osc);
-        if (c + 1 < ncp) {
+            for (int j = 0; j < K; ++j)
+                f[j] = a.seg_enter[p + a.P * (int64_t)j];
+            sc = a.seg_enter[p + a.P * (int64_t)K];
+            c0 = 0;
+        }
+        if (l0 && c0 < ncp) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                a.sc_st[p + a.P * (int64_t)((c + 1) * K + k)] = out[k];
-            a.sc_sl[p + a.P * (int64_t)(c + 1)] = osc;
+                a.sc_st[p + a.P * (int64_t)(c0 * K + k)] = f[k];
+            a.sc_sl[p + a.P * (int64_t)c0] = sc;
         }
+        RawMat<K> nx;
+        rawmat_fetch<K, false>(a.sc_mf, a, max(min(c0 + lane, ncp - 1), 0), p, 0, nx);
+        for (int cb = c0; cb < ncp; cb += 64) {
+            const int c = cb + lane;
+            RowMat<K> P;
+            rowmat_from<K>(nx, c >= ncp, P);
+            rawmat_fetch<K, false>(a.sc_mf, a, max(min(cb + 64 + lane, ncp - 1), 0), p, 0, nx);
+            double out[K], osc;
+            bound_block<K>(P, lane, min(ncp - cb, 64), f, sc, out, osc);
+            if (c + 1 < ncp) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    a.sc_st[p + a.P * (int64_t)((c + 1) * K + k)] = out[k];
+                a.sc_sl[p + a.P * (int64_t)(c + 1)] = osc;
+            }
+        }
+        if (l0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
+            a.loglik[p] = log(vsum<K>(f)) + sc;
+        return;
     }
-    if (l0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
-        a.loglik[p] = log(vsum<K>(f)) + sc;
 
     if constexpr (BWD) {
-        /* ---- backward: beta leaving chunks ncp-1 .. 0; chunk c's map applied
+        /* ---- backward (blockIdx.y == 1, its own wave: the two walks are
+         * independent): beta leaving chunks ncp-1 .. 0; chunk c's map applied
          * to a row vector is Q_c^T, lane l holds chunk ncp-1-(block)-l ---- */
         double b[K];
         /* beta at the last step: unbeta_tk[T] = 1 (Q1), or a segment window's
@@ -2722,12 +2745,14 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
         }
         if (l0)
             a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = bsc;
+        RawMat<K> nx;
+        rawmat_fetch<K, true>(a.sc_qb, a, max(min(max(ncp - 1 - lane, 1), ncp - 1), 0), p, 2, nx);
         for (int ct = ncp - 1; ct >= 1; ct -= 64) {
             const int c = ct - lane;
             const bool live = c >= 1;
-            const int cc = live ? c : 1;
             RowMat<K> P;
-            rowmat_load<K, true>(a.sc_qb, a, cc, p, live ? (int)mx(cc, 2) : 0, live ? mx(cc, 1) : 0.0, !live, P);
+            rowmat_from<K>(nx, !live, P);
+            rawmat_fetch<K, true>(a.sc_qb, a, max(min(max(ct - 64 - lane, 1), ncp - 1), 0), p, 2, nx);
             double out[K], osc;
             bound_block<K>(P, lane, min(ct, 64), b, bsc, out, osc);
             if (live) {
@@ -2995,7 +3020,7 @@ static hhmm_status launch_fb_scan(const DevArgs &a, bool fwd_only, hipStream_t s
         hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
     } else {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, true>), gridG, s.block, s.lds, st, a);
-        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64), 0, st,
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P, 2), dim3(64), 0, st,
                            a);
         if (a.outputs & extra)
             hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
@@ -3176,7 +3201,7 @@ static hhmm_status launch_segment(const DevArgs &a, hipStream_t st)
         const dim3 gridG3((unsigned)((G3 + s.block.x - 1) / s.block.x));
         const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
         if (bwd) {
-            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P), dim3(64), 0,
+            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P, 2), dim3(64), 0,
                                st, a);
             if (a.outputs & extra)
                 hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
