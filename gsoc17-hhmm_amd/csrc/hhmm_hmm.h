@@ -2475,23 +2475,59 @@ __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
                 F[i][j] = f0[j];
         tb = 1;
     }
-    Obs onx = load_obs<MODEL, AUX>(sp, tb);
-    for (int t = tb; t < t1; ++t) {
-        const Obs o = onx;
-        onx = load_obs<MODEL, AUX>(sp, t + 1);
+    auto step = [&](const Obs &o, bool rn) {
         Em<K> em;
         emit_prob<MODEL, K>(pp, slab, a.L, o, em);
         lsc += em.m;
 #pragma unroll
         for (int r = 0; r < K; ++r)
             fwd_step_raw<MODEL, K>(F[r], F[r], pp, em.e, o);
-        renorm_mat<K>(F, fex);
+        if (rn)
+            renorm_mat<K>(F, fex);
         if constexpr (BWD) {
 #pragma unroll
             for (int r = 0; r < K; ++r)
                 bwd_row_raw<MODEL, K>(Q[r], pp, em.e, o);
-            renorm_mat<K>(Q, qex);
+            if (rn)
+                renorm_mat<K>(Q, qex);
         }
+    };
+    /* Discrete emissions renormalise the products every kBigRenorm-th step
+     * (and every step of the chunk's ragged tail) where the pair's parameters
+     * bound the shrink (renorm_sparse_safe, FB_BIG's argument: the max stays
+     * above 2^-156 between renormalisations; a step grows it by at most K);
+     * a wave holding an unsafe pair renormalises every step.  The exponents
+     * are exact powers of two either way (round 4: a quarter of the
+     * renormalisations, which were a sixth of the phase's VALU at C5). */
+    bool sparse = false;
+    if constexpr (ModelTraits<MODEL>::kDiscrete)
+        sparse = !wave_any(!renorm_sparse_safe<MODEL, K>(pp, slab, a.L));
+    Obs onx = load_obs<MODEL, AUX>(sp, tb);
+    int t = tb;
+    if (sparse) {
+        constexpr int G = kBigRenorm;
+        Obs og[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+            og[u] = load_obs<MODEL, AUX>(sp, tb + u);
+        for (; t + G <= t1; t += G) {
+            Obs on[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                on[u] = load_obs<MODEL, AUX>(sp, t + G + u);
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                step(og[u], u == G - 1);
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                og[u] = on[u];
+        }
+        onx = og[0];
+    }
+    for (; t < t1; ++t) {
+        const Obs o = onx;
+        onx = load_obs<MODEL, AUX>(sp, t + 1);
+        step(o, true);
     }
 #pragma unroll
     for (int i = 0; i < K; ++i)
