@@ -2427,6 +2427,18 @@ __device__ __forceinline__ Obs load_obs(const SeriesPtrs &sp, int t)
     return o[0];
 }
 
+/* The chunk products in HBM, pair-major: chunk c of pair p is the K*K
+ * record at sc_mat, its exponents / log scale the 3 doubles at sc_mxi. */
+template <int K>
+__device__ __forceinline__ int64_t sc_mat(const DevArgs &a, int64_t p, int c)
+{
+    return (p * a.scan_nc + c) * (int64_t)(K * K);
+}
+__device__ __forceinline__ int64_t sc_mxi(const DevArgs &a, int64_t p, int c, int f)
+{
+    return (p * a.scan_nc + c) * 3 + f;
+}
+
 template <int MODEL, int K, bool BWD>
 __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
 {
@@ -2529,27 +2541,32 @@ __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
         onx = load_obs<MODEL, AUX>(sp, t + 1);
         step(o, true);
     }
+    /* pair-major records (sc_mat / sc_mxi): a lane writes whole lines, and
+     * the boundary scan's lanes (consecutive chunks of one pair) read
+     * consecutive lines */
+    double *mf = a.sc_mf + sc_mat<K>(a, p, c);
 #pragma unroll
     for (int i = 0; i < K; ++i)
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            at(a.sc_mf + a.P * ((int64_t)(c * K + i) * K + j), (uint32_t)p * 8u) = F[i][j];
+            mf[i * K + j] = F[i][j];
             if constexpr (BWD)
-                at(a.sc_qb + a.P * ((int64_t)(c * K + i) * K + j), (uint32_t)p * 8u) = Q[i][j];
+                a.sc_qb[sc_mat<K>(a, p, c) + i * K + j] = Q[i][j];
         }
-    at(a.sc_mx + a.P * (int64_t)(c * 3 + 0), (uint32_t)p * 8u) = (double)fex;
-    at(a.sc_mx + a.P * (int64_t)(c * 3 + 1), (uint32_t)p * 8u) = lsc;
-    at(a.sc_mx + a.P * (int64_t)(c * 3 + 2), (uint32_t)p * 8u) = (double)qex;
+    a.sc_mx[sc_mxi(a, p, c, 0)] = (double)fex;
+    a.sc_mx[sc_mxi(a, p, c, 1)] = lsc;
+    a.sc_mx[sc_mxi(a, p, c, 2)] = (double)qex;
 }
 
 template <int K>
 __device__ __forceinline__ void load_mat(const double *base, const DevArgs &a, int c, int64_t p, double (&M)[K][K])
 {
+    const double *m = base + sc_mat<K>(a, p, c);
 #pragma unroll
     for (int i = 0; i < K; ++i)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            M[i][j] = base[p + a.P * ((int64_t)(c * K + i) * K + j)];
+            M[i][j] = m[i * K + j];
 }
 
 /* Phase 2: one wave per pair scans its chunk products, 64 chunks per step of
@@ -2616,13 +2633,14 @@ template <int K, bool TR>
 __device__ __forceinline__ void rawmat_fetch(const double *base, const DevArgs &a, int c, int64_t p, int xf,
                                              RawMat<K> &R)
 {
+    const double *m = base + sc_mat<K>(a, p, c);
 #pragma unroll
     for (int i = 0; i < K; ++i)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            R.m[i][j] = base[p + a.P * ((int64_t)(c * K + (TR ? j : i)) * K + (TR ? i : j))];
-    R.ex = a.sc_mx[p + a.P * (int64_t)(c * 3 + xf)];
-    R.ls = a.sc_mx[p + a.P * (int64_t)(c * 3 + 1)];
+            R.m[i][j] = m[(TR ? j : i) * K + (TR ? i : j)];
+    R.ex = a.sc_mx[sc_mxi(a, p, c, xf)];
+    R.ls = a.sc_mx[sc_mxi(a, p, c, 1)];
 }
 
 /* ... in the row-scaled form */
@@ -2705,19 +2723,112 @@ __device__ __forceinline__ void bound_block(RowMat<K> &P, int lane, int nb, doub
     vsc = __shfl(osc, nb - 1);
 }
 
-template <int MODEL, int K, bool BWD>
-__global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
+/* The boundary walk of one direction over items i = 0 .. n-1 (item i is chunk
+ * c0 + i forward, chunk ncp-1-i backward), split over the workgroup's
+ * kBoundWaves waves (round 4): each wave first multiplies its own range's
+ * chunk products into one total (block prefixes, the block totals chained),
+ * the totals meet in LDS, each wave forms the vector entering its range from
+ * the ones before it, then walks its range storing every boundary vector --
+ * twice the products of one wave walking everything, on four waves. */
+#ifndef HHMM_BOUND_WAVES
+#define HHMM_BOUND_WAVES 4 /* build knob: waves per (pair, direction) of the boundary scan */
+#endif
+constexpr int kBoundWaves = HHMM_BOUND_WAVES;
+
+template <int K, bool BW>
+__device__ __forceinline__ void bound_walk(const DevArgs &a, int64_t p, int ncp, int c0, int n, double (&v)[K],
+                                           double &vsc, RowMat<K> *tot)
 {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lo = (int)((int64_t)n * wave / kBoundWaves), hi = (int)((int64_t)n * (wave + 1) / kBoundWaves);
+    const double *base = BW ? a.sc_qb : a.sc_mf;
+    auto chunk = [&](int i) { return BW ? ncp - 1 - i : c0 + i; };
+    auto fetch = [&](int ib, RawMat<K> &r) { /* item ib + lane, clamped into the range */
+        rawmat_fetch<K, BW>(base, a, chunk(max(min(ib + lane, hi - 1), 0)), p, BW ? 2 : 0, r);
+    };
+    /* ---- 1. the range's total ---- */
+    RowMat<K> T;
+    {
+        RawMat<K> id;
+        rowmat_from<K>(id, true, T);
+    }
+    RawMat<K> nx;
+    if (lo < hi)
+        fetch(lo, nx);
+    for (int ib = lo; ib < hi; ib += 64) {
+        RowMat<K> P;
+        rowmat_from<K>(nx, ib + lane >= hi, P);
+        fetch(ib + 64, nx);
+        rowmat_prefix<K>(P, lane);
+        RowMat<K> B, R;
+        const int last = min(hi - ib, 64) - 1;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                B.m[i][j] = __shfl(P.m[i][j], last);
+            B.rs[i] = __shfl(P.rs[i], last);
+        }
+        B.ls = __shfl(P.ls, last);
+        rowmat_mul<K>(T, B, R);
+        T = R;
+    }
+    if (lane == 0)
+        tot[wave] = T;
+    __syncthreads();
+    /* ---- 2. the vector entering this wave's range ---- */
+    for (int w = 0; w < wave; ++w) {
+        const RowMat<K> &U = tot[w];
+        double o[K];
+        int ex = 0;
+        vec_rowmat<K>(v, U.m, U.rs, o, ex);
+        vsc += U.ls + kLn2 * ex;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            v[k] = o[k];
+    }
+    /* ---- 3. the walk, every boundary vector stored by its own lane ---- */
+    if (lo < hi)
+        fetch(lo, nx);
+    for (int ib = lo; ib < hi; ib += 64) {
+        const int i = ib + lane;
+        RowMat<K> P;
+        rowmat_from<K>(nx, i >= hi, P);
+        fetch(ib + 64, nx);
+        double out[K], osc;
+        bound_block<K>(P, lane, min(hi - ib, 64), v, vsc, out, osc);
+        const int c = chunk(i);
+        if (!BW && i < hi && c + 1 < ncp) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                a.sc_st[p + a.P * (int64_t)((c + 1) * K + k)] = out[k];
+            a.sc_sl[p + a.P * (int64_t)(c + 1)] = osc;
+        }
+        if (BW && i < hi) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                a.sc_be[p + a.P * (int64_t)((c - 1) * K + k)] = out[k];
+            a.sc_bl[p + a.P * (int64_t)(c - 1)] = osc;
+        }
+    }
+}
+
+/* One workgroup of kBoundWaves waves per (pair, direction): blockIdx.y == 0
+ * the forward walk (f entering chunks c0 .. ncp-1, the loglik), 1 the
+ * backward walk (beta leaving chunks ncp-1 .. 0; chunk c's map applied to a
+ * row vector is Q_c^T).  The two are independent. */
+template <int MODEL, int K, bool BWD>
+__global__ void __launch_bounds__(64 * kBoundWaves) scan_bound_kernel(const DevArgs a)
+{
+    __shared__ RowMat<K> tot[kBoundWaves];
     const int64_t p = blockIdx.x;
-    const int lane = threadIdx.x & 63;
-    const bool l0 = lane == 0;
+    const bool t0 = threadIdx.x == 0;
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
     const int ncp = (Tp + a.scan_cl - 1) / a.scan_cl;
-    auto mx = [&](int c, int f) { return a.sc_mx[p + a.P * (int64_t)(c * 3 + f)]; };
+    auto mx = [&](int c, int f) { return a.sc_mx[sc_mxi(a, p, c, f)]; };
 
-    /* ---- forward (blockIdx.y == 0): f entering chunks c0 .. ncp-1, the loglik ---- */
     if (blockIdx.y == 0) {
         double f[K];
         double sc;
@@ -2726,7 +2837,7 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
             /* chunk 0's product has every row equal to the filter leaving it */
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                f[j] = a.sc_mf[p + a.P * (int64_t)j];
+                f[j] = a.sc_mf[sc_mat<K>(a, p, 0) + j];
             sc = mx(0, 1) + kLn2 * mx(0, 0);
             c0 = 1;
         } else {
@@ -2738,37 +2849,21 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
             sc = a.seg_enter[p + a.P * (int64_t)K];
             c0 = 0;
         }
-        if (l0 && c0 < ncp) {
+        if (t0 && c0 < ncp) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 a.sc_st[p + a.P * (int64_t)(c0 * K + k)] = f[k];
             a.sc_sl[p + a.P * (int64_t)c0] = sc;
         }
-        RawMat<K> nx;
-        rawmat_fetch<K, false>(a.sc_mf, a, max(min(c0 + lane, ncp - 1), 0), p, 0, nx);
-        for (int cb = c0; cb < ncp; cb += 64) {
-            const int c = cb + lane;
-            RowMat<K> P;
-            rowmat_from<K>(nx, c >= ncp, P);
-            rawmat_fetch<K, false>(a.sc_mf, a, max(min(cb + 64 + lane, ncp - 1), 0), p, 0, nx);
-            double out[K], osc;
-            bound_block<K>(P, lane, min(ncp - cb, 64), f, sc, out, osc);
-            if (c + 1 < ncp) {
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    a.sc_st[p + a.P * (int64_t)((c + 1) * K + k)] = out[k];
-                a.sc_sl[p + a.P * (int64_t)(c + 1)] = osc;
-            }
-        }
-        if (l0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
+        bound_walk<K, false>(a, p, ncp, c0, max(ncp - c0, 0), f, sc, tot);
+        /* the last wave leaves with the filter after chunk ncp-1 */
+        if ((threadIdx.x == 64 * (kBoundWaves - 1)) && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik &&
+            !a.seg_nolast)
             a.loglik[p] = log(vsum<K>(f)) + sc;
         return;
     }
 
     if constexpr (BWD) {
-        /* ---- backward (blockIdx.y == 1, its own wave: the two walks are
-         * independent): beta leaving chunks ncp-1 .. 0; chunk c's map applied
-         * to a row vector is Q_c^T, lane l holds chunk ncp-1-(block)-l ---- */
         double b[K];
         /* beta at the last step: unbeta_tk[T] = 1 (Q1), or a segment window's
          * beta leaving it (the caller's) */
@@ -2776,28 +2871,12 @@ __global__ void __launch_bounds__(64) scan_bound_kernel(const DevArgs a)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             b[k] = a.seg_nolast ? a.seg_leave[p + a.P * (int64_t)k] : 1.0;
-            if (l0)
+            if (t0)
                 a.sc_be[p + a.P * (int64_t)((ncp - 1) * K + k)] = b[k];
         }
-        if (l0)
+        if (t0)
             a.sc_bl[p + a.P * (int64_t)(ncp - 1)] = bsc;
-        RawMat<K> nx;
-        rawmat_fetch<K, true>(a.sc_qb, a, max(min(max(ncp - 1 - lane, 1), ncp - 1), 0), p, 2, nx);
-        for (int ct = ncp - 1; ct >= 1; ct -= 64) {
-            const int c = ct - lane;
-            const bool live = c >= 1;
-            RowMat<K> P;
-            rowmat_from<K>(nx, !live, P);
-            rawmat_fetch<K, true>(a.sc_qb, a, max(min(max(ct - 64 - lane, 1), ncp - 1), 0), p, 2, nx);
-            double out[K], osc;
-            bound_block<K>(P, lane, min(ct, 64), b, bsc, out, osc);
-            if (live) {
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    a.sc_be[p + a.P * (int64_t)((c - 1) * K + k)] = out[k];
-                a.sc_bl[p + a.P * (int64_t)(c - 1)] = osc;
-            }
-        }
+        bound_walk<K, true>(a, p, ncp, 0, max(ncp - 1, 0), b, bsc, tot);
     }
 }
 
@@ -2838,20 +2917,20 @@ __global__ void __launch_bounds__(kBlock) seg_summary_kernel(const DevArgs a)
     load_mat<K>(a.sc_mf, a, 0, p, SF);
     if constexpr (BWD)
         load_mat<K>(a.sc_qb, a, 0, p, SQ);
-    double fex = a.sc_mx[p], lsc = a.sc_mx[p + a.P], qex = a.sc_mx[p + 2 * a.P];
+    double fex = a.sc_mx[sc_mxi(a, p, 0, 0)], lsc = a.sc_mx[sc_mxi(a, p, 0, 1)], qex = a.sc_mx[sc_mxi(a, p, 0, 2)];
     for (int c = 1; c < ncp; ++c) {
         int e = 0;
         load_mat<K>(a.sc_mf, a, c, p, M);
         mat_mul_acc<K>(SF, M);
         renorm_mat<K>(SF, e);
-        fex += a.sc_mx[p + a.P * (int64_t)(c * 3 + 0)] + e;
-        lsc += a.sc_mx[p + a.P * (int64_t)(c * 3 + 1)];
+        fex += a.sc_mx[sc_mxi(a, p, c, 0)] + e;
+        lsc += a.sc_mx[sc_mxi(a, p, c, 1)];
         if constexpr (BWD) {
             e = 0;
             load_mat<K>(a.sc_qb, a, c, p, M);
             mat_mul_acc<K>(SQ, M);
             renorm_mat<K>(SQ, e);
-            qex += a.sc_mx[p + a.P * (int64_t)(c * 3 + 2)] + e;
+            qex += a.sc_mx[sc_mxi(a, p, c, 2)] + e;
         }
     }
     if constexpr (!BWD) {
@@ -3051,12 +3130,12 @@ static hhmm_status launch_fb_scan(const DevArgs &a, bool fwd_only, hipStream_t s
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     if (fwd_only) {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, false>), gridG, s.block, s.lds, st, a);
-        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64), 0, st,
-                           a);
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64 * kBoundWaves), 0,
+                           st, a);
         hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
     } else {
         hipLaunchKernelGGL((scan_prod_kernel<MODEL, K, true>), gridG, s.block, s.lds, st, a);
-        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P, 2), dim3(64), 0, st,
+        hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P, 2), dim3(64 * kBoundWaves), 0, st,
                            a);
         if (a.outputs & extra)
             hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
@@ -3237,14 +3316,14 @@ static hhmm_status launch_segment(const DevArgs &a, hipStream_t st)
         const dim3 gridG3((unsigned)((G3 + s.block.x - 1) / s.block.x));
         const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
         if (bwd) {
-            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P, 2), dim3(64), 0,
+            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, true>), dim3((unsigned)a.P, 2), dim3(64 * kBoundWaves), 0,
                                st, a);
             if (a.outputs & extra)
                 hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FULL>), gridG3, s.block, s.lds, st, a);
             else
                 hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_GAMMA>), gridG3, s.block, s.lds, st, a);
         } else {
-            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64), 0,
+            hipLaunchKernelGGL((scan_bound_kernel<MODEL, K, false>), dim3((unsigned)a.P), dim3(64 * kBoundWaves), 0,
                                st, a);
             if (a.outputs & (HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA))
                 hipLaunchKernelGGL((fb_scan_kernel<MODEL, K, FB_FWD>), gridG3, s.block, s.lds, st, a);
