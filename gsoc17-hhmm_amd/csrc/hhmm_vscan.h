@@ -141,6 +141,15 @@ struct VsTerm {
     bool tie;
 };
 
+/* The chunk products in HBM, pair-major (round 4): chunk c of pair p is the
+ * K*K record at vs_mat, so the scans' lanes (consecutive chunks of one pair)
+ * read consecutive lines. */
+template <int K>
+__device__ __forceinline__ int64_t vs_mat(const DevArgs &a, int64_t p, int c)
+{
+    return (p * a.vs_nc + c) * (int64_t)(K * K);
+}
+
 /* parity (0 or 1) of an integer-valued double */
 __device__ __forceinline__ double vs_parity(double x) { return x - 2.0 * floor(x * 0.5); }
 
@@ -248,7 +257,7 @@ __device__ __forceinline__ void vs_tie_product(const DevArgs &a, const VsLane &v
     for (int r = 0; r < K; ++r)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            out[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = M[r][j] * u;
+            out[vs_mat<K>(a, v.p, v.c) + r * K + j] = M[r][j] * u;
 }
 
 /* The tie chunks' two parity products, one lane per parity, for the chunks
@@ -444,7 +453,7 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
     for (int r = 0; r < K; ++r)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            a.vs_m[v.p + a.P * ((int64_t)v.c * K * K + r * K + j)] = (double)M[r][j];
+            a.vs_m[vs_mat<K>(a, v.p, v.c) + r * K + j] = (double)M[r][j];
     if (GRID && tie) /* a tie met during the pass (Gaussian emissions); kc < 0 (|delta| < 1): decoded step by step */
         vs_list_tie(a, v, kc);
 }
@@ -579,14 +588,14 @@ __device__ __forceinline__ void vs_fetch(const DevArgs &a, int64_t p, int c0, in
     for (int r = 0; r < K; ++r)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            b.m[r][j] = a.vs_m[p + a.P * ((int64_t)c * K * K + r * K + j)];
+            b.m[r][j] = a.vs_m[vs_mat<K>(a, p, c) + r * K + j];
     b.k = a.vs_k[p + a.P * (int64_t)c];
     const bool tie = b.k >= 0 && (b.k & kVsTie);
 #pragma unroll
     for (int r = 0; r < K; ++r)
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            b.m1[r][j] = tie ? a.vs_m1[p + a.P * ((int64_t)c * K * K + r * K + j)] : 0.0;
+            b.m1[r][j] = tie ? a.vs_m1[vs_mat<K>(a, p, c) + r * K + j] : 0.0;
 }
 
 /* The scans' series index as a VGPR value: with one pair per wave every
