@@ -108,7 +108,12 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
         /* large K (hhmm_lkscan.h): hmm-multinom; chunks a multiple of the
          * 32-step observation blocks; automatic when the batch is under 4096
          * pairs (2048 waves of two groups: two per SIMD) and long, with about
-         * 64k (pair, chunk) groups for the chunks' sweeps */
+         * 128k (pair, chunk) groups for the chunks' sweeps.  At N2 (250 pairs x
+         * T = 10^6) that is 2048-step chunks: 223.4 ms against 228.2 for 4096
+         * and 226.0 for 1024, and lk_fb_kernel writes 55.7 GB against 68.1
+         * (1024: 53.6) for 46 GB of gamma + 5.75 GB of checkpoints: a 128-byte
+         * line of a gamma row is written by several waves, whose stores meet in
+         * L2 less often the longer the chunks (profiles/r04r_n2_chunks.txt) */
         if (model != HHMM_MODEL_HMM_MULTINOM || K > kMaxKLarge)
             return sp;
         if (!(flags & HHMM_FLAG_SCAN_FORCE) && !(P < 4096 && Tmax >= 8192))
@@ -117,7 +122,7 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
         if (log2cl > 0) {
             cl = max(32, 1 << log2cl);
         } else {
-            while ((int64_t)P * ((Tmax + cl - 1) / cl) > 65536 && cl < (1 << 20))
+            while ((int64_t)P * ((Tmax + cl - 1) / cl) > 131072 && cl < (1 << 20))
                 cl *= 2;
         }
         cl = (cl + 31) & ~31;
