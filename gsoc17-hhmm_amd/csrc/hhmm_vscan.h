@@ -932,13 +932,133 @@ __global__ void __launch_bounds__(64) vs_scan0_kernel(const DevArgs a)
     }
 }
 
+/* A chunk the exact scan cannot take whole -- its values cross into the next
+ * binade (11 chunks per pair at C5, each 512 steps decoded step by step at
+ * ~370 cycles a step on the pair's one wave), or a check failed -- in
+ * kVsSub sub-chunks (round 4, discrete emissions): lane g kVsSub + s forms
+ * sub-chunk s's max-plus product on the grid of the entry's binade kb + g
+ * (g = 0, 1: the chunk's values start in kb and cross into kb + 1), then the
+ * wave walks the sub-chunks from the exact entry with the chunk checks at the
+ * sub-chunk's own binade: a sub-chunk that passes takes its product (exact,
+ * the grid argument), the one the crossing falls in (or a rounding tie) is
+ * decoded step by step.  The replay still checks the chunk's exit bit for
+ * bit. */
+constexpr int kVsSub = 8;
+
+template <int MODEL, int K>
+__device__ __forceinline__ void vs_cross_chunk(const DevArgs &a, const SpLane<MODEL, K> &ln,
+                                                         const SeriesPtrs &sp, const double *ldsd, int t0, int t1,
+                                                         double (&dl)[K])
+{
+    constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
+    constexpr int SL = kVsChunk / kVsSub;
+    const int lane = threadIdx.x & 63;
+    const double hi0 = vs_hi<K>(dl);
+    if (!(hi0 > dev_ninf() && hi0 != 0.0)) {
+        vs_sp_steps<MODEL, K, false>(a, ln, sp, t0, t1, dl);
+        return;
+    }
+    const int kb0 = vs_binade(hi0);
+    const int sub = lane % kVsSub, g = min(lane / kVsSub, 1);
+    const double u = ldexp(1.0, kb0 + g - 52), iu = ldexp(1.0, 52 - (kb0 + g));
+    bool tie = false;
+    double gA[K][K]; /* log A[i][j] on the grid: column j from quad lane j (non-Tayal) */
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            gA[i][j] = vs_grid(__shfl(ln.colA[i], j, 64), iu, u, tie);
+    double M[K][K];
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            M[r][j] = (r == j) ? 0.0 : dev_ninf();
+    const int s0 = t0 + sub * SL, s1 = min(s0 + SL, t1);
+    for (int t = s0; t < s1; ++t) {
+        Obs o[1];
+        load_chunk<MODEL, 1, VAUX>(o, sp, t);
+        const int xr = min(max(o[0].x, 1), a.L) - 1;
+        double le[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            le[j] = vs_grid(ldsd[xr * 64 + j], iu, u, tie); /* log phi[j][x_t]: quad lane j's column */
+        double aij[K][K];
+        if constexpr (ModelTraits<MODEL>::kTayal) {
+            /* the masked column of quad lane j for this step's sign (-0.0 where off) */
+            const int rr = (o[0].aux == 1) ? 0 : (o[0].aux == 2 ? 1 : 2);
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    aij[i][j] = vs_grid(ldsd[(size_t)(a.L + rr * K + i) * 64 + j], iu, u, tie);
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    aij[i][j] = gA[i][j];
+        }
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            double nm[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                double best = M[r][0] + aij[0][j];
+#pragma unroll
+                for (int i = 1; i < K; ++i)
+                    best = fmax(best, M[r][i] + aij[i][j]);
+                nm[j] = best + le[j];
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                M[r][j] = nm[j];
+        }
+    }
+    const uint64_t ties = __ballot(tie && lane < 2 * kVsSub);
+    for (int sb = 0; sb < kVsSub; ++sb) {
+        const int a0 = t0 + sb * SL;
+        if (a0 >= t1)
+            break;
+        const int a1 = min(a0 + SL, t1);
+        const double hi = vs_hi<K>(dl);
+        bool ok = hi > dev_ninf() && hi != 0.0;
+        const int kd = ok ? vs_binade(hi) : kb0;
+        const int gg = kd - kb0;
+        ok = ok && (gg == 0 || gg == 1);
+        const int src = (ok ? gg : 0) * kVsSub + sb;
+        ok = ok && !((ties >> src) & 1);
+        double nx[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            double best = dl[0] + __shfl(M[0][j], src, 64);
+#pragma unroll
+            for (int r = 1; r < K; ++r)
+                best = fmax(best, dl[r] + __shfl(M[r][j], src, 64));
+            nx[j] = best;
+        }
+        const double edge = -ldexp(1.0 - 0x1p-40, kd + 1);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            ok = ok && (nx[k] == dev_ninf() || nx[k] > edge);
+        if (ok) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                dl[k] = nx[k];
+        } else {
+            vs_sp_steps<MODEL, K, false>(a, ln, sp, a0, a1, dl);
+        }
+    }
+}
+
 /* One chunk of the exact scan from the exact entry dl (wave-uniform): the
  * grid product where the checks hold (a tie chunk through M0 / M1 by the
- * entry values' parities), else step by step.  Row c + 1 of vs_d. */
+ * entry values' parities), else in sub-chunks (vs_cross_chunk; step by step
+ * for Gaussian emissions).  Row c + 1 of vs_d. */
 template <int MODEL, int K>
 __device__ __forceinline__ void vs_exact_chunk(const DevArgs &a, int64_t p, const SpLane<MODEL, K> &ln,
-                                               const SeriesPtrs &sp, const double *blk, int i, int c, int Tp,
-                                               double (&dl)[K])
+                                               const SeriesPtrs &sp, const double *blk, const double *ldsd, int i,
+                                               int c, int Tp, double (&dl)[K])
 {
     const bool l0 = (threadIdx.x & 63) == 0;
     const double hi = vs_hi<K>(dl);
@@ -957,7 +1077,10 @@ __device__ __forceinline__ void vs_exact_chunk(const DevArgs &a, int64_t p, cons
             dl[k] = nx[k];
     } else {
         const int t0 = c * kVsChunk;
-        vs_sp_steps<MODEL, K, false>(a, ln, sp, t0, min(t0 + kVsChunk, Tp), dl);
+        if constexpr (ModelTraits<MODEL>::kDiscrete)
+            vs_cross_chunk<MODEL, K>(a, ln, sp, ldsd, t0, min(t0 + kVsChunk, Tp), dl);
+        else
+            vs_sp_steps<MODEL, K, false>(a, ln, sp, t0, min(t0 + kVsChunk, Tp), dl);
         if (l0)
             a.vs_k[p + a.P * (int64_t)c] = kVsSeq;
     }
@@ -1076,7 +1199,7 @@ __global__ void __launch_bounds__(64) vs_scan1_kernel(const DevArgs a)
             }
             if (f == nb)
                 break;
-            vs_exact_chunk<MODEL, K>(a, p, ln, sp, blk, f, cb + f, Tp, dl);
+            vs_exact_chunk<MODEL, K>(a, p, ln, sp, blk, ldsd, f, cb + f, Tp, dl);
             s = f + 1;
         }
         __syncthreads();
