@@ -2,7 +2,7 @@
 # Runs on the GPU box (via gpurun): the judged default bench line (C2) and
 # every evidence workload, each with its CPU baseline, under its own time
 # limit; stops at the first failure.
-# Usage: tools/round_bench.sh TAG  -> gpurun_out/rb_TAG/{c2,c1,c3,c4,c5,n1,f1}.json
+# Usage: tools/round_bench.sh TAG  -> gpurun_out/rb_TAG/{c2,c1,c3,c4,c5,n1,n2,f1}.json
 set -o pipefail
 TAG=$1
 R=$GRAFT_REPO_ROOT
@@ -14,7 +14,7 @@ run() {
   echo "ok $name"
 }
 run c2 --steps 20 --warmup 5
-for w in c1 c3 c4 c5 n1 f1; do
+for w in c1 c3 c4 c5 n1 n2 f1; do
   run $w --workload $w --steps 5 --warmup 2
 done
 exit 0
