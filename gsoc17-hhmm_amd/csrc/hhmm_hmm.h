@@ -62,6 +62,13 @@ __device__ __forceinline__ bool tayal_pred(int s, int j0)
     const int j = j0 + 1;
     return (s == 1 && (j == 2 || j == 3)) || (s == 2 && (j == 1 || j == 4));
 }
+/* tayal_pred for a compile-time sign class sg (1, 2, or 3 = any other sign):
+ * the kernels whose wave shares one step's sign (one series under many draws,
+ * C5) take the masks as constants, so the masked-off terms cost nothing. */
+__host__ __device__ constexpr bool tayal_on(int sg, int j0)
+{
+    return (sg == 1 && (j0 == 1 || j0 == 2)) || (sg == 2 && (j0 == 0 || j0 == 3));
+}
 /* hhmm-tayal2009.stan:51 */
 __device__ __forceinline__ bool tayal_init_pred(int s, int j0)
 {
@@ -296,11 +303,35 @@ __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const 
  * g_t on the current state, hmm-multinom-semisup.stan:42-44; Tayal sign_t on
  * the current state, hhmm-tayal2009.stan:62-64); no renormalisation.  in may
  * alias out. */
-template <int MODEL, int K>
+template <int MODEL, int K, int SG = -1>
 __device__ __forceinline__ void fwd_step_raw(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
                                              const double (&e)[K], const Obs &o)
 {
     double s[K];
+    if constexpr (SG > 0 && ModelTraits<MODEL>::kTayal) {
+        /* the sign class is known: the off columns take the row total (the
+         * same additions), the on ones the same fma chain -- the same bits */
+        double tot = al[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            tot += al[i];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            if (tayal_on(SG, j)) {
+                double acc = al[0] * pp.A[0][j];
+#pragma unroll
+                for (int i = 1; i < K; ++i)
+                    acc = fma(al[i], pp.A[i][j], acc);
+                s[j] = acc;
+            } else {
+                s[j] = tot;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            out[j] = s[j] * e[j];
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         double acc = al[0] * pp.A[0][j];
@@ -2390,10 +2421,37 @@ __device__ __forceinline__ void renorm_mat(double (&M)[K][K], int &ex)
 /* q <- q B_t for a row vector q: q'(i) = e(i) sum_j q(j) Abar'(j,i), with the
  * model's BACKWARD mask (hhmm-tayal2009.stan:109-111: the predicate on the
  * previous state j; unmasked otherwise). */
-template <int MODEL, int K>
+template <int MODEL, int K, int SG = -1>
 __device__ __forceinline__ void bwd_row_raw(double (&q)[K], const PairParams<MODEL, K> &pp, const double (&e)[K],
                                             const Obs &o)
 {
+    if constexpr (SG > 0 && ModelTraits<MODEL>::kTayal) {
+        /* the sign class is known: the off rows' terms (0 x A, + 0) dropped,
+         * the rest in the same order -- the same bits */
+        double qoff = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (!tayal_on(SG, j))
+                qoff += q[j];
+        double s[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            double acc = 0.0;
+            bool first = true;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                if (tayal_on(SG, j)) {
+                    acc = first ? q[j] * pp.A[j][i] : fma(q[j], pp.A[j][i], acc);
+                    first = false;
+                }
+            }
+            s[i] = acc + qoff;
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            q[i] = s[i] * e[i];
+        return;
+    }
     double qon[K];
     double qoff = 0.0;
 #pragma unroll
@@ -2487,20 +2545,41 @@ __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
                 F[i][j] = f0[j];
         tb = 1;
     }
+    auto prods = [&](auto sgc, const Obs &o, const Em<K> &em) {
+        constexpr int SG = decltype(sgc)::value;
+#pragma unroll
+        for (int r = 0; r < K; ++r)
+            fwd_step_raw<MODEL, K, SG>(F[r], F[r], pp, em.e, o);
+        if constexpr (BWD) {
+#pragma unroll
+            for (int r = 0; r < K; ++r)
+                bwd_row_raw<MODEL, K, SG>(Q[r], pp, em.e, o);
+        }
+    };
     auto step = [&](const Obs &o, bool rn) {
         Em<K> em;
         emit_prob<MODEL, K>(pp, slab, a.L, o, em);
         lsc += em.m;
-#pragma unroll
-        for (int r = 0; r < K; ++r)
-            fwd_step_raw<MODEL, K>(F[r], F[r], pp, em.e, o);
-        if (rn)
+        if constexpr (ModelTraits<MODEL>::kTayal) {
+            /* a wave whose lanes share the step's sign (one series under many
+             * draws: C5) takes the masks as constants (round 4) */
+            const int s0 = __builtin_amdgcn_readfirstlane(o.aux);
+            if (__ballot(o.aux != s0) == 0) {
+                if (s0 == 1)
+                    prods(std::integral_constant<int, 1>(), o, em);
+                else if (s0 == 2)
+                    prods(std::integral_constant<int, 2>(), o, em);
+                else
+                    prods(std::integral_constant<int, 3>(), o, em);
+            } else {
+                prods(std::integral_constant<int, -1>(), o, em);
+            }
+        } else {
+            prods(std::integral_constant<int, -1>(), o, em);
+        }
+        if (rn) {
             renorm_mat<K>(F, fex);
-        if constexpr (BWD) {
-#pragma unroll
-            for (int r = 0; r < K; ++r)
-                bwd_row_raw<MODEL, K>(Q[r], pp, em.e, o);
-            if (rn)
+            if constexpr (BWD)
                 renorm_mat<K>(Q, qex);
         }
     };
