@@ -40,6 +40,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 #include <stdarg.h>
 #include <stdio.h>
@@ -363,11 +364,33 @@ __device__ __forceinline__ void fwd_step_raw(const double (&al)[K], double (&out
 /* rn: renormalise after this step (every step, except the FB_BIG gamma
  * profile's every kBigRenorm-th; the flag is a compile-time constant after
  * unrolling) */
+/* F(sg) with sg a std::integral_constant: the Tayal sign class of the step
+ * when every lane of the wave has the same sign (readfirstlane + ballot: a
+ * wave of one series under many draws, the T-scan's chunks at C5), else -1
+ * (the masks per lane).  Other models: always -1. */
+template <int MODEL, typename F>
+__device__ __forceinline__ void tayal_dispatch(const Obs &o, F &&f)
+{
+    if constexpr (ModelTraits<MODEL>::kTayal) {
+        const int s0 = __builtin_amdgcn_readfirstlane(o.aux);
+        if (__ballot(o.aux != s0) == 0) {
+            if (s0 == 1)
+                f(std::integral_constant<int, 1>());
+            else if (s0 == 2)
+                f(std::integral_constant<int, 2>());
+            else
+                f(std::integral_constant<int, 3>());
+            return;
+        }
+    }
+    f(std::integral_constant<int, -1>());
+}
+
 template <int MODEL, int K>
 __device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
                                             const double (&e)[K], const Obs &o, int &ex, bool rn = true)
 {
-    fwd_step_raw<MODEL, K>(al, out, pp, e, o);
+    tayal_dispatch<MODEL>(o, [&](auto sgc) { fwd_step_raw<MODEL, K, decltype(sgc)::value>(al, out, pp, e, o); });
     if (rn)
         renorm<K>(out, ex);
 }
@@ -380,28 +403,35 @@ __device__ __forceinline__ void fwd_step(double (&al)[K], const PairParams<MODEL
 }
 
 /* beta_{t-1} from beta_t and step t's emission / masks. */
-template <int MODEL, int K>
-__device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL, K> &pp,
-                                         const double (&e)[K], const Obs &o, int &ex, bool rn = true)
+template <int MODEL, int K, int SG>
+__device__ __forceinline__ void bwd_step_sg(double (&be)[K], const PairParams<MODEL, K> &pp, const double (&e)[K],
+                                            const Obs &o)
 {
     double b[K];
 #pragma unroll
     for (int i = 0; i < K; ++i)
         b[i] = e[i] * be[i];
     double s[K];
+    double tot = 0.0;
+    if constexpr (ModelTraits<MODEL>::kTayal) {
+        tot = b[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            tot += b[i];
+    }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
+        if (SG > 0 && !tayal_on(SG, j)) { /* known off: the row total alone (the same bits) */
+            s[j] = tot;
+            continue;
+        }
         double acc = pp.A[j][0] * b[0];
 #pragma unroll
         for (int i = 1; i < K; ++i)
             acc = fma(pp.A[j][i], b[i], acc);
         s[j] = acc;
     }
-    if constexpr (ModelTraits<MODEL>::kTayal) { /* predicate on the PREVIOUS state j (Q6) */
-        double tot = b[0];
-#pragma unroll
-        for (int i = 1; i < K; ++i)
-            tot += b[i];
+    if constexpr (ModelTraits<MODEL>::kTayal && SG < 0) { /* predicate on the PREVIOUS state j (Q6) */
 #pragma unroll
         for (int j = 0; j < K; ++j)
             s[j] = tayal_pred(o.aux, j) ? s[j] : tot;
@@ -409,6 +439,13 @@ __device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL
 #pragma unroll
     for (int j = 0; j < K; ++j)
         be[j] = s[j];
+}
+
+template <int MODEL, int K>
+__device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL, K> &pp,
+                                         const double (&e)[K], const Obs &o, int &ex, bool rn = true)
+{
+    tayal_dispatch<MODEL>(o, [&](auto sgc) { bwd_step_sg<MODEL, K, decltype(sgc)::value>(be, pp, e, o); });
     if (rn)
         renorm<K>(be, ex);
 }
@@ -2560,23 +2597,9 @@ __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
         Em<K> em;
         emit_prob<MODEL, K>(pp, slab, a.L, o, em);
         lsc += em.m;
-        if constexpr (ModelTraits<MODEL>::kTayal) {
-            /* a wave whose lanes share the step's sign (one series under many
-             * draws: C5) takes the masks as constants (round 4) */
-            const int s0 = __builtin_amdgcn_readfirstlane(o.aux);
-            if (__ballot(o.aux != s0) == 0) {
-                if (s0 == 1)
-                    prods(std::integral_constant<int, 1>(), o, em);
-                else if (s0 == 2)
-                    prods(std::integral_constant<int, 2>(), o, em);
-                else
-                    prods(std::integral_constant<int, 3>(), o, em);
-            } else {
-                prods(std::integral_constant<int, -1>(), o, em);
-            }
-        } else {
-            prods(std::integral_constant<int, -1>(), o, em);
-        }
+        /* a wave whose lanes share the step's sign (one series under many
+         * draws: C5) takes the masks as constants (round 4) */
+        tayal_dispatch<MODEL>(o, [&](auto sgc) { prods(sgc, o, em); });
         if (rn) {
             renorm_mat<K>(F, fex);
             if constexpr (BWD)
