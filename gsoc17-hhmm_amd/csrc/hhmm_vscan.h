@@ -411,16 +411,22 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
     vs_steps<MODEL, VAUX>(sp, v.t0, v.t1, [&](int, const Obs &o) {
         double le[K];
         emit_log<MODEL, K>(pp, slab, a.L, o, le);
-        bool on[K];
         V lv[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             if constexpr (GRID && ModelTraits<MODEL>::kGauss)
                 le[j] = vs_grid(le[j], iu, u, tie);
             lv[j] = (V)le[j];
+        }
+        /* the Tayal sign class as a constant where the wave shares it */
+        tayal_dispatch<MODEL>(o, [&](auto sgc) {
+        constexpr int SG = decltype(sgc)::value;
+        bool on[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
             on[j] = true;
             if constexpr (ModelTraits<MODEL>::kTayal)
-                on[j] = tayal_pred(o.aux, j);
+                on[j] = SG > 0 ? tayal_on(SG, j) : tayal_pred(o.aux, j);
         }
 #pragma unroll
         for (int r = 0; r < K; ++r) {
@@ -448,6 +454,7 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
             for (int j = 0; j < K; ++j)
                 M[r][j] = nm[j];
         }
+        });
     });
 #pragma unroll
     for (int r = 0; r < K; ++r)
@@ -488,16 +495,16 @@ __device__ __forceinline__ double vs_hi(const double (&D)[K])
 
 /* One step of the reference's recursion (vit_step's arithmetic) that also
  * returns each state's arg max. */
-template <int MODEL, int K, bool NANIN>
-__device__ __forceinline__ void vs_step(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
-                                        const Obs &o, int (&arg)[K])
+template <int MODEL, int K, bool NANIN, int SG = -1>
+__device__ __forceinline__ void vs_step_sg(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
+                                           const Obs &o, int (&arg)[K])
 {
     double nd[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         bool on = true;
         if constexpr (ModelTraits<MODEL>::kTayal)
-            on = tayal_pred(o.aux, j);
+            on = SG > 0 ? tayal_on(SG, j) : tayal_pred(o.aux, j);
         double best = dev_ninf();
         int am = 0;
 #pragma unroll
@@ -523,6 +530,15 @@ __device__ __forceinline__ void vs_step(double (&dl)[K], const PairParams<MODEL,
 #pragma unroll
     for (int j = 0; j < K; ++j)
         dl[j] = nd[j];
+}
+
+/* vs_step with the Tayal sign class as a constant where the wave shares it
+ * (tayal_dispatch: one series under many draws; the same operations) */
+template <int MODEL, int K, bool NANIN>
+__device__ __forceinline__ void vs_step(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
+                                        const Obs &o, int (&arg)[K])
+{
+    tayal_dispatch<MODEL>(o, [&](auto sgc) { vs_step_sg<MODEL, K, NANIN, decltype(sgc)::value>(dl, pp, le, o, arg); });
 }
 
 /* Chunk 0 from the model's first row: delta_tk[1] has only column K written
