@@ -70,6 +70,16 @@ __host__ __device__ constexpr bool tayal_on(int sg, int j0)
 {
     return (sg == 1 && (j0 == 1 || j0 == 2)) || (sg == 2 && (j0 == 0 || j0 == 3));
 }
+/* The flattened HHMM's structural transition pattern (hhmm-tayal2009.stan:
+ * 36-44; load_params builds A = {{0, r00, r01, 0}, {1, 0, 0, 0},
+ * {r10, 0, 0, r11}, {0, 0, 1, 0}}): entry (i, j) can be nonzero.  A term with
+ * a structural zero adds exactly nothing (0 x f to a linear sum, a -inf
+ * candidate to a max-plus one), so the sign-class paths skip it. */
+__host__ __device__ constexpr bool tayal_nz(int i, int j)
+{
+    return (i == 0 && (j == 1 || j == 2)) || (i == 1 && j == 0) || (i == 2 && (j == 0 || j == 3)) ||
+           (i == 3 && j == 2);
+}
 /* hhmm-tayal2009.stan:51 */
 __device__ __forceinline__ bool tayal_init_pred(int s, int j0)
 {
@@ -319,10 +329,17 @@ __device__ __forceinline__ void fwd_step_raw(const double (&al)[K], double (&out
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             if (tayal_on(SG, j)) {
-                double acc = al[0] * pp.A[0][j];
+                /* the structurally nonzero terms in the same order (a zero term
+                 * 0 x f adds nothing to the chain: the same bits) */
+                double acc = 0.0;
+                bool first = true;
 #pragma unroll
-                for (int i = 1; i < K; ++i)
-                    acc = fma(al[i], pp.A[i][j], acc);
+                for (int i = 0; i < K; ++i) {
+                    if (tayal_nz(i, j)) {
+                        acc = first ? al[i] * pp.A[i][j] : fma(al[i], pp.A[i][j], acc);
+                        first = false;
+                    }
+                }
                 s[j] = acc;
             } else {
                 s[j] = tot;
@@ -423,6 +440,20 @@ __device__ __forceinline__ void bwd_step_sg(double (&be)[K], const PairParams<MO
     for (int j = 0; j < K; ++j) {
         if (SG > 0 && !tayal_on(SG, j)) { /* known off: the row total alone (the same bits) */
             s[j] = tot;
+            continue;
+        }
+        if constexpr (SG > 0 && ModelTraits<MODEL>::kTayal) {
+            /* known on: row j's structurally nonzero terms in the same order */
+            double acc = 0.0;
+            bool first = true;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                if (tayal_nz(j, i)) {
+                    acc = first ? pp.A[j][i] * b[i] : fma(pp.A[j][i], b[i], acc);
+                    first = false;
+                }
+            }
+            s[j] = acc;
             continue;
         }
         double acc = pp.A[j][0] * b[0];
@@ -2477,7 +2508,7 @@ __device__ __forceinline__ void bwd_row_raw(double (&q)[K], const PairParams<MOD
             bool first = true;
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-                if (tayal_on(SG, j)) {
+                if (tayal_on(SG, j) && tayal_nz(j, i)) {
                     acc = first ? q[j] * pp.A[j][i] : fma(q[j], pp.A[j][i], acc);
                     first = false;
                 }

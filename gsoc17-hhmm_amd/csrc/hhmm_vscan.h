@@ -446,7 +446,8 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
                     best = M[r][0] + Av[0][j];
 #pragma unroll
                     for (int i = 1; i < K; ++i)
-                        best = fmax(best, M[r][i] + Av[i][j]);
+                        if (!(SG > 0 && ModelTraits<MODEL>::kTayal && !tayal_nz(i, j))) /* -inf: no effect */
+                            best = fmax(best, M[r][i] + Av[i][j]);
                 }
                 nm[j] = best + lv[j];
             }
@@ -509,6 +510,11 @@ __device__ __forceinline__ void vs_step_sg(double (&dl)[K], const PairParams<MOD
         int am = 0;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
+            /* a known-on column's structural zeros (log A = -inf) past i = 0:
+             * a -inf / NaN candidate changes neither the max nor the arg max */
+            if constexpr (SG > 0 && ModelTraits<MODEL>::kTayal)
+                if (i > 0 && on && !tayal_nz(i, j))
+                    continue;
             double cand;
             if constexpr (ModelTraits<MODEL>::kTayal) {
                 cand = dl[i] + le[j];
