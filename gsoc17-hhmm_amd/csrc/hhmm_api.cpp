@@ -869,7 +869,9 @@ hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res, void *wor
         set_error("workspace of %zu bytes < %zu required", workspace_bytes_, need);
         return HHMM_ERR_INVALID_ARGUMENT;
     }
-    return launch_all(req, res, npairs(req), workspace, (hipStream_t)stream);
+    /* the data arrays are device memory: their data-block bounds are checked on
+     * the device, pair by pair (HHMM_PAIR_INVALID_DATA) */
+    return launch_all(req, res, npairs(req), workspace, (hipStream_t)stream, nullptr, 0, true);
 }
 
 hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res)
@@ -1023,7 +1025,7 @@ static hhmm_status segment_run(const hhmm_request *req, hhmm_result *res, const 
         set_error("workspace of %zu bytes < %zu required (hhmm_segment_workspace_size)", wsb, need);
         return HHMM_ERR_INVALID_ARGUMENT;
     }
-    return launch_all(&r2, rr, npairs(&r2), ws, (hipStream_t)stream, seg, phase);
+    return launch_all(&r2, rr, npairs(&r2), ws, (hipStream_t)stream, seg, phase, phase == 2);
 }
 
 hhmm_status hhmm_segment_summary_device(const hhmm_request *req, const hhmm_segment *seg, void *workspace,

@@ -1699,19 +1699,28 @@ __device__ __forceinline__ uint32_t pack_chunk(const Obs (&cur)[8])
     return w;
 }
 
-/* Phase 1: the max-plus forward over x, packing each chunk's symbols. */
+/* Phase 1: the max-plus forward over x, packing each chunk's symbols.  The
+ * packing also checks the data block's bound on x (int<lower=1,upper=L> x[T],
+ * hmm-multinom.stan:11) for the steps t < Tp: bad = some symbol is outside
+ * 1..L (the device entry's HHMM_PAIR_INVALID_DATA, at no extra read of x). */
 template <int MODEL, int K>
 __device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const PairParams<MODEL, K> &pp,
                                             const double2 *slab, const SeriesPtrs &sp, int Tp, int Tw_min,
-                                            int Tw_max, double (&dl)[K], uint32_t &word)
+                                            int Tw_max, double (&dl)[K], uint32_t &word, bool &bad)
 {
     constexpr int CV = vit_chunk(K);
     static_assert(CV == 8, "phased sweep: 8-step chunks");
     const int nfull = Tw_min / CV;
     const int nchunk = (Tw_max + CV - 1) / CV;
+    const uint32_t L = (uint32_t)a.L;
+    uint32_t oob = 0;
     auto pack_put = [&](int c, const Obs (&cur)[CV]) {
-        if (c * CV < Tp)
+        if (c * CV < Tp) {
             put_tmp(a.xpk + a.P * (int64_t)c, (uint32_t)p * 4u, pack_chunk<MODEL, K>(cur));
+#pragma unroll
+            for (int v = 0; v < CV; ++v)
+                oob |= ((uint32_t)(cur[v].x - 1) >= L) & (c * CV + v < Tp);
+        }
     };
     Obs cur[CV];
     load_chunk<MODEL, CV, false>(cur, sp, 0);
@@ -1759,6 +1768,7 @@ __device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const P
         for (int u = 0; u < CV; ++u)
             cur[u] = nxt[u];
     }
+    bad = oob != 0;
 }
 
 /* Phase 2: the scaled filter over the packed symbols (FB_BIG checkpoints),
@@ -1876,7 +1886,10 @@ __device__ __forceinline__ void vfb_block(const DevArgs &a, int64_t gwave)
         const SeriesPtrs sp = series_ptrs<MODEL, false>(a, n);
         double dl[K];
         uint32_t word;
-        vfb_viterbi<MODEL, K>(a, p, lpp, slab, sp, Tp, Tw_min, Tw_max, dl, word);
+        bool bad;
+        vfb_viterbi<MODEL, K>(a, p, lpp, slab, sp, Tp, Tw_min, Tw_max, dl, word, bad);
+        if (a.T)
+            bad |= a.T[n] < 1 || a.T[n] > a.Tmax;
         constexpr int SPW = bp_steps_per_word(K);
         if ((Tp - 1) % SPW != SPW - 1) /* partial last word */
             put_tmp(a.bp + a.P * (int64_t)((Tp - 1) / SPW), (uint32_t)p * 4u, word);
@@ -1890,7 +1903,7 @@ __device__ __forceinline__ void vfb_block(const DevArgs &a, int64_t gwave)
         if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
             a.logp_zstar[p] = lpz;
         if (a.pair_status)
-            a.pair_status[p] = invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
+            a.pair_status[p] = bad ? HHMM_PAIR_INVALID_DATA : invalid ? HHMM_PAIR_INVALID_BACKPOINTER : HHMM_PAIR_OK;
         if (invalid)
             z = 0;
     }
@@ -3372,6 +3385,7 @@ static hhmm_status launch_vfb(const DevArgs &a, hipStream_t st)
     }
     hipError_t e = hipMemsetAsync(a.rnw, 0, sizeof(int32_t), st); /* the dense-wave list's count */
     if (e == hipSuccess) {
+        t_data_checked_inline = !ModelTraits<MODEL>::kAux; /* x (and T) checked in phase 1 */
         hipLaunchKernelGGL((vfb_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
         hipLaunchKernelGGL((vfb_dense_kernel<MODEL, K>), dim3(kDenseBlocks), dim3(64), s.lds / (s.block.x / 64), st,
                            a);

@@ -92,6 +92,7 @@ struct DevArgs {
     int32_t *vs_fail;   /* [P]          a replayed chunk disagreed: decode again sequentially */
     int32_t *vs_tl;     /* [1 + P*nc]   chunks with a grid rounding tie: count, then p + P c */
     const int32_t *vs_redo; /* state-parallel decoder: only pairs with vs_redo[p] != 0 (null: all) */
+    int32_t *dc_flag;       /* [N] device entry: series breaking a data-block constraint (null: host-validated) */
     /* one time window of a series split over ranks (hhmm_segment; 0: a whole series) */
     int32_t seg_phase;      /* 1: summary call, 2: finish call */
     int32_t seg_nofirst;    /* the window does not start at t = 1: chunk 0 enters from seg_enter */
@@ -143,9 +144,15 @@ size_t workspace_bytes(int model, int K, int L, int Tmax, int Toos, int64_t P, u
 /* Carves the workspace into DevArgs pointers. */
 void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags);
 
-/* Launches every kernel the request needs on `stream` (device pointers). */
+/* Launches every kernel the request needs on `stream` (device pointers).
+ * check_data: the data arrays were not validated on the host (the device
+ * entry): flag pairs whose series breaks a data-block constraint
+ * (HHMM_PAIR_INVALID_DATA) after the model's kernels. */
 hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws, hipStream_t st,
-                       const hhmm_segment *seg = nullptr, int seg_phase = 0);
+                       const hhmm_segment *seg = nullptr, int seg_phase = 0, bool check_data = false);
+/* Set by a launcher whose kernel checks the data-block constraints inline
+ * (the phased sweep, launch_vfb): launch_all then skips its separate pass. */
+extern thread_local bool t_data_checked_inline;
 
 /* HMM family, one translation unit per model / K range (hhmm_m_*.hip). */
 hhmm_status run_gauss_lo(const DevArgs &a, const hhmm_request *req, const hhmm_result *res, hipStream_t st);

@@ -200,6 +200,7 @@ int vscan_chunks(int model, int K, int Tv, int64_t P, uint32_t outputs, uint32_t
 struct WsLayout {
     size_t ckpt, ckpt_ls, xpk, rnw, bp, lam, ior, mf, qb, mx, st, sl, be, bl, total;
     size_t vm, vm1, vd, vk, ve, vz, vf, vt;
+    size_t dc; /* [N] int32 data-check flags (the device entry) */
     int vnc;
     ScanPlan sp;
 };
@@ -212,6 +213,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
     w.ckpt = w.ckpt_ls = w.xpk = w.rnw = w.bp = w.lam = w.ior = w.mf = w.qb = w.mx = w.st = w.sl = w.be = w.bl = NONE;
     w.vm = w.vm1 = w.vd = w.vk = w.ve = w.vz = w.vf = w.vt = NONE;
     w.vnc = 0;
+    w.dc = NONE;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -246,6 +248,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
             w.lam = take((size_t)Tmax * P * d);
         if (is_iohmm_model(model) && (outputs & kIoFilt))
             w.ior = take((size_t)(1 + P) * sizeof(int32_t));
+        w.dc = take((size_t)N * sizeof(int32_t));
         w.total = off + 256;
         return w;
     }
@@ -295,6 +298,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
         w.lam = take((size_t)Tmax * P * d);
     if (is_iohmm_model(model) && (outputs & kIoFilt))
         w.ior = take((size_t)(1 + P) * sizeof(int32_t));
+    w.dc = take((size_t)N * sizeof(int32_t));
     w.total = off + 256;
     return w;
 }
@@ -335,6 +339,7 @@ void bind_workspace(DevArgs &a, void *ws, int Tmax, int Toos, uint32_t flags)
     a.vs_z = (int32_t *)at_off(w.vz);
     a.vs_fail = (int32_t *)at_off(w.vf);
     a.vs_tl = (int32_t *)at_off(w.vt);
+    a.dc_flag = (int32_t *)at_off(w.dc);
 }
 
 DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
@@ -397,6 +402,86 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
     return a;
 }
 
+/* ------------------------------------------------------------------ */
+/* Data-block constraints on the device entry (HHMM_PAIR_INVALID_DATA)   */
+/* ------------------------------------------------------------------ */
+thread_local bool t_data_checked_inline = false;
+
+constexpr int kDcSteps = 64; /* time steps per thread of data_check_kernel */
+
+/* Flags series n when one of its steps t < T[n] breaks an int<lower=1,
+ * upper=hi> bound: v (x, 1..L), w (sign 1..2 / g 1..G; null: none).  Lanes
+ * run over series (the fastest index: coalesced rows), grid.y over strips of
+ * kDcSteps steps.  A flag is a plain vector store of 1 (every writer stores
+ * the same value). */
+__global__ void __launch_bounds__(256) data_check_kernel(const int32_t *v, int vhi, const int32_t *w, int whi,
+                                                         const int32_t *T, int64_t N, int Tmax, int32_t *flag)
+{
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N)
+        return;
+    const int Tn = T ? min(max(T[n], 1), Tmax) : Tmax; /* a length outside 1..T_max: data_mark_kernel */
+    const int t0 = (int)blockIdx.y * kDcSteps;
+    const int t1 = min(t0 + kDcSteps, Tn);
+    bool bad = false;
+    for (int t = t0; t < t1; ++t) {
+        const int64_t i = n + N * (int64_t)t;
+        bad |= (uint32_t)(v[i] - 1) >= (uint32_t)vhi;
+        if (w)
+            bad |= (uint32_t)(w[i] - 1) >= (uint32_t)whi;
+    }
+    if (bad)
+        flag[n] = 1;
+}
+
+/* pair_status[p] = HHMM_PAIR_INVALID_DATA for the pairs of flagged series and
+ * of series whose T[n] / T_oos[n] lies outside 1..T_max / 1..T_oos_max. */
+__global__ void __launch_bounds__(256) data_mark_kernel(const DevArgs a, const int32_t *T_oos, int Toos_max)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.P)
+        return;
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    bool bad = a.dc_flag[n] != 0;
+    if (a.T)
+        bad |= a.T[n] < 1 || a.T[n] > a.Tmax;
+    if (T_oos)
+        bad |= T_oos[n] < 1 || T_oos[n] > Toos_max;
+    if (bad)
+        a.pair_status[p] = HHMM_PAIR_INVALID_DATA;
+}
+
+static hhmm_status launch_data_check(const DevArgs &a, const hhmm_request *req, hipStream_t st, bool inline_checked)
+{
+    const hhmm_data &d = req->data;
+    const int m = req->model;
+    const bool discrete = m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ||
+                          m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE;
+    const bool tayal = m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE;
+    hipError_t e = hipMemsetAsync(a.dc_flag, 0, (size_t)d.n_series * sizeof(int32_t), st);
+    auto check = [&](const int32_t *v, int vhi, const int32_t *w, int whi, const int32_t *T, int Tmax) {
+        const dim3 grid((unsigned)((d.n_series + 255) / 256), (unsigned)((Tmax + kDcSteps - 1) / kDcSteps));
+        hipLaunchKernelGGL(data_check_kernel, grid, dim3(256), 0, st, v, vhi, w, whi, T, (int64_t)d.n_series, Tmax,
+                           a.dc_flag);
+    };
+    if (e == hipSuccess && discrete && !inline_checked)
+        check(d.x_int, d.L, tayal ? d.sign : (m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ? d.g : nullptr),
+              tayal ? 2 : d.G, d.T, d.T_max);
+    if (e == hipSuccess && m == HHMM_MODEL_TAYAL_LITE)
+        check(d.x_oos, d.L, d.sign_oos, 2, d.T_oos, d.T_oos_max);
+    if (e == hipSuccess)
+        hipLaunchKernelGGL(data_mark_kernel, dim3((unsigned)((a.P + 255) / 256)), dim3(256), 0, st, a,
+                           m == HHMM_MODEL_TAYAL_LITE ? d.T_oos : nullptr, d.T_oos_max);
+    if (e == hipSuccess)
+        e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("data check: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
 /* An IOHMM sweep with its log-space fallback: the list of underflowed pairs
  * is cleared, the sweep lists them, launch_iohmm_log re-runs them (all on `st`). */
 static hhmm_status run_iohmm_filtered(const DevArgs &a, hipStream_t st, hhmm_status (*sweep)(const DevArgs &, hipStream_t))
@@ -414,11 +499,16 @@ static hhmm_status run_iohmm_filtered(const DevArgs &a, hipStream_t st, hhmm_sta
     return launch_iohmm_log(a, st);
 }
 
+static hhmm_status launch_model(const hhmm_request *req, const DevArgs &a, const hhmm_result *res, hipStream_t st);
+
 hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws, hipStream_t st,
-                       const hhmm_segment *seg, int seg_phase)
+                       const hhmm_segment *seg, int seg_phase, bool check_data)
 {
     DevArgs a = make_args(req, res, P);
     bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max, (uint32_t)req->flags);
+    const bool check = check_data && a.pair_status && a.dc_flag;
+    if (!check)
+        a.dc_flag = nullptr;
     if (seg) {
         a.seg_phase = seg_phase;
         a.seg_nofirst = !seg->first;
@@ -431,6 +521,15 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
             return HHMM_ERR_UNSUPPORTED;
         }
     }
+    t_data_checked_inline = false;
+    hhmm_status s = launch_model(req, a, res, st);
+    if (s != HHMM_OK || !check)
+        return s;
+    return launch_data_check(a, req, st, t_data_checked_inline);
+}
+
+static hhmm_status launch_model(const hhmm_request *req, const DevArgs &a, const hhmm_result *res, hipStream_t st)
+{
     const bool lo = a.K <= 4;
     if (a.K > kMaxK) {
         if (a.K > kMaxKLarge) {

@@ -78,6 +78,13 @@ typedef enum hhmm_status {
 /* Per-pair status codes (hhmm_result.pair_status). */
 #define HHMM_PAIR_OK 0
 #define HHMM_PAIR_INVALID_BACKPOINTER 1
+/* hhmm_run_device only (hhmm_run rejects the whole request instead, as Stan
+ * rejects the data block): the pair's series breaks a data-block constraint --
+ * x outside 1..L (int<lower=1,upper=L> x[T], hmm-multinom.stan:11), sign outside
+ * 1..2 (hhmm-tayal2009.stan:11-12), g outside 1..G, T[n] outside 1..T_max, or
+ * the same for the tayal-lite out-of-sample arrays.  The pair's outputs are
+ * unspecified; every other pair is computed as usual. */
+#define HHMM_PAIR_INVALID_DATA 2
 
 /* One id per Stan program on the path. */
 typedef enum hhmm_model {
@@ -307,7 +314,10 @@ hhmm_status hhmm_run(const hhmm_request *req, hhmm_result *res);
 /* Device-resident entry: every pointer in req/res is a device pointer on the
  * current HIP device; enqueues on `stream` (hipStream_t, NULL = default) and
  * returns without synchronising.  `workspace` must hold
- * hhmm_workspace_size() bytes.  Per-pair failures land in res->pair_status. */
+ * hhmm_workspace_size() bytes.  Per-pair failures land in res->pair_status,
+ * among them the data-block bounds hhmm_run checks on the host: a pair whose
+ * series breaks one is flagged HHMM_PAIR_INVALID_DATA (when pair_status is
+ * given), every other pair is unaffected. */
 hhmm_status hhmm_workspace_size(const hhmm_request *req, size_t *bytes);
 hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res,
                             void *workspace, size_t workspace_bytes, void *stream);

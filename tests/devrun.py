@@ -37,10 +37,12 @@ class DeviceRequest:
             self._keep["ffbs_u"] = torch.from_numpy(uu.reshape(-1, order="F").copy()).to(self.dev)
             req.ffbs_u = self._keep["ffbs_u"].data_ptr()
         P, T, K = host.P, host.Tmax, host.K
+        To = host.T_oos_max
         req.outputs = 0
         req.flags = int(flags)
         self.out = {}
-        shapes = {"P": (P,), "PTK": (K, T, P), "PT": (T, P), "PTz": (T, P)}
+        Tz = To if model == "hhmm-tayal2009-lite" else T
+        shapes = {"P": (P,), "PTK": (K, T, P), "PT": (T, P), "PTz": (Tz, P), "PToK": (K, To, P)}
         for name in pars:
             dt, code = _abi.RESULT_ARRAYS[name]
             buf = torch.full(shapes[code], float("nan"), dtype=torch.float64, device=self.dev) if dt == "f64" \

@@ -147,3 +147,120 @@ def test_in_sample_feature_histogram_matches_report_table4(oracle):
     x, sign = legs["x"][ins], legs["sign"][ins]
     assert tuple(np.bincount(x[sign == 1], minlength=10)[1:]) == TABLE4_U
     assert tuple(np.bincount(x[sign == 2], minlength=10)[1:]) == TABLE4_D
+
+
+# ---- Reference-held pin of the Tayal forward (A2/A6/A7/A12 with the Q6 mask) -------------------
+#
+# Table 4 of main.pdf (main.Rmd:704-723) is table(x.ins, state.filtered.ins), where
+# state.filtered.ins is the per-t which.max of the median over draws of hhmm-tayal2009-lite's
+# alpha_tk (main.Rmd:436, 596-602).  Rows = bottom states 1..4, columns = U1..U9, D1..D9.
+TABLE4 = np.array([
+    [0, 15, 0, 810, 0, 828, 33, 0, 17, 0, 0, 0, 0, 0, 0, 0, 0, 0],
+    [0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 72, 0, 0, 2208, 0, 181, 0, 59],
+    [0, 0, 0, 0, 0, 0, 0, 27, 0, 15, 0, 34, 831, 0, 846, 0, 16, 0],
+    [58, 0, 158, 0, 2155, 0, 0, 22, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0]])
+
+# Table 8 of main.pdf (main.Rmd:869-907): posterior means of the same fit, printed to 2 decimals.
+# p_1k = (.51, 0, .49, 0); A_ij: a12 .46, a13 .54, a21 1, a31 .09, a34 .91, a43 1.
+TABLE8_P11 = 0.51
+TABLE8_A_ROW = ((0.46, 0.54), (0.09, 0.91))
+TABLE8_PHI = np.array([
+    [.01, .02, .01, .34, .22, .35, .03, .01, .02],
+    [.00, .02, .00, .05, .80, .02, .08, .00, .02],
+    [.01, .00, .03, .36, .20, .39, .00, .02, .00],
+    [.02, .00, .06, .02, .88, .01, .00, .01, .00]])
+# A printed 0.00 is a simplex entry below 0.005, never exactly 0 (simplex[L] phi_k, lite.stan:25);
+# it is floored at the midpoint of [0, 0.005) and each row renormalised.
+PHI_FLOOR = 0.0025
+
+
+def table8_draw():
+    phi = np.where(TABLE8_PHI == 0.0, PHI_FLOOR, TABLE8_PHI)
+    phi = phi / phi.sum(axis=1, keepdims=True)
+    return {"p_11": np.array([TABLE8_P11]), "A_row": np.array([TABLE8_A_ROW]), "phi_k": phi[None]}
+
+
+def table8_flat(draw):
+    """hhmm-tayal2009-lite.stan:34-48: the transformed-parameters expansion."""
+    p11, (r1, r2) = draw["p_11"][0], draw["A_row"][0]
+    p_1k = np.array([[p11, 0.0, 1.0 - p11, 0.0]])
+    A = np.zeros((1, 4, 4))
+    A[0, 0, 1], A[0, 0, 2], A[0, 1, 0], A[0, 2, 0], A[0, 2, 3], A[0, 3, 2] = r1[0], r1[1], 1, r2[0], r2[1], 1
+    return p_1k, A
+
+
+def tabulate(feature, state):
+    """table(x.ins, state) laid out like Table 4: [state, feature]."""
+    t = np.zeros((4, 18), dtype=np.int64)
+    np.add.at(t, (state - 1, feature - 1), 1)
+    return t
+
+
+def table_agreement(got):
+    """Observations whose (feature, state) cell is shared with Table 4: sum of cell-wise minima."""
+    return int(np.minimum(got, TABLE4).sum())
+
+
+def _gto_legs(oracle):
+    from hhmm_amd import features as F
+    files = [DATA / "G.TO" / f"{d}.G.TO.RData" for d in RMD_DAYS]
+    price, size, time = rdata.load_ticks(files)
+    legs = oracle.extract_features(price, size, time, alpha=0.25)
+    when = time[F.index_ticks(legs, price)]
+    return legs, F.xts_window(when, RMD_INS), F.xts_window(when, RMD_OOS)
+
+
+@pytest.mark.skipif(not DATA.exists(), reason="reference tick data not present (GPU box)")
+def test_tayal_forward_reproduces_report_table4(oracle):
+    """Pins the oracle's Tayal forward to the reference's own output.  The report's chain on
+    CPU: six G.TO files -> extract_features -> in-sample / OOS windows (main.Rmd:405-446) ->
+    hhmm-tayal2009-lite at Table 8's posterior means -> which.max(alpha_tk) per t, tabulated
+    against the 18 features.  A point estimate stands in for the median over 250 draws, so a
+    few observations near a decision boundary may move (U6, U8); every other cell must agree,
+    including the Q6-mask cells where up legs go to the bear state 1 (U2/U4/U6/U7/U9) and the
+    single D5 observation in state 4."""
+    legs, ins, oos = _gto_legs(oracle)
+    feat, x, sign = legs["feature"][ins], legs["x"][ins], legs["sign"][ins]
+    assert feat.size == 8386 and np.array_equal(feat, np.where(sign == 1, x, x + 9))
+    data = {"K": 4, "L": 9, "x": x, "sign": sign, "x_oos": legs["x"][oos], "sign_oos": legs["sign"][oos]}
+    draw = table8_draw()
+    out = oracle.gqs("hhmm-tayal2009-lite", data, draw, pars=["alpha_tk", "alpha_tk_oos", "zstar_t"])
+    got = tabulate(feat, np.argmax(out["alpha_tk"][0], axis=1) + 1)
+    assert got.sum() == 8386
+    agree = table_agreement(got)
+    assert agree >= 8350, (agree, got)
+    # the 16 features other than U6 and U8 land exactly where the report put them
+    exact = [c for c in range(18) if c not in (5, 7)]
+    assert np.array_equal(got[:, exact], TABLE4[:, exact]), got
+    assert got[1, 13] == 2208 and got[3, 13] == 1  # D5: 2208 in state 2, one in state 4
+    assert got[0, 5] + got[2, 5] == 828 and got[0, 5] >= 800  # U6 mostly in state 1, as the report
+    assert got[2, 7] + got[3, 7] == 49  # U8 split between states 3 and 4, as the report
+    print(f"Table 4 agreement {agree} / 8386; U6 {got[:, 5]}, U8 {got[:, 7]}")
+
+    # The check discriminates: without the sign mask (the transition applied for every j and the
+    # initial distribution for every j, i.e. the plain multinomial HMM of hmm-multinom.stan at the
+    # same expanded parameters) the table falls apart.
+    p_1k, A = table8_flat(draw)
+    plain = oracle.gqs("hmm-multinom", {"K": 4, "L": 9, "x": x},
+                       {"p_1k": p_1k, "A_ij": A, "phi_k": draw["phi_k"]}, pars=["alpha_tk"])
+    nomask = table_agreement(tabulate(feat, np.argmax(plain["alpha_tk"][0], axis=1) + 1))
+    print(f"no-mask agreement {nomask} / 8386")
+    assert nomask < 5000, nomask
+
+
+@pytest.mark.skipif(not DATA.exists(), reason="reference tick data not present (GPU box)")
+def test_table4_point_oracle_vs_numpy_transcription(oracle):
+    """The same real-data request through the independent pure-Python transcription
+    (tests/oracle_numpy.py): every in-sample and OOS output of the lite model agrees with the
+    C oracle, so the Table 4 pin above covers both restatements."""
+    import oracle_numpy as onp
+    from tolerances import compare
+    legs, ins, oos = _gto_legs(oracle)
+    x, sign, xo, so = legs["x"][ins], legs["sign"][ins], legs["x"][oos], legs["sign"][oos]
+    data = {"K": 4, "L": 9, "x": x, "sign": sign, "x_oos": xo, "sign_oos": so}
+    draw = table8_draw()
+    pars = ["loglik", "unalpha_tk", "alpha_tk", "unalpha_tk_oos", "alpha_tk_oos", "zstar_t", "logp_zstar"]
+    got = oracle.gqs("hhmm-tayal2009-lite", data, draw, pars=pars)
+    ref = onp.tayal_lite(x.size, x, sign, xo.size, xo, so, draw["p_11"][0], draw["A_row"][0], draw["phi_k"][0])
+    for name in pars:
+        compare(name, np.asarray(got[name])[0], np.asarray(ref[name]))
