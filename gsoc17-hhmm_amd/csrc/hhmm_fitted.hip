@@ -18,32 +18,15 @@
  * (correctly rounded exp in the softmax), so hatz / hatl / hatx match it
  * exactly.
  *
- * Layout: one lane per pair; every per-step load and store is a coalesced
- * pair-fastest wave transaction (u_t is a broadcast in GRID pairing).  The
+ * Layout (K <= 8): one lane per pair; every per-step load and store is a
+ * coalesced pair-fastest wave transaction (u_t is a broadcast in GRID
+ * pairing); 8 < K <= 32: a group of lanes per pair (hhmm_lkio.h).  The
  * kernel is HBM-bound at (K*8 hatpi + 4 + 4 + 8 outputs + 24 random inputs)
  * B per series-timestep.
  */
-#include "hhmm_iohmm.h"
+#include "hhmm_lkio.h"
 
 namespace hhmm {
-
-/* Stan Math categorical_rng(theta) with the caller's uniform:
- * index = cumulative_sum(theta); b = 0; while (c > index[b]) ++b (bounded to
- * n - 1: a uniform above a rounded-down total lands in the last category). */
-template <int NMAX>
-__device__ __forceinline__ int stan_categorical(const double (&th)[NMAX], int n, double u)
-{
-    int b = 0;
-    double cum = th[0];
-#pragma unroll
-    for (int i = 1; i < NMAX; ++i) {
-        if (i < n && b == i - 1 && u > cum) {
-            b = i;
-            cum = cum + th[i];
-        }
-    }
-    return b;
-}
 
 template <int FAM, int K, int MMAX>
 __global__ void __launch_bounds__(kBlock) fitted_kernel(const DevArgs a)
@@ -162,6 +145,8 @@ hhmm_status launch_fitted(const DevArgs &a, hipStream_t st)
 {
     char why[160];
     const bool reg = a.model == HHMM_MODEL_IOHMM_REG;
+    if (a.K > kMaxK && a.K <= kMaxKLarge) /* group per pair (hhmm_lkio.h lkfit_kernel) */
+        return reg ? launch_lkfit<IO_REG>(a, st) : launch_lkfit<IO_MIX>(a, st);
     if (!iohmm_supported(a.K, a.M, reg ? 1 : a.L, why, sizeof(why))) {
         set_error("%s", why);
         return HHMM_ERR_UNSUPPORTED;

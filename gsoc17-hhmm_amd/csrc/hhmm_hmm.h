@@ -70,16 +70,17 @@ __host__ __device__ constexpr bool tayal_on(int sg, int j0)
 {
     return (sg == 1 && (j0 == 1 || j0 == 2)) || (sg == 2 && (j0 == 0 || j0 == 3));
 }
-/* The flattened HHMM's structural transition pattern (hhmm-tayal2009.stan:
- * 36-44; load_params builds A = {{0, r00, r01, 0}, {1, 0, 0, 0},
- * {r10, 0, 0, r11}, {0, 0, 1, 0}}): entry (i, j) can be nonzero.  A term with
- * a structural zero adds exactly nothing (0 x f to a linear sum, a -inf
- * candidate to a max-plus one), so the sign-class paths skip it. */
-__host__ __device__ constexpr bool tayal_nz(int i, int j)
-{
-    return (i == 0 && (j == 1 || j == 2)) || (i == 1 && j == 0) || (i == 2 && (j == 0 || j == 3)) ||
-           (i == 3 && j == 2);
-}
+/* The flattened HHMM's transition matrix (hhmm-tayal2009.stan:36-44), as ONE
+ * table both load_params (which builds A) and tayal_nz (which skips its
+ * structural zeros) read: entry (i, j) is 0 (a structural zero), 1 (one), or
+ * 2 + 2r + c for A_row[r][c]. */
+constexpr int kTayalA[4][4] = {{0, 2, 3, 0}, {1, 0, 0, 0}, {4, 0, 0, 5}, {0, 0, 1, 0}};
+/* Entry (i, j) can be nonzero.  A term with a structural zero adds exactly
+ * nothing (0 x f to a linear sum of finite terms, a -inf candidate to a
+ * max-plus one), so the sign-class paths skip it -- in the linear filters only
+ * where the wave's parameters are probabilities (PairParams::skip_ok), so no
+ * NaN or infinity can meet a skipped zero (the reference's 0 x NaN = NaN). */
+__host__ __device__ constexpr bool tayal_nz(int i, int j) { return kTayalA[i][j] != 0; }
 /* hhmm-tayal2009.stan:51 */
 __device__ __forceinline__ bool tayal_init_pred(int s, int j0)
 {
@@ -145,6 +146,7 @@ struct PairParams {
     double A[K][K];  /* probability (FB) or log (Viterbi) */
     double p[K];
     double mu[K], isig[K], lsig[K], c0[K]; /* gauss: 1/sigma, log sigma, NEG_LOG_SQRT_TWO_PI - log sigma */
+    bool skip_ok;    /* tayal: p_11, A_row (load_params) and phi (fill_table) all in [0, 1] */
 };
 
 template <int K>
@@ -157,6 +159,9 @@ __device__ __forceinline__ double draw2(const double *arr, const DevArgs &a, int
 {
     return arr[d + a.S * ((int64_t)i + (int64_t)I * j)];
 }
+
+/* 0 <= v <= 1 (false for NaN) */
+__device__ __forceinline__ bool in01(double v) { return (v >= 0.0) & (v <= 1.0); }
 
 /* Loads p_1k, A_ij (Tayal: expands p_11 / A_row, hhmm-tayal2009.stan:30-44)
  * and the Gaussian constants.  LOG = true puts log A in params.A.
@@ -172,7 +177,14 @@ __device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevA
         const double p11 = a.p_11[d];
         const double r00 = a.A_row[d + a.S * 0], r10 = a.A_row[d + a.S * 1];
         const double r01 = a.A_row[d + a.S * 2], r11 = a.A_row[d + a.S * 3];
-        double A[4][4] = {{0, r00, r01, 0}, {1, 0, 0, 0}, {r10, 0, 0, r11}, {0, 0, 1, 0}};
+        const double src[6] = {0.0, 1.0, r00, r01, r10, r11}; /* kTayalA's codes */
+        double A[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                A[i][j] = src[kTayalA[i][j]];
+        pp.skip_ok = in01(p11) && in01(r00) && in01(r01) && in01(r10) && in01(r11);
         pp.p[0] = p11;
         pp.p[1] = 0;
         pp.p[2] = 1 - p11;
@@ -183,6 +195,7 @@ __device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevA
             for (int j = 0; j < 4; ++j)
                 pp.A[i][j] = LOG ? dev_cr_log(A[i][j]) : A[i][j];
     } else {
+        pp.skip_ok = false;
         double raw[K][K];
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -222,9 +235,10 @@ __device__ __forceinline__ void load_params(PairParams<MODEL, K> &pp, const DevA
  * row followed by its LDS store costs one HBM round trip per row). */
 constexpr int kRowBatch = 4;
 template <int K, bool LOG>
-__device__ __forceinline__ void fill_table(double2 *slab, const DevArgs &a, int64_t d)
+__device__ __forceinline__ bool fill_table(double2 *slab, const DevArgs &a, int64_t d)
 {
     constexpr int KP = (K + 1) / 2;
+    bool ok = true; /* every phi entry in [0, 1] (PairParams::skip_ok) */
     for (int l0 = 0; l0 < a.L; l0 += kRowBatch) {
         double v[kRowBatch][2 * KP];
 #pragma unroll
@@ -240,6 +254,7 @@ __device__ __forceinline__ void fill_table(double2 *slab, const DevArgs &a, int6
 #pragma unroll
                 for (int kp = 0; kp < KP; ++kp) {
                     double v0 = v[r][2 * kp], v1 = v[r][2 * kp + 1];
+                    ok = ok && in01(v0) && in01(v1);
                     if (LOG) {
                         v0 = dev_cr_log(v0);
                         v1 = dev_cr_log(v1);
@@ -249,6 +264,7 @@ __device__ __forceinline__ void fill_table(double2 *slab, const DevArgs &a, int6
             }
         }
     }
+    return ok;
 }
 
 template <int K>
@@ -386,11 +402,11 @@ __device__ __forceinline__ void fwd_step_raw(const double (&al)[K], double (&out
  * wave of one series under many draws, the T-scan's chunks at C5), else -1
  * (the masks per lane).  Other models: always -1. */
 template <int MODEL, typename F>
-__device__ __forceinline__ void tayal_dispatch(const Obs &o, F &&f)
+__device__ __forceinline__ void tayal_dispatch(const Obs &o, bool skip_ok, F &&f)
 {
     if constexpr (ModelTraits<MODEL>::kTayal) {
         const int s0 = __builtin_amdgcn_readfirstlane(o.aux);
-        if (__ballot(o.aux != s0) == 0) {
+        if (__ballot((o.aux != s0) | !skip_ok) == 0) {
             if (s0 == 1)
                 f(std::integral_constant<int, 1>());
             else if (s0 == 2)
@@ -407,7 +423,7 @@ template <int MODEL, int K>
 __device__ __forceinline__ void fwd_step_to(const double (&al)[K], double (&out)[K], const PairParams<MODEL, K> &pp,
                                             const double (&e)[K], const Obs &o, int &ex, bool rn = true)
 {
-    tayal_dispatch<MODEL>(o, [&](auto sgc) { fwd_step_raw<MODEL, K, decltype(sgc)::value>(al, out, pp, e, o); });
+    tayal_dispatch<MODEL>(o, pp.skip_ok, [&](auto sgc) { fwd_step_raw<MODEL, K, decltype(sgc)::value>(al, out, pp, e, o); });
     if (rn)
         renorm<K>(out, ex);
 }
@@ -476,7 +492,7 @@ template <int MODEL, int K>
 __device__ __forceinline__ void bwd_step(double (&be)[K], const PairParams<MODEL, K> &pp,
                                          const double (&e)[K], const Obs &o, int &ex, bool rn = true)
 {
-    tayal_dispatch<MODEL>(o, [&](auto sgc) { bwd_step_sg<MODEL, K, decltype(sgc)::value>(be, pp, e, o); });
+    tayal_dispatch<MODEL>(o, pp.skip_ok, [&](auto sgc) { bwd_step_sg<MODEL, K, decltype(sgc)::value>(be, pp, e, o); });
     if (rn)
         renorm<K>(be, ex);
 }
@@ -1179,7 +1195,7 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, int64_t gwave)
     ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
     load_params<MODEL, K, false>(ln.pp, a, d);
     if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
+        ln.pp.skip_ok &= fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
     const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
     double al[K], be[K];
 #pragma unroll
@@ -2599,7 +2615,7 @@ __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
     load_params<MODEL, K, false>(pp, a, d);
     const double2 *slab = lds + (size_t)wave * a.L * KP * 64 + lane;
     if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
+        pp.skip_ok &= fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
     const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
 
     double F[K][K], Q[K][K];
@@ -2643,7 +2659,7 @@ __global__ void __launch_bounds__(kBlock) scan_prod_kernel(const DevArgs a)
         lsc += em.m;
         /* a wave whose lanes share the step's sign (one series under many
          * draws: C5) takes the masks as constants (round 4) */
-        tayal_dispatch<MODEL>(o, [&](auto sgc) { prods(sgc, o, em); });
+        tayal_dispatch<MODEL>(o, pp.skip_ok, [&](auto sgc) { prods(sgc, o, em); });
         if (rn) {
             renorm_mat<K>(F, fex);
             if constexpr (BWD)
@@ -3131,7 +3147,7 @@ __global__ void __launch_bounds__(kBlock) fb_scan_kernel(const DevArgs a)
     ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
     load_params<MODEL, K, false>(ln.pp, a, d);
     if constexpr (ModelTraits<MODEL>::kDiscrete)
-        fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
+        ln.pp.skip_ok &= fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
     const SeriesPtrs sp = series_ptrs<MODEL, AUX>(a, n);
     const bool live = ln.t0 < Tpair;
     /* a segment window's chunk 0 enters from the state scan_bound_kernel stored */

@@ -125,6 +125,24 @@ __device__ __forceinline__ double sse_dot(const double (&a)[MMAX], const double 
     return res;
 }
 
+/* Stan Math categorical_rng(theta) with the caller's uniform:
+ * index = cumulative_sum(theta); b = 0; while (c > index[b]) ++b (bounded to
+ * n - 1: a uniform above a rounded-down total lands in the last category). */
+template <int NMAX>
+__device__ __forceinline__ int stan_categorical(const double (&th)[NMAX], int n, double u)
+{
+    int b = 0;
+    double cum = th[0];
+#pragma unroll
+    for (int i = 1; i < NMAX; ++i) {
+        if (i < n && b == i - 1 && u > cum) {
+            b = i;
+            cum = cum + th[i];
+        }
+    }
+    return b;
+}
+
 /* Stan Math softmax(v): theta = exp(v - max v); theta / sequential sum.
  * num: the numerators exp(v - max v) (the FFBS contract's weights). */
 template <int K, int MATH>

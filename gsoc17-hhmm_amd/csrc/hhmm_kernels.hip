@@ -499,6 +499,22 @@ static hhmm_status run_iohmm_filtered(const DevArgs &a, hipStream_t st, hhmm_sta
     return launch_iohmm_log(a, st);
 }
 
+/* The IOHMM sweep (with its log-space fallback) for every output but the
+ * fitted draws, then the fitted draws (hatpi / hatz / hatl / hatx). */
+static hhmm_status run_iohmm_hat(const DevArgs &a, hipStream_t st, hhmm_status (*sweep)(const DevArgs &, hipStream_t))
+{
+    constexpr uint32_t kHat = HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
+    hhmm_status s = HHMM_OK;
+    if (a.outputs & ~kHat) {
+        DevArgs b = a;
+        b.outputs &= ~kHat;
+        s = run_iohmm_filtered(b, st, sweep);
+    }
+    if (s == HHMM_OK && (a.outputs & kHat))
+        s = launch_fitted(a, st);
+    return s;
+}
+
 static hhmm_status launch_model(const hhmm_request *req, const DevArgs &a, const hhmm_result *res, hipStream_t st);
 
 hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t P, void *ws, hipStream_t st,
@@ -537,7 +553,7 @@ static hhmm_status launch_model(const hhmm_request *req, const DevArgs &a, const
             return HHMM_ERR_UNSUPPORTED;
         }
         if (is_iohmm_model(req->model))
-            return run_iohmm_filtered(a, st, run_large_iohmm);
+            return run_iohmm_hat(a, st, run_large_iohmm);
         if (req->model != HHMM_MODEL_HMM_GAUSS && req->model != HHMM_MODEL_HMM_MULTINOM) {
             set_error("K = %d: the device path of model %d supports K <= %d", a.K, req->model, kMaxK);
             return HHMM_ERR_UNSUPPORTED;
@@ -554,15 +570,8 @@ static hhmm_status launch_model(const hhmm_request *req, const DevArgs &a, const
     case HHMM_MODEL_IOHMM_REG:
     case HHMM_MODEL_IOHMM_MIX:
     case HHMM_MODEL_IOHMM_HMIX:
-    case HHMM_MODEL_IOHMM_HMIX_LITE: {
-        constexpr uint32_t kHat = HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
-        hhmm_status s = HHMM_OK;
-        if (a.outputs & ~kHat)
-            s = run_iohmm_filtered(a, st, launch_iohmm);
-        if (s == HHMM_OK && (a.outputs & kHat))
-            s = launch_fitted(a, st);
-        return s;
-    }
+    case HHMM_MODEL_IOHMM_HMIX_LITE:
+        return run_iohmm_hat(a, st, launch_iohmm);
     default:
         set_error("model %d has no device path in this build", req->model);
         return HHMM_ERR_UNSUPPORTED;

@@ -29,7 +29,8 @@
  * bytes, one 16-byte store per lane and block).  FFBS (IO_DET, its own sweep):
  * the transition does not depend on the next state, so each draw z_{t-1} =
  * cat(v_{t-1} .* th_t, u_{t-1}) is formed in the forward sweep from the
- * exchanged weights.  The fitted-output draws stay at K <= 8.
+ * exchanged weights.  The fitted-output draws (hatpi / hatz /
+ * hatl / hatx) run in lkfit_kernel below, the same group layout.
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -465,10 +466,10 @@ static hhmm_status launch_lkio_g(const DevArgs &a, hipStream_t st)
 template <int FAM>
 static hhmm_status launch_lkio(const DevArgs &a, hipStream_t st)
 {
-    constexpr uint32_t kNo = HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
-    if (a.outputs & kNo) {
-        set_error("K = %d: the fitted-output draws of the IOHMM programs run at K <= %d", a.K, kMaxK);
-        return HHMM_ERR_UNSUPPORTED;
+    constexpr uint32_t kHat = HHMM_OUT_HATPI | HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX;
+    if (a.outputs & kHat) { /* launch_all hands the fitted draws to launch_fitted */
+        set_error("internal: lkio_kernel got fitted-output bits");
+        return HHMM_ERR_INVALID_ARGUMENT;
     }
     if (a.M > kLkioMmax || (FAM == IO_MIX && a.L > kIoLmax)) {
         set_error("large-K IOHMM: M = %d (at most %d), L = %d (at most %d)", a.M, kLkioMmax, a.L, kIoLmax);
@@ -477,6 +478,136 @@ static hhmm_status launch_lkio(const DevArgs &a, hipStream_t st)
     return a.K <= 16 ? launch_lkio_g<FAM, 16, 16>(a, st)
            : a.K <= 24 ? launch_lkio_g<FAM, 32, 24>(a, st)
                        : launch_lkio_g<FAM, 32, 32>(a, st);
+}
+
+/* ---- fitted-output draws at large K (fitted_kernel's arithmetic) ----
+ * iohmm-reg.stan:131-148, iohmm-mix.stan:140-160, iohmm-hmix.stan:146-157 with
+ * K free data (iohmm-reg.stan:9).  A group of G lanes per pair, lane j state j:
+ *   v_j = u_t' w_j (sse_dot), exchanged through LDS; every lane forms the max
+ *   by the strict '>' scan, its numerator dev_cr_exp(v_j - max), and after a
+ *   second exchange the SEQUENTIAL sum in state order and th_i = num_i / sum for
+ *   every i -- stan_softmax<K, IO_CR>'s doubles, so hatpi_tk and the draws
+ *   match fitted_kernel and the oracle bit for bit;
+ *   hatz = categorical_rng(th) with the caller's uniform (stan_categorical over
+ *   the first K entries, evaluated by every lane alike);
+ *   reg: hatx = z sigma + mu with mu = u_t' b_hatz (lane hatz's sse_dot) and
+ *   sigma = s_hatz, both read from lane hatz; mix / hmix: hatl =
+ *   categorical_rng(lambda_kl[hatz]), mu / sigma = mu_kl / s_kl[hatz][hatl]. */
+template <int FAM, int G, int KM>
+__global__ void __launch_bounds__(kBlock) lkfit_kernel(const DevArgs a)
+{
+    constexpr int MMAX = kLkioMmax;
+    HIP_DYNAMIC_SHARED(double, lds)
+    const int tid = threadIdx.x;
+    const int g = tid / G;
+    const int j = tid % G;
+    const int K = a.K, M = a.M, L = a.L;
+    const bool on = j < K;
+    const int jj = on ? j : 0;
+    const int64_t p = lk_group<G>(a.P);
+    int64_t n, d;
+    pair_coords(a, p, n, d);
+    const int Tp = pair_len(a, n);
+    const int64_t S = a.S;
+    const uint32_t out = a.outputs;
+    double w[MMAX], b[MMAX];
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) {
+        w[m] = (m < M) ? a.w_km[d + S * ((int64_t)jj + (int64_t)K * m)] : 0.0;
+        b[m] = (FAM == IO_REG && m < M) ? a.b_km[d + S * ((int64_t)jj + (int64_t)K * m)] : 0.0;
+    }
+    const double sj = (FAM == IO_REG) ? a.s_k[d + S * jj] : 0.0;
+    double *xch = lds + (size_t)g * 2 * G;
+    const bool draw = a.hat_rand && (out & (HHMM_OUT_HATZ | HHMM_OUT_HATL | HHMM_OUT_HATX));
+    const int64_t rs = a.P * (int64_t)a.Tmax;
+    const int base = tid - j; /* lane of state 0 in this group (shuffle source) */
+    double vx[KM];
+    const int Tw = wave_max(Tp);
+#pragma unroll 1
+    for (int t = 0; t < Tw; ++t) {
+        if (t >= Tp) /* group-uniform */
+            continue;
+        double u[MMAX];
+#pragma unroll
+        for (int m = 0; m < MMAX; ++m)
+            u[m] = (m < M) ? a.u[n + a.N * ((int64_t)t + (int64_t)a.Tmax * m)] : 0.0;
+        const double v = on ? sse_dot<MMAX>(u, w, M) : 0.0;
+        grp_exchange<G, KM>(xch, 0, j, v, vx);
+        double mx = vx[0];
+#pragma unroll
+        for (int i = 1; i < KM; ++i)
+            if (i < K && vx[i] > mx)
+                mx = vx[i];
+        const double num = on ? dev_cr_exp(v - mx) : 0.0;
+        grp_exchange<G, KM>(xch, 1, j, num, vx);
+        double sum = 0.0;
+#pragma unroll
+        for (int i = 0; i < KM; ++i)
+            if (i < K)
+                sum += vx[i];
+        if ((out & HHMM_OUT_HATPI) && a.hatpi && on)
+            a.hatpi[p + a.P * ((int64_t)t + (int64_t)a.Tout * j)] = num / sum;
+        if (!draw)
+            continue;
+        double th[KM];
+#pragma unroll
+        for (int i = 0; i < KM; ++i)
+            th[i] = vx[i] / sum;
+        const double *rnd = a.hat_rand + a.P * (int64_t)t;
+        const int z = stan_categorical<KM>(th, K, rnd[p]);
+        const double zn = rnd[2 * rs + p];
+        double mu, sg;
+        int l = 0;
+        if constexpr (FAM == IO_REG) {
+            const double mj = sse_dot<MMAX>(u, b, M); /* reg_tk[t] = u_tm[t]' * b_km[hatz_t[t]] on lane hatz */
+            mu = __shfl(mj, base + z);
+            sg = __shfl(sj, base + z);
+        } else {
+            double lam[kIoLmax];
+#pragma unroll
+            for (int q = 0; q < kIoLmax; ++q)
+                lam[q] = (q < L) ? a.lambda_kl[d + S * ((int64_t)z + (int64_t)K * q)] : 0.0;
+            l = stan_categorical<kIoLmax>(lam, L, rnd[rs + p]);
+            const int64_t ix = d + S * ((int64_t)z + (int64_t)K * l);
+            mu = a.mu_kl[ix];
+            sg = a.s_kl[ix];
+        }
+        if (j == 0) {
+            if ((out & HHMM_OUT_HATZ) && a.hatz)
+                a.hatz[p + a.P * (int64_t)t] = z + 1;
+            if (FAM == IO_MIX && (out & HHMM_OUT_HATL) && a.hatl)
+                a.hatl[p + a.P * (int64_t)t] = l + 1;
+            if ((out & HHMM_OUT_HATX) && a.hatx)
+                a.hatx[p + a.P * (int64_t)t] = zn * sg + mu;
+        }
+    }
+}
+
+template <int FAM, int G, int KM>
+static hhmm_status launch_lkfit_g(const DevArgs &a, hipStream_t st)
+{
+    const int gpb = kBlock / G;
+    const size_t lds = (size_t)gpb * 2 * G * sizeof(double);
+    const dim3 grid((unsigned)((a.P + gpb - 1) / gpb));
+    hipLaunchKernelGGL((lkfit_kernel<FAM, G, KM>), grid, dim3(kBlock), lds, st, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("lkfit_kernel launch: %s", hipGetErrorString(e));
+        return HHMM_ERR_HIP;
+    }
+    return HHMM_OK;
+}
+
+template <int FAM>
+static hhmm_status launch_lkfit(const DevArgs &a, hipStream_t st)
+{
+    if (a.M > kLkioMmax || (FAM == IO_MIX && a.L > kIoLmax)) {
+        set_error("large-K fitted draws: M = %d (at most %d), L = %d (at most %d)", a.M, kLkioMmax, a.L, kIoLmax);
+        return HHMM_ERR_UNSUPPORTED;
+    }
+    return a.K <= 16 ? launch_lkfit_g<FAM, 16, 16>(a, st)
+           : a.K <= 24 ? launch_lkfit_g<FAM, 32, 24>(a, st)
+                       : launch_lkfit_g<FAM, 32, 32>(a, st);
 }
 
 } // namespace hhmm

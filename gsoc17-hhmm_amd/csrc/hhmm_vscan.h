@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
             lv[j] = (V)le[j];
         }
         /* the Tayal sign class as a constant where the wave shares it */
-        tayal_dispatch<MODEL>(o, [&](auto sgc) {
+        tayal_dispatch<MODEL>(o, true, [&](auto sgc) {
         constexpr int SG = decltype(sgc)::value;
         bool on[K];
 #pragma unroll
@@ -544,7 +544,7 @@ template <int MODEL, int K, bool NANIN>
 __device__ __forceinline__ void vs_step(double (&dl)[K], const PairParams<MODEL, K> &pp, const double (&le)[K],
                                         const Obs &o, int (&arg)[K])
 {
-    tayal_dispatch<MODEL>(o, [&](auto sgc) { vs_step_sg<MODEL, K, NANIN, decltype(sgc)::value>(dl, pp, le, o, arg); });
+    tayal_dispatch<MODEL>(o, true, [&](auto sgc) { vs_step_sg<MODEL, K, NANIN, decltype(sgc)::value>(dl, pp, le, o, arg); });
 }
 
 /* Chunk 0 from the model's first row: delta_tk[1] has only column K written

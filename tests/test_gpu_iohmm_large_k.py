@@ -3,7 +3,8 @@ oracle -- iohmm-reg, iohmm-mix, iohmm-hmix and iohmm-hmix-lite with Stan's free
 K (iohmm-reg/stan/iohmm-reg.stan:9).  One group of 16 or 32 lanes owns a pair,
 lane j state j; the softmax over states is each lane's sequential max / sum
 over the exchanged vector, so A_t, log A_t, the Viterbi paths, logp_zstar and
-pair_status are bit-exact, the posteriors within tests/tolerances.py."""
+pair_status are bit-exact, the posteriors within tests/tolerances.py; the
+fitted-output draws (lkfit_kernel, same layout) bit-exact given hat_rand."""
 import numpy as np
 import pytest
 
@@ -94,10 +95,26 @@ def test_iohmm_large_K_ffbs(engine, oracle, model, K):
     compare_all(got, ref, pars + ["pair_status"])
 
 
-def test_iohmm_large_K_fitted_draws_unsupported(engine):
+@pytest.mark.parametrize("K", [12, 23, 32])
+@pytest.mark.parametrize("model", ["iohmm-reg", "iohmm-mix", "iohmm-hmix"])
+def test_iohmm_large_K_fitted_draws(engine, oracle, model, K):
+    """SURVEY §8 F4 at large K (iohmm-reg.stan:131-148, iohmm-hmix.stan:145-158; K is data,
+    iohmm-reg.stan:9): hatpi_tk / hatz_t / hatl_t / hatx_t bit-exact given hat_rand,
+    ragged series, alone and together with the recursion outputs (one call, two kernels)."""
     import hhmm_amd
-    from hhmm_amd.api import HHMMError
-    data, draws = synth.iohmm_reg(N=1, S=2, T=20, K=12, M=4)
-    hr = np.random.default_rng(1).random((2, 20, 3))
-    with pytest.raises(HHMMError, match="fitted-output"):
-        hhmm_amd.gqs("iohmm-reg", data, draws, pars=["loglik", "hatz_t"], lib=engine, hat_rand=hr)
+    data, draws = synth.GENERATORS[model](N=3, S=24, T=41, K=K, M=4)
+    data["T"] = np.array([41, 17, 1], dtype=np.int32)
+    P = 72
+    hr = synth.hat_rand(P, 41, seed=K)
+    hat = synth.HAT_PARS[model]
+    Tn = np.repeat(data["T"], 24)
+    for pars in (hat, pars_of(model) + hat):
+        got = hhmm_amd.gqs(model, data, draws, pars=pars, lib=engine, hat_rand=hr, return_status=True)
+        ref = oracle.gqs(model, data, draws, pars=pars, hat_rand=hr, return_status=True, nthreads=8)
+        for name in hat:
+            for p in range(P):
+                g, r = got[name][p, :Tn[p]], ref[name][p, :Tn[p]]
+                assert np.array_equal(g.view(np.int64) if g.dtype == np.float64 else g,
+                                      r.view(np.int64) if r.dtype == np.float64 else r), (model, K, name, p)
+        rest = [n for n in pars if n not in hat]
+        compare_all(got, ref, rest + ["pair_status"])

@@ -99,17 +99,65 @@ def test_table8_neighbourhood_lite_batch(engine, oracle, S):
             compare(name, np.asarray(got[name])[ss + S * n], ref[name])
 
 
-FULL = ["loglik", "alpha_tk", "beta_tk", "gamma_tk", "zstar_t", "logp_zstar", "unalpha_tk", "unbeta_tk"]
+# LIN: the probability-space outputs (the scaled linear filters, the T-scan); with unalpha_tk /
+# unbeta_tk requested the engine runs the log-space recursions instead (FULL).
+LIN = ["loglik", "alpha_tk", "beta_tk", "gamma_tk", "zstar_t", "logp_zstar"]
+FULL = LIN + ["unalpha_tk", "unbeta_tk"]
 
 
-def test_table8_point_full_model(engine, oracle):
+@pytest.mark.parametrize("pars", [LIN, FULL], ids=["linear", "log-space"])
+def test_table8_point_full_model(engine, oracle, pars):
     """hhmm-tayal2009.stan at the same point: backward (Q6 previous-state mask), gamma, Viterbi."""
     import hhmm_amd
     _, data = _data(2, True, seed=7)
     data = {k: v for k, v in data.items() if not k.endswith("_oos")}
     draws = _draws(16)
-    got = hhmm_amd.gqs("hhmm-tayal2009", data, draws, pars=FULL, lib=engine, return_status=True)
+    got = hhmm_amd.gqs("hhmm-tayal2009", data, draws, pars=pars, lib=engine, return_status=True)
     ref = oracle.gqs("hhmm-tayal2009", data, draws, pars=FULL, return_status=True)
-    compare_all(got, ref, [n for n in FULL if n != "gamma_tk"] + ["pair_status"])
+    compare_all(got, ref, [n for n in pars if n != "gamma_tk"] + ["pair_status"])
+    from test_gpu_configs import compare_tayal_gamma
+    compare_tayal_gamma(got, ref, max_forgiven=0)
+
+
+# ---- degenerate draws on the sign-class paths (ADVICE r4) ------------------------------------
+# The Tayal kernels skip the flattened HHMM's structural transition zeros when a wave's lanes
+# share a step's sign (hhmm_hmm.h tayal_nz / tayal_dispatch).  0 x f adds nothing to a sum of
+# finite terms, but the reference computes in log space, where a NaN on a skipped path still
+# reaches every accumulator (NaN + -inf = NaN, hhmm-tayal2009.stan:60-71).  The skip is taken
+# only where the wave's p_11, A_row and phi_k are all probabilities; these draws are not, and
+# must give the oracle's values and NaN placement exactly.
+DEGENERATE = ["p11_nan", "phi_nan", "arow_above_one", "arow_zero", "phi_inf"]
+
+
+def _degenerate(kind, S=64):
+    d = _draws(S)
+    d = {k: v.copy() for k, v in d.items()}
+    s = 5
+    if kind == "p11_nan":
+        d["p_11"][s] = np.nan
+    elif kind == "phi_nan":
+        d["phi_k"][s, 1, 4] = np.nan
+    elif kind == "arow_above_one":
+        d["A_row"][s, 1, 0] = 1.5
+    elif kind == "arow_zero":  # a valid draw with an extra zero: the skip stays on
+        d["A_row"][s, 0] = (0.0, 1.0)
+    elif kind == "phi_inf":
+        d["phi_k"][s, 2, 3] = np.inf
+    return d
+
+
+@pytest.mark.parametrize("kind", DEGENERATE)
+@pytest.mark.parametrize("T,flags", [(300, 0), (40_000, 0), (40_000, 2)], ids=["lanes", "scan", "scan-off"])
+def test_degenerate_draw_sign_class_paths(engine, oracle, kind, T, flags):
+    """One series under 64 draws (C5's wave shape: every lane shares each step's sign)."""
+    import hhmm_amd
+    g = synth.rng(synth.SEED, 9)
+    f = _legs(g, T, True)
+    data = {"K": 4, "L": 9, "x": np.where(f <= 9, f, f - 9)[None], "sign": np.where(f <= 9, 1, 2)[None]}
+    draws = _degenerate(kind)
+    got = hhmm_amd.gqs("hhmm-tayal2009", data, draws, pars=LIN, lib=engine, return_status=True, flags=flags)
+    ref = oracle.gqs("hhmm-tayal2009", data, draws, pars=FULL, return_status=True, nthreads=8)
+    names = ["loglik", "alpha_tk", "beta_tk", "zstar_t", "logp_zstar", "pair_status"]
+    compare_all(got, ref, names)
     from test_gpu_configs import compare_tayal_gamma
     compare_tayal_gamma(got, ref, max_forgiven=0)
