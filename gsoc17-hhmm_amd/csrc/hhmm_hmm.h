@@ -2853,12 +2853,15 @@ __device__ __forceinline__ void rowmat_shfl_up(const RowMat<K> &S, RowMat<K> &D,
     D.ls = __shfl_up(S.ls, d);
 }
 
-/* Inclusive prefix product over the wave's lanes: P_l = M_0 M_1 ... M_l. */
+/* Inclusive prefix product over the wave's lanes: P_l = M_0 M_1 ... M_l, for
+ * the first nb lanes (wave-uniform; ceil(log2 nb) levels). */
 template <int K>
-__device__ __forceinline__ void rowmat_prefix(RowMat<K> &P, int lane)
+__device__ __forceinline__ void rowmat_prefix(RowMat<K> &P, int lane, int nb = 64)
 {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
+        if (d >= nb)
+            break;
         RowMat<K> X, R;
         rowmat_shfl_up<K>(P, X, d);
         rowmat_mul<K>(X, P, R);
@@ -2875,7 +2878,7 @@ template <int K>
 __device__ __forceinline__ void bound_block(RowMat<K> &P, int lane, int nb, double (&v)[K], double &vsc,
                                             double (&out)[K], double &osc)
 {
-    rowmat_prefix<K>(P, lane);
+    rowmat_prefix<K>(P, lane, nb);
     int ex = 0;
     vec_rowmat<K>(v, P.m, P.rs, out, ex);
     osc = vsc + (P.ls + kLn2 * ex);
@@ -2896,32 +2899,44 @@ __device__ __forceinline__ void bound_block(RowMat<K> &P, int lane, int nb, doub
 #define HHMM_BOUND_WAVES 4 /* build knob: waves per (pair, direction) of the boundary scan */
 #endif
 constexpr int kBoundWaves = HHMM_BOUND_WAVES;
+/* A walk of at most one block (n <= 64 items: C1's 16 chunks per pair) runs on
+ * wave 0 alone, without the range totals: one prefix of ceil(log2 n) levels
+ * instead of two six-level prefixes and a workgroup barrier on every wave
+ * (C1 0.107 -> 0.121 ms with the four-wave scan).  Build knob. */
+#ifndef HHMM_BOUND_SHORT
+#define HHMM_BOUND_SHORT 1
+#endif
 
 template <int K, bool BW>
 __device__ __forceinline__ void bound_walk(const DevArgs &a, int64_t p, int ncp, int c0, int n, double (&v)[K],
                                            double &vsc, RowMat<K> *tot)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int lo = (int)((int64_t)n * wave / kBoundWaves), hi = (int)((int64_t)n * (wave + 1) / kBoundWaves);
+    const bool one = HHMM_BOUND_SHORT && n <= 64; /* workgroup-uniform */
+    if (one && wave > 0)
+        return;
+    const int nw = one ? 1 : kBoundWaves;
+    const int lo = (int)((int64_t)n * wave / nw), hi = (int)((int64_t)n * (wave + 1) / nw);
     const double *base = BW ? a.sc_qb : a.sc_mf;
     auto chunk = [&](int i) { return BW ? ncp - 1 - i : c0 + i; };
     auto fetch = [&](int ib, RawMat<K> &r) { /* item ib + lane, clamped into the range */
         rawmat_fetch<K, BW>(base, a, chunk(max(min(ib + lane, hi - 1), 0)), p, BW ? 2 : 0, r);
     };
+    RawMat<K> nx;
+    if (!one) {
     /* ---- 1. the range's total ---- */
     RowMat<K> T;
     {
         RawMat<K> id;
         rowmat_from<K>(id, true, T);
     }
-    RawMat<K> nx;
     if (lo < hi)
         fetch(lo, nx);
     for (int ib = lo; ib < hi; ib += 64) {
         RowMat<K> P;
         rowmat_from<K>(nx, ib + lane >= hi, P);
         fetch(ib + 64, nx);
-        rowmat_prefix<K>(P, lane);
+        rowmat_prefix<K>(P, lane, min(hi - ib, 64));
         RowMat<K> B, R;
         const int last = min(hi - ib, 64) - 1;
 #pragma unroll
@@ -2948,6 +2963,7 @@ __device__ __forceinline__ void bound_walk(const DevArgs &a, int64_t p, int ncp,
 #pragma unroll
         for (int k = 0; k < K; ++k)
             v[k] = o[k];
+    }
     }
     /* ---- 3. the walk, every boundary vector stored by its own lane ---- */
     if (lo < hi)
@@ -3018,9 +3034,10 @@ __global__ void __launch_bounds__(64 * kBoundWaves) scan_bound_kernel(const DevA
             a.sc_sl[p + a.P * (int64_t)c0] = sc;
         }
         bound_walk<K, false>(a, p, ncp, c0, max(ncp - c0, 0), f, sc, tot);
-        /* the last wave leaves with the filter after chunk ncp-1 */
-        if ((threadIdx.x == 64 * (kBoundWaves - 1)) && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik &&
-            !a.seg_nolast)
+        /* the last wave leaves with the filter after chunk ncp-1 (wave 0 alone
+         * on a short walk; the others returned from it) */
+        const int nlast = (HHMM_BOUND_SHORT && ncp - c0 <= 64) ? 0 : kBoundWaves - 1;
+        if ((threadIdx.x == 64 * nlast) && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
             a.loglik[p] = log(vsum<K>(f)) + sc;
         return;
     }

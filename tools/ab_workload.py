@@ -32,7 +32,7 @@ import hhmm_amd  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("variants", nargs="+")
-    ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5", "n1", "n2"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c3", "c4", "c5", "n1", "n2"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pars", default=None)
