@@ -956,9 +956,10 @@ static hhmm_status segment_check(const hhmm_request *req, const hhmm_segment *se
     const int m = req->model;
     if (!(m == HHMM_MODEL_HMM_GAUSS || m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ||
           m == HHMM_MODEL_TAYAL) ||
-        req->data.K > kMaxKLarge || (req->data.K > kMaxK && m != HHMM_MODEL_HMM_MULTINOM)) {
+        req->data.K > kMaxKLarge ||
+        (req->data.K > kMaxK && m != HHMM_MODEL_HMM_MULTINOM && m != HHMM_MODEL_HMM_GAUSS)) {
         set_error("segment windows: the HMM family at K <= %d (hmm, hmm-multinom, semisup, tayal), "
-                  "hmm-multinom at K <= %d", kMaxK, kMaxKLarge);
+                  "hmm and hmm-multinom at K <= %d", kMaxK, kMaxKLarge);
         return HHMM_ERR_UNSUPPORTED;
     }
     const uint32_t ok = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;

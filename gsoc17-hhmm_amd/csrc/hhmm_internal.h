@@ -80,7 +80,7 @@ struct DevArgs {
     double *sc_st;      /* [nc][K][P]    forward state entering each chunk */
     double *sc_sl;      /* [nc][P]       its log scale */
     double *sc_be;      /* [nc][K][P]    beta at each chunk's last step */
-    double *sc_bl;      /* [nc][P]       its log scale */
+    double *sc_bl;      /* [nc][P]       its log scale; large K: [P][nc] the chunk products' Gaussian log scales */
     /* T-parallel exact Viterbi (hhmm_vscan.h); vs_nc = 0: sequential decoders */
     int32_t vs_nc;      /* V-chunks of kVsChunk steps per pair (of the Viterbi's T_max) */
     double *vs_m;       /* [nc][K*K][P] chunk max-plus products (approximate, then on the grid) */

@@ -105,7 +105,7 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
         return sp;
     const int log2cl = (int)((flags >> 8) & 0xffu);
     if (K > kMaxK) {
-        /* large K (hhmm_lkscan.h): hmm-multinom; chunks a multiple of the
+        /* large K (hhmm_lkscan.h): hmm-multinom and hmm; chunks a multiple of the
          * 32-step observation blocks; automatic when the batch is under 4096
          * pairs (2048 waves of two groups: two per SIMD) and long, with about
          * 128k (pair, chunk) groups for the chunks' sweeps.  At N2 (250 pairs x
@@ -114,7 +114,7 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
          * (1024: 53.6) for 46 GB of gamma + 5.75 GB of checkpoints: a 128-byte
          * line of a gamma row is written by several waves, whose stores meet in
          * L2 less often the longer the chunks (profiles/r04r_n2_chunks.txt) */
-        if (model != HHMM_MODEL_HMM_MULTINOM || K > kMaxKLarge)
+        if ((model != HHMM_MODEL_HMM_MULTINOM && model != HHMM_MODEL_HMM_GAUSS) || K > kMaxKLarge)
             return sp;
         if (!(flags & HHMM_FLAG_SCAN_FORCE) && !(P < 4096 && Tmax >= 8192))
             return sp;
@@ -233,6 +233,7 @@ static WsLayout ws_layout(int model, int K, int L, int Tmax, int Toos, int64_t P
             w.st = take(Q * K * d);
             w.sl = take(Q * d);
             w.be = take(Q * K * d);
+            w.bl = take(Q * d); /* hmm.stan: each chunk's Gaussian log scale */
             if (needs_ckpt(model, outputs))
                 w.ckpt = take((size_t)((w.sp.cl + 7) / 8) * K * Q * d);
         } else if (lkm_plan(model, K, N, pairing, outputs, flags, 0) && needs_ckpt(model, outputs)) {

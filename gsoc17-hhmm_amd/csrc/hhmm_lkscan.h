@@ -1,6 +1,8 @@
 /*
  * hhmm_lkscan.h -- the parallel scan over T at large K (8 < K <= 32; SURVEY.md
- * §8 A16 + N1, the verdict's N2): hmm-multinom with few pairs and long series,
+ * §8 A16 + N1, the verdict's N2): hmm-multinom -- and hmm.stan's Gaussian
+ * emissions, whose per-step shift m_t = max_j lpdf_j travels as each chunk's
+ * log scale (sc_bl) -- with few pairs and long series,
  * e.g. a flattened HHMM with 23 states (log.md:657-658) over a tick series of
  * 10^6 zig-zags (tayal2009/main.Rmd:310-346).  The sequential state-parallel
  * kernels (hhmm_large.h) give one 32-lane group per pair: 250 pairs are 125
@@ -37,6 +39,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "hhmm_large.h"
 
 namespace hhmm {
@@ -55,7 +59,7 @@ __device__ __forceinline__ lks_d4 lks_mfma(double a, double b, lks_d4 c)
  * k-steps of 4 states (K <= 16: 1 / 4; K <= 24: 2 / 6; K <= 32: 2 / 8). */
 constexpr int kLksTiles = 2;
 
-template <int RT, int KSM>
+template <int RT, int KSM, bool GS>
 __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
 {
     constexpr int TPW = kLksTiles;
@@ -75,11 +79,26 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
     const int Tp = pair_len(a, n);
     const int64_t S = a.S;
 
-    /* the pair's emission table phi[l][j] (rows j >= K zero), one per wave */
+    /* multinomial: the pair's emission table phi[l][j] (rows j >= K zero), one
+     * per wave; Gaussian (hmm.stan): mu, 1/sigma and NEG_LOG_SQRT_TWO_PI -
+     * log(sigma) of the lane's rows j = 4kk + (lane >> 4) */
     double *tab = lds + (size_t)wv * a.L * KR;
-    for (int idx = lane; idx < a.L * KR; idx += 64) {
-        const int l = idx / KR, j = idx - l * KR;
-        tab[idx] = j < K ? a.phi_k[d + S * ((int64_t)j + (int64_t)K * l)] : 0.0;
+    double gmu[GS ? KSM : 1], gis[GS ? KSM : 1], gc0[GS ? KSM : 1];
+    if constexpr (GS) {
+#pragma unroll
+        for (int kk = 0; kk < KSM; ++kk) {
+            const int j = 4 * kk + (lane >> 4);
+            const int jc = j < K ? j : 0;
+            const double sg = a.sigma_k[d + S * jc];
+            gmu[kk] = a.mu_k[d + S * jc];
+            gis[kk] = 1.0 / sg;
+            gc0[kk] = HHMM_NEG_LOG_SQRT_TWO_PI - dev_cr_log(sg); /* lk_setup's constant */
+        }
+    } else {
+        for (int idx = lane; idx < a.L * KR; idx += 64) {
+            const int l = idx / KR, j = idx - l * KR;
+            tab[idx] = j < K ? a.phi_k[d + S * ((int64_t)j + (int64_t)K * l)] : 0.0;
+        }
     }
     /* A operand: Aop[rt][kk] = A^T[j][i] = A(i, j), i = 4kk + (lane >> 4), j = 16rt + (lane & 15) */
     double aop[RT][KSM];
@@ -93,8 +112,10 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
     __syncthreads();
 
     /* this lane's column in each tile: (chunk c, initial state i); B operand
-     * Q[u][kk] = row 4kk + (lane >> 4) of the column */
+     * Q[u][kk] = row 4kk + (lane >> 4) of the column; gls: the chunk's Gaussian
+     * log scale (the sum of the steps' emission shifts) */
     double q[TPW][KSM];
+    double gls[TPW];
     int ex[TPW], t0[TPW], t1[TPW];
     bool valid[TPW];
 #pragma unroll
@@ -105,6 +126,7 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
         t0[u] = c * cl;
         t1[u] = valid[u] ? min(t0[u] + cl, Tp) : t0[u];
         ex[u] = 0;
+        gls[u] = 0.0;
 #pragma unroll
         for (int kk = 0; kk < KSM; ++kk)
             q[u][kk] = (valid[u] && 4 * kk + (lane >> 4) == i) ? 1.0 : 0.0;
@@ -118,11 +140,15 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
 
     /* observations a block of kB steps ahead (clamped, unconditional) */
     constexpr int kB = 8;
-    auto ldx = [&](int u, int s) -> int {
+    typedef typename std::conditional<GS, double, int>::type ObsT;
+    auto ldx = [&](int u, int s) -> ObsT {
         const int t = min(max(t0[u] + s, 0), a.Tmax - 1);
-        return a.x[n + a.N * (int64_t)t];
+        if constexpr (GS)
+            return a.xr[n + a.N * (int64_t)t];
+        else
+            return a.x[n + a.N * (int64_t)t];
     };
-    int xb[TPW][kB], xn[TPW][kB];
+    ObsT xb[TPW][kB], xn[TPW][kB];
 #pragma unroll
     for (int u = 0; u < TPW; ++u)
 #pragma unroll
@@ -164,14 +190,36 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
                  * segment window that starts inside the series: there every
                  * step is a transition */
                 const bool on = (t >= 1 || a.seg_nofirst) && t < t1[u];
-                const int xc = min(max(xb[u][v], 1), a.L);
-                const double *row = tab + (xc - 1) * KR + (lane >> 4);
+                double em[KSM];
+                if constexpr (GS) {
+                    /* e_t(j) = exp(lpdf_j - m_t), m_t = max_j lpdf_j (emit_prob's
+                     * shift; the column's rows sit on lanes l, l ^ 16, l ^ 32, l ^ 48) */
+                    double lp[KSM];
+                    double m = dev_ninf();
+#pragma unroll
+                    for (int kk = 0; kk < KSM; ++kk) {
+                        const double z = (xb[u][v] - gmu[kk]) * gis[kk];
+                        lp[kk] = (4 * kk + (lane >> 4) < K) ? gc0[kk] + (-0.5 * (z * z)) : dev_ninf();
+                        m = fmax(m, lp[kk]);
+                    }
+                    m = fmax(m, __shfl_xor(m, 16));
+                    m = fmax(m, __shfl_xor(m, 32));
+#pragma unroll
+                    for (int kk = 0; kk < KSM; ++kk)
+                        em[kk] = exp(lp[kk] - m);
+                    gls[u] += on ? m : 0.0;
+                } else {
+                    const int xc = min(max(xb[u][v], 1), a.L);
+                    const double *row = tab + (xc - 1) * KR + (lane >> 4);
+#pragma unroll
+                    for (int kk = 0; kk < KSM; ++kk)
+                        em[kk] = row[4 * kk];
+                }
                 double nv[KSM];
                 double mx = 0.0;
 #pragma unroll
                 for (int kk = 0; kk < KSM; ++kk) {
-                    const double e = row[4 * kk];
-                    nv[kk] = acc[u][kk >> 2][kk & 3] * e;
+                    nv[kk] = acc[u][kk >> 2][kk & 3] * em[kk];
                     mx = fmax(mx, nv[kk]);
                 }
                 mx = fmax(mx, __shfl_xor(mx, 16));
@@ -210,6 +258,8 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
         mx = fmax(mx, __shfl_xor(mx, 32));
         if ((lane >> 4) == 0)
             a.sc_mx[((int64_t)p * nc + c) * K + i] = mx > 0.0 ? (double)ex[u] : dev_ninf();
+        if (GS && (lane >> 4) == 0 && i == 0) /* every column of the chunk has the same shifts */
+            a.sc_bl[(int64_t)p * nc + c] = gls[u];
     }
 }
 
@@ -227,7 +277,23 @@ __device__ __forceinline__ void lks_stage_load(const DevArgs &a, int64_t p, int 
     }
 }
 
-template <int KM>
+/* hmm.stan:30 (Q2): log(p_1k) + SUM_k normal_lpdf(x[1] | mu_k, sigma_k), the
+ * sum in state order (fwd_init's), evaluated by every lane */
+__device__ __forceinline__ double lks_gauss_init(const DevArgs &a, int64_t n, int64_t d)
+{
+    const double x1 = a.xr[n];
+    double s = 0.0;
+    for (int k = 0; k < a.K; ++k) {
+        const double sg = a.sigma_k[d + a.S * k];
+        const double z = (x1 - a.mu_k[d + a.S * k]) * (1.0 / sg);
+        s += HHMM_NEG_LOG_SQRT_TWO_PI;
+        s -= dev_cr_log(sg);
+        s += -0.5 * (z * z);
+    }
+    return s;
+}
+
+template <int KM, bool GS>
 __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
 {
     __shared__ double mt[KM * KM];
@@ -270,8 +336,13 @@ __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
      * state (seg_enter: K values up to scale, then their log scale) ---- */
     double f, lsc = 0.0;
     if (!a.seg_nofirst) {
-        const int x0 = min(max(a.x[n], 1), a.L);
-        f = on ? a.p_1k[d + S * jj] * a.phi_k[d + S * ((int64_t)jj + (int64_t)K * (x0 - 1))] : 0.0;
+        if constexpr (GS) { /* alpha_1 = p_1k, the summed emission into the log scale (Q2) */
+            f = on ? a.p_1k[d + S * jj] : 0.0;
+            lsc = lks_gauss_init(a, n, d);
+        } else {
+            const int x0 = min(max(a.x[n], 1), a.L);
+            f = on ? a.p_1k[d + S * jj] * a.phi_k[d + S * ((int64_t)jj + (int64_t)K * (x0 - 1))] : 0.0;
+        }
     } else {
         f = on ? a.seg_enter[p + a.P * (int64_t)jj] : 0.0;
         lsc = a.seg_enter[p + a.P * (int64_t)K];
@@ -307,6 +378,8 @@ __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
         const int e2 = __builtin_amdgcn_frexp_exp(wmax_d(nf));
         f = ldexp(nf, -e2);
         lsc += kLn2 * ((double)(em == kDead ? 0 : em) + e2);
+        if constexpr (GS)
+            lsc += a.sc_bl[base(c)]; /* the chunk's Gaussian emission shifts */
     }
     const double sf = wsum_d(on ? f : 0.0);
     if (j == 0 && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik && !a.seg_nolast)
@@ -357,7 +430,7 @@ __global__ void __launch_bounds__(64) lks_bound_kernel(const DevArgs a)
  * largest entry.  The first window's rows all hold the state leaving it
  * (p_1k .* phi[., x_1] times S): the layout of the K <= 8 summary
  * (seg_summary_kernel), so hhmm_amd.segment.boundaries chains both. ---- */
-template <int KM>
+template <int KM, bool GS>
 __global__ void __launch_bounds__(64) lks_seg_summary_kernel(const DevArgs a)
 {
     __shared__ double Sm[KM * KM];
@@ -444,10 +517,22 @@ __global__ void __launch_bounds__(64) lks_seg_summary_kernel(const DevArgs a)
     for (int idx = l; idx < KK; idx += 64) /* SQ = the product (beta entering = SQ beta leaving) */
         out[p + a.P * (int64_t)(KK + idx)] = Sm[idx];
     int fex = E;
+    /* the window's Gaussian log scale: its chunks' emission shifts (hmm.stan) */
+    double gl = 0.0;
+    if constexpr (GS)
+        for (int c = 0; c < ncp; ++c)
+            gl += a.sc_bl[base(c)];
     if (!a.seg_nofirst) {
-        /* the first window: every row holds p_1k .* phi[., x_1] (hmm-multinom.stan:31) times S */
-        const int x0 = min(max(a.x[n], 1), a.L);
-        const double f0 = (l < K) ? a.p_1k[d + S * l] * a.phi_k[d + S * ((int64_t)l + (int64_t)K * (x0 - 1))] : 0.0;
+        /* the first window: every row holds p_1k .* phi[., x_1] (hmm-multinom.stan:31) times S;
+         * hmm.stan: p_1k, the summed emission of x_1 into the log scale (Q2) */
+        double f0;
+        if constexpr (GS) {
+            f0 = (l < K) ? a.p_1k[d + S * l] : 0.0;
+            gl += lks_gauss_init(a, n, d);
+        } else {
+            const int x0 = min(max(a.x[n], 1), a.L);
+            f0 = (l < K) ? a.p_1k[d + S * l] * a.phi_k[d + S * ((int64_t)l + (int64_t)K * (x0 - 1))] : 0.0;
+        }
         const int fe = __builtin_amdgcn_frexp_exp(wmax_d(f0));
         if (l < K)
             fk[l] = ldexp(f0, -fe);
@@ -468,7 +553,7 @@ __global__ void __launch_bounds__(64) lks_seg_summary_kernel(const DevArgs a)
     }
     if (l == 0) {
         out[p + a.P * (int64_t)(2 * KK + 0)] = (double)fex;
-        out[p + a.P * (int64_t)(2 * KK + 1)] = 0.0; /* no Gaussian log scale */
+        out[p + a.P * (int64_t)(2 * KK + 1)] = gl; /* the Gaussian log scale (0: hmm-multinom) */
         out[p + a.P * (int64_t)(2 * KK + 2)] = (double)E;
     }
 }
@@ -782,10 +867,12 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
     const uint32_t fb = HHMM_OUT_LOGLIK | HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA;
     const uint32_t vit = HHMM_OUT_ZSTAR | HHMM_OUT_LOGP_ZSTAR;
     const uint32_t ffbs = HHMM_OUT_FFBS;
-    if (a.scan_cl > 0 && (!discrete || a.L * 16 * ((KM + 15) / 16) * 4 * sizeof(double) > 64 * 1024)) {
+    if (a.scan_cl > 0 && discrete && a.L * 16 * ((KM + 15) / 16) * 4 * sizeof(double) > 64 * 1024) {
         set_error("K = %d: the parallel scan over T runs hmm-multinom with L <= %d", a.K, 64 * 1024 / (4 * 8 * 16 * ((KM + 15) / 16)));
         return HHMM_ERR_UNSUPPORTED;
     }
+    constexpr bool GS = LkTraits<MODEL>::kGauss;
+    const size_t plds = discrete ? (size_t)4 * a.L * 16 * ((KM + 15) / 16) * sizeof(double) : 0;
     const uint32_t logs = HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA;
     if (out & ~(fb | vit | ffbs | logs)) {
         set_error("K = %d > %d: the large-K path evaluates loglik, unalpha, alpha, unbeta, beta, ungamma, gamma, "
@@ -804,19 +891,19 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         /* one window of a series split over ranks along T (hhmm_segment):
          * phase 1 + the window's summary, or phases 2 + 3 from the caller's
          * entering state / leaving beta */
-        if (MODEL != HHMM_MODEL_HMM_MULTINOM || a.scan_cl <= 0) {
-            set_error("segment windows at K = %d > %d: hmm-multinom on the T-scan", a.K, kMaxK);
+        if (a.scan_cl <= 0) {
+            set_error("segment windows at K = %d > %d: hmm / hmm-multinom on the T-scan", a.K, kMaxK);
             return HHMM_ERR_UNSUPPORTED;
         }
         constexpr int RT = (KM + 15) / 16, KSM = KM / 4;
         if (a.seg_phase == 1) {
             const int ntile = (a.scan_nc * a.K + 15) / 16;
             const int64_t waves = a.P * (int64_t)((ntile + kLksTiles - 1) / kLksTiles);
-            const size_t plds = (size_t)4 * a.L * 16 * RT * sizeof(double);
-            hipLaunchKernelGGL((lks_prod_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
-            hipLaunchKernelGGL((lks_seg_summary_kernel<KM>), dim3((unsigned)a.P), dim3(64), 0, st, a);
+            hipLaunchKernelGGL((lks_prod_kernel<RT, KSM, GS>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st,
+                               a);
+            hipLaunchKernelGGL((lks_seg_summary_kernel<KM, GS>), dim3((unsigned)a.P), dim3(64), 0, st, a);
         } else {
-            hipLaunchKernelGGL((lks_bound_kernel<KM>), dim3((unsigned)a.P), dim3(64), 0, st, a);
+            hipLaunchKernelGGL((lks_bound_kernel<KM, GS>), dim3((unsigned)a.P), dim3(64), 0, st, a);
             const int64_t nq = a.P * (int64_t)a.scan_nc;
             if (out & (fb & ~HHMM_OUT_LOGLIK))
                 hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)),
@@ -864,9 +951,8 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         constexpr int RT = (KM + 15) / 16, KSM = KM / 4;
         const int ntile = (a.scan_nc * a.K + 15) / 16;
         const int64_t waves = a.P * (int64_t)((ntile + kLksTiles - 1) / kLksTiles);
-        const size_t plds = (size_t)4 * a.L * 16 * RT * sizeof(double);
-        hipLaunchKernelGGL((lks_prod_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
-        hipLaunchKernelGGL((lks_bound_kernel<KM>), dim3((unsigned)a.P), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((lks_prod_kernel<RT, KSM, GS>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
+        hipLaunchKernelGGL((lks_bound_kernel<KM, GS>), dim3((unsigned)a.P), dim3(64), 0, st, a);
         const int64_t nq = a.P * (int64_t)a.scan_nc;
         if (out & (fb & ~HHMM_OUT_LOGLIK)) /* the chunks' sweeps: posteriors (the loglik is phase 2's) */
             hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)), dim3(threads),
@@ -876,7 +962,6 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         /* many series under each draw: the forward-backward on the matrix cores */
         constexpr int RT = (KM + 15) / 16, KSM = KM / 4;
         const int64_t waves = a.S * ((a.N + 15) / 16);
-        const size_t plds = (size_t)4 * a.L * 16 * RT * sizeof(double);
         hipLaunchKernelGGL((lkm_fb_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
         e = hipGetLastError();
     } else if ((out & fb) && e == hipSuccess) {

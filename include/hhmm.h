@@ -343,10 +343,10 @@ hhmm_status hhmm_run_device(const hhmm_request *req, hhmm_result *res,
  *       the window's steps.
  * The caller all-gathers the ranks' summaries (K x K per pair: 2K^2 + 3
  * doubles) and chains them (hhmm_amd.segment.boundaries; dist.gqs_tsplit).
- * HMM family at K <= 8 (hmm, hmm-multinom, semisup, tayal) and hmm-multinom
- * at 8 < K <= 32 (the flattened-HHMM state spaces: SF = SQ, its chunk products
- * on the matrix cores); the Viterbi and FFBS stay sequential per pair (no
- * segment form). */
+ * HMM family at K <= 8 (hmm, hmm-multinom, semisup, tayal) and hmm /
+ * hmm-multinom at 8 < K <= 32 (the flattened-HHMM state spaces: SF = SQ, its
+ * chunk products on the matrix cores); the Viterbi and FFBS stay sequential
+ * per pair (no segment form). */
 typedef struct hhmm_segment {
     int32_t first;           /* the window starts at the series' first step */
     int32_t last;            /* the window ends at the series' last step */

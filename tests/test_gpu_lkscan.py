@@ -92,3 +92,30 @@ def test_scan_transient_states(engine, oracle):
     phi /= phi.sum(axis=2, keepdims=True)
     draws["phi_k"] = phi
     run_both(engine, oracle, data, draws, FB + ["alpha_tk", "beta_tk"], flags=scan_flags(5))
+
+
+# ---- hmm.stan (Gaussian emissions) on the large-K scan (Missing 4) ----------------
+def run_gauss(engine, oracle, data, draws, pars, flags=0):
+    import hhmm_amd
+    got = hhmm_amd.gqs("hmm", data, draws, pars=pars, lib=engine, return_status=True, flags=flags)
+    ref = oracle.gqs("hmm", data, draws, pars=pars, return_status=True, nthreads=16)
+    extra = ["pair_status"] if "zstar_t" in pars else []
+    compare_all(got, ref, pars + extra)
+
+
+@pytest.mark.parametrize("K", [9, 16, 23, 32])
+@pytest.mark.parametrize("T,log2", [(1, 5), (33, 5), (700, 6), (4000, 8)])
+def test_forced_scan_gauss(engine, oracle, K, T, log2):
+    """hmm.stan at K > 8 (K is data, hmm/stan/hmm.stan:8): e_t(j) = exp(lpdf_j - m_t)
+    in the chunk products, each chunk's sum of the shifts m_t its log scale, the
+    summed t = 1 emission (Q2) in phase 2's initial log scale."""
+    data, draws = synth.hmm_gauss(N=2, S=3, T=T, K=K)
+    run_gauss(engine, oracle, data, draws, ["loglik", "alpha_tk", "beta_tk", "ungamma_tk", "gamma_tk"],
+              flags=scan_flags(log2))
+
+
+def test_auto_scan_gauss_T1e5(engine, oracle):
+    """Few pairs, long T: the automatic dispatch takes the scan for hmm.stan too."""
+    data, draws = synth.hmm_gauss(N=1, S=3, T=100_000, K=12)
+    data["T"] = np.array([100_000], dtype=np.int32)
+    run_gauss(engine, oracle, data, draws, FB + ["zstar_t", "logp_zstar"])

@@ -3,9 +3,15 @@
 * probability-space outputs (alpha, beta, gamma, ungamma): |a - b| <= 1e-9 |b| + 1e-250.
   The reference normalises in probability space, so components below ~1e-308
   flush to 0; the floor keeps such underflow from counting.
-* log-space outputs (loglik, unalpha, unbeta, logp_zstar, oblik): |a - b| <= 1e-9 max(|b|, 1).
-  A relative error is meaningless for a log-density near 0; 1e-9 absolute in
-  log space is 1e-9 relative in probability.
+* log-space outputs (loglik, unalpha, unbeta, logp_zstar, oblik): |a - b| <= 1e-9 max(|b|, 1),
+  i.e. 1e-9 relative to the log value (north_star's bound for the
+  log-likelihood), with an absolute floor of 1e-9 near 0 where a relative
+  error is meaningless.  This is NOT 1e-9 relative in probability for the
+  per-step log outputs of a long series: at T = 10^6 |unalpha_tk| reaches
+  ~2e6, so the bound is 2e-3 in log space there.  The per-step
+  posteriors are held to 1e-9 relative in probability by the alpha / beta /
+  gamma comparisons (PROB above), which every long-series test makes; the
+  log-space bound is reported (max_log_abs_err) where those tests print it.
 * NaN / +-inf must sit in the same places on both sides.
 * integer outputs (zstar_t, z_ffbs, pair_status): exact.
 """
