@@ -53,12 +53,19 @@ __device__ __forceinline__ bool cr_round_safe(double v, double w, double err)
     return (eb != 0) & (eb != 0x7ff0000000000000ULL) & (__builtin_fabs(w) + err < hu);
 }
 
+/* The quick phases' rounding test on the device: hhmm_round_ziv (one fma and
+ * one compare; hhmm_crmath.h states the bound) instead of cr_round_safe's
+ * ~10 VALU -- the round tests were 154 static VALU of the C3 sweep. */
+__device__ __forceinline__ bool cr_fast_ok(double hi, double lo, double c) { return hhmm_round_ziv(hi, lo, c); }
+constexpr double kCrExpC = HHMM_CR_EXP_ZIV;
+constexpr double kCrLogC = HHMM_CR_LOG_ZIV;
+
 __device__ __forceinline__ double dev_cr_exp(double x)
 {
     const bool in = (x > -707.0) & (x < 693.0); /* NaN: false */
     int e;
     const hhmm_dd f = hhmm_cr_exp_quick_dd(in ? x : 0.0, &e);
-    const bool ok = in & cr_round_safe(f.hi, f.lo, f.hi * 0x1p-72);
+    const bool ok = in & cr_fast_ok(f.hi, f.lo, kCrExpC); /* f.hi in [0.99, 2.01): normal */
     double r = f.hi * hhmm_bits_to_double((uint64_t)(e + 1023) << 52);
     if (!ok)
         r = cr_exp_cold(x);
@@ -69,7 +76,7 @@ __device__ __forceinline__ double dev_cr_log(double x)
 {
     const bool in = (x >= 0x1p-1022) & (x < __builtin_inf()) & (x != 1.0); /* NaN: false */
     const hhmm_dd f = hhmm_cr_log_quick_dd(in ? x : 2.0);
-    const bool ok = in & cr_round_safe(f.hi, f.lo, __builtin_fabs(f.hi) * 0x1p-68);
+    const bool ok = in & cr_fast_ok(f.hi, f.lo, kCrLogC); /* x normal, != 1: |f.hi| >= 2^-54, normal */
     double r = f.hi;
     if (!ok)
         r = cr_log_cold(x);

@@ -212,7 +212,7 @@ __device__ __forceinline__ void softmax_cr_log(const double (&v)[K], double (&A)
         const bool in = (y[i] > -707.0) & (y[i] < 693.0); /* NaN: false */
         int e;
         const hhmm_dd f = hhmm_cr_exp_quick_dd(in ? y[i] : 0.0, &e);
-        ok[i] = in & cr_round_safe(f.hi, f.lo, f.hi * 0x1p-72);
+        ok[i] = in & cr_fast_ok(f.hi, f.lo, kCrExpC);
         double r = f.hi * hhmm_bits_to_double((uint64_t)(e + 1023) << 52);
         rho[i] = f.lo * rcp_refined(f.hi);
         if (!ok[i])

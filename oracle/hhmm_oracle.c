@@ -1416,7 +1416,7 @@ void hhmm_oracle_det_exp_array(const double *in, double *out, int64_t n)
  * once (must be 0), stats[3] = arguments the quick phase covered. */
 void hhmm_oracle_crmath_quick_check(int which, const double *in, int64_t n, double *stats)
 {
-    double maxrel = 0.0, fails = 0.0, bad = 0.0, covered = 0.0;
+    double maxrel = 0.0, fails = 0.0, bad = 0.0, covered = 0.0, zfails = 0.0, zbad = 0.0;
     for (int64_t i = 0; i < n; ++i) {
         const double x = in[i];
         hhmm_dd q, a;
@@ -1430,6 +1430,10 @@ void hhmm_oracle_crmath_quick_check(int which, const double *in, int64_t n, doub
             acc = a.hi + a.lo;
             bound = fabs(q.hi) * 0x1p-68;
             bad += (hhmm_cr_log(x) != acc);
+            /* the device's test (hhmm_round_ziv): where it accepts, q.hi must be the CR value */
+            const int zok = hhmm_round_ziv(q.hi, q.lo, HHMM_CR_LOG_ZIV);
+            zfails += !zok;
+            zbad += zok && q.hi != acc;
         } else {
             if (!(x > -707.0 && x < 693.0))
                 continue;
@@ -1442,6 +1446,9 @@ void hhmm_oracle_crmath_quick_check(int which, const double *in, int64_t n, doub
             acc = a.hi + a.lo;
             bound = q.hi * 0x1p-72;
             bad += (hhmm_cr_exp(x) != acc * ldexp(1.0, ea));
+            const int zok = hhmm_round_ziv(q.hi, q.lo, HHMM_CR_EXP_ZIV);
+            zfails += !zok;
+            zbad += zok && q.hi != acc;
         }
         covered += 1.0;
         const double rel = fabs((q.hi - a.hi) + (q.lo - a.lo)) / fabs(a.hi);
@@ -1453,6 +1460,8 @@ void hhmm_oracle_crmath_quick_check(int which, const double *in, int64_t n, doub
     stats[1] = fails;
     stats[2] = bad;
     stats[3] = covered;
+    stats[4] = zfails;
+    stats[5] = zbad;
 }
 
 const char *hhmm_oracle_variant(void)

@@ -91,18 +91,20 @@ def det_array(which, x):
     return y
 
 
-def crmath_quick_check(which, x):
+def crmath_quick_check(which, x, ziv=False):
     """(max relative quick-vs-accurate distance, rounding-test fallbacks,
     mismatches, arguments covered) of hhmm_crmath.h's quick phase; which is
-    "log" or "exp"."""
+    "log" or "exp".  ziv=True appends (the device's one-fma test hhmm_round_ziv:
+    fallbacks, accepted-but-not-correctly-rounded arguments -- must be 0)."""
     import numpy as np
     lib = load("cr")
     x = np.ascontiguousarray(x, dtype=np.float64)
-    st = np.zeros(4)
+    st = np.zeros(6)
     lib.hhmm_oracle_crmath_quick_check(C.c_int({"log": 0, "exp": 1}[which]),
                                        x.ctypes.data_as(C.POINTER(C.c_double)), C.c_int64(x.size),
                                        st.ctypes.data_as(C.POINTER(C.c_double)))
-    return float(st[0]), int(st[1]), int(st[2]), int(st[3])
+    out = (float(st[0]), int(st[1]), int(st[2]), int(st[3]))
+    return out + (int(st[4]), int(st[5])) if ziv else out
 
 
 def log_array(x, variant="cr"):

@@ -136,3 +136,22 @@ def test_crmath_quick_phase_matches_accurate_phase(oracle):
         assert bad == 0, name
         assert maxrel < 2.0 ** -75, (name, np.log2(maxrel))
         assert fails < 1e-3 * cov, (name, fails)
+
+
+def test_device_ziv_rounding_test_is_sound(oracle):
+    """The device's one-fma rounding test (hhmm_round_ziv, hhmm_crmath.h) on the
+    oracle's quick phases: every argument it accepts has the quick head equal to
+    the accurate phase's rounding, and it falls back about as rarely as the
+    exact-interval test it replaced (cr_round_safe / hhmm_round_safe).  Includes
+    arguments built to sit next to rounding boundaries: products / quotients of
+    nearby doubles and exact powers of two, where the gap halves."""
+    import pyoracle
+    logs, exps = _quick_sets(1_000_000, seed=23)
+    g = np.random.Generator(np.random.Philox(24))
+    logs["pow2"] = np.ldexp(1.0, g.integers(-1000, 1000, 20000)) * (1.0 + g.integers(-4, 5, 20000) * 2.0 ** -52)
+    exps["log_pow2"] = np.log(2.0) * g.integers(-1000, 990, 20000) + g.integers(-3, 4, 20000) * 2.0 ** -40
+    for which, sets in (("log", logs), ("exp", exps)):
+        for name, x in sets.items():
+            maxrel, fails, bad, cov, zfails, zbad = pyoracle.crmath_quick_check(which, x, ziv=True)
+            assert zbad == 0, (which, name)
+            assert zfails <= 2 * fails + 1e-4 * cov, (which, name, zfails, fails)
