@@ -55,6 +55,23 @@ __device__ __forceinline__ lks_d4 lks_mfma(double a, double b, lks_d4 c)
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+/* v_mfma_f64_4x4x4_16b_f64 (operand maps measured by tools/mfma_probe.hip,
+ * profiles/r05a_mfma_probe.txt): four independent 4 x 4 x 4 blocks b = 0..3;
+ * lane 16k + 4b + r holds block b's A[r][k], lane 16k + 4b + c its B[k][c],
+ * and the result D[r][c] lands in lane 16r + 4b + c -- the B layout again.
+ * 512 FLOP per instruction at a quarter of the 16x16x4 form's cycles (the
+ * probe: 71.5 against 49.5 TFLOP/s). */
+__device__ __forceinline__ double lks_mfma4(double a, double b, double c)
+{
+    return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+/* Build knob: the chunk products on v_mfma_f64_4x4x4 (1) or 16x16x4 (0).  With
+ * the 4 x 4 blocks the state dimension pads to a multiple of 4 instead of 16
+ * (K = 23: 24 x 24 instead of 32 x 24 per step, VERDICT r4's 1.45x padding). */
+#ifndef HHMM_LKS_MFMA4
+#define HHMM_LKS_MFMA4 1
+#endif
+
 /* Columns of M'^T per wave: TPW tiles of 16.  RT row tiles of 16 states, KSM
  * k-steps of 4 states (K <= 16: 1 / 4; K <= 24: 2 / 6; K <= 32: 2 / 8). */
 constexpr int kLksTiles = 2;
@@ -100,6 +117,19 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
             tab[idx] = j < K ? a.phi_k[d + S * ((int64_t)j + (int64_t)K * l)] : 0.0;
         }
     }
+#if HHMM_LKS_MFMA4
+    /* A operand of the 4 x 4 blocks: every block takes the same 4 x 4 block of
+     * A^T, aop4[so][si] = A^T[4so + r][4si + k] = A(4si + k, 4so + r) with
+     * r = lane & 3, k = lane >> 4 */
+    double aop4[KSM][KSM];
+#pragma unroll
+    for (int so = 0; so < KSM; ++so)
+#pragma unroll
+        for (int si = 0; si < KSM; ++si) {
+            const int i = 4 * si + (lane >> 4), j = 4 * so + (lane & 3);
+            aop4[so][si] = (i < K && j < K) ? a.A_ij[d + S * ((int64_t)i + (int64_t)K * j)] : 0.0;
+        }
+#else
     /* A operand: Aop[rt][kk] = A^T[j][i] = A(i, j), i = 4kk + (lane >> 4), j = 16rt + (lane & 15) */
     double aop[RT][KSM];
 #pragma unroll
@@ -109,6 +139,7 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
             const int i = 4 * kk + (lane >> 4), j = 16 * rt + (lane & 15);
             aop[rt][kk] = (i < K && j < K) ? a.A_ij[d + S * ((int64_t)i + (int64_t)K * j)] : 0.0;
         }
+#endif
     __syncthreads();
 
     /* this lane's column in each tile: (chunk c, initial state i); B operand
@@ -165,7 +196,30 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
             const int s = s0 + v;
             if (s >= smax)
                 break;
-            /* D = A^T Q for every tile (independent accumulators interleaved) */
+            /* D = A^T Q for every tile (independent accumulators interleaved);
+             * accv(u, kk): state 4kk + (lane >> 4) of the lane's column */
+#if HHMM_LKS_MFMA4
+            double acc4[TPW][KSM];
+#pragma unroll
+            for (int u = 0; u < TPW; ++u)
+#pragma unroll
+                for (int so = 0; so < KSM; ++so)
+                    acc4[u][so] = 0.0;
+#pragma unroll
+            for (int si = 0; si < KSM; ++si) {
+                if (si < ks) {
+#pragma unroll
+                    for (int so = 0; so < KSM; ++so) {
+                        if (so < ks) {
+#pragma unroll
+                            for (int u = 0; u < TPW; ++u)
+                                acc4[u][so] = lks_mfma4(aop4[so][si], q[u][si], acc4[u][so]);
+                        }
+                    }
+                }
+            }
+            auto accv = [&](int u, int kk) -> double { return acc4[u][kk]; };
+#else
             lks_d4 acc[TPW][RT];
 #pragma unroll
             for (int u = 0; u < TPW; ++u)
@@ -182,6 +236,8 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
                             acc[u][rt] = lks_mfma(aop[rt][kk], q[u][kk], acc[u][rt]);
                 }
             }
+            auto accv = [&](int u, int kk) -> double { return acc[u][kk >> 2][kk & 3]; };
+#endif
             /* emission of the column's step, renormalisation of the column */
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
@@ -219,7 +275,7 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
                 double mx = 0.0;
 #pragma unroll
                 for (int kk = 0; kk < KSM; ++kk) {
-                    nv[kk] = acc[u][kk >> 2][kk & 3] * em[kk];
+                    nv[kk] = accv(u, kk) * em[kk];
                     mx = fmax(mx, nv[kk]);
                 }
                 mx = fmax(mx, __shfl_xor(mx, 16));

@@ -101,7 +101,9 @@ def test_tayal_long_series_scan(engine, oracle):
     """One series under many draws, long T: the T-scan and the V-scan (C5's dispatch)."""
     data, draws = synth.tayal(N=2, S=8, T=40_000)
     bad = _corrupt(data, "x", 1, 39_999, 0)
-    _run(engine, oracle, "hhmm-tayal2009", data, bad, draws, ["loglik", "gamma_tk", "zstar_t"], [1])
+    # alpha / beta, not gamma: past t ~ 2000 the Q6 masks underflow gamma's overlap to
+    # NaN at the subnormal edge (tests/test_gpu_configs.py compare_tayal_gamma)
+    _run(engine, oracle, "hhmm-tayal2009", data, bad, draws, ["loglik", "alpha_tk", "beta_tk", "zstar_t"], [1])
 
 
 def test_large_k_symbol_out_of_range(engine, oracle):
