@@ -117,4 +117,6 @@ def test_iohmm_large_K_fitted_draws(engine, oracle, model, K):
                 assert np.array_equal(g.view(np.int64) if g.dtype == np.float64 else g,
                                       r.view(np.int64) if r.dtype == np.float64 else r), (model, K, name, p)
         rest = [n for n in pars if n not in hat]
-        compare_all(got, ref, rest + ["pair_status"])
+        # pair_status is the Viterbi's (the oracle always decodes: T = 1 pairs are Q3's
+        # unset back-pointer); compared where the engine decodes too
+        compare_all(got, ref, rest + (["pair_status"] if "zstar_t" in pars else []))
