@@ -162,3 +162,26 @@ def test_degenerate_draw_sign_class_paths(engine, oracle, kind, T, flags):
     compare_all(got, ref, names)
     from test_gpu_configs import compare_tayal_gamma
     compare_tayal_gamma(got, ref, max_forgiven=0)
+
+
+def test_c5_scale_gamma_at_table8_point(engine, oracle):
+    """C5's shape (one series of 10^6 legs under many draws; the T-scan and the V-scan) at
+    the reference's own parameter point, over the report's symbol mix in runs.  On C5's
+    synthetic data gamma is ~99.7 % NaN rows (Q6: the forward and backward masks drive
+    alpha and beta apart until their overlap underflows); at Table 8's
+    point and Table 4's mix the overlap stays finite, so gamma itself is compared at every
+    one of the 10^6 steps of 8 pairs -- with loglik, alpha, beta and the Viterbi."""
+    import hhmm_amd
+    T = 1_000_000
+    g = synth.rng(synth.SEED, 10)
+    f = _legs(g, T, True)
+    data = {"K": 4, "L": 9, "x": np.where(f <= 9, f, f - 9)[None], "sign": np.where(f <= 9, 1, 2)[None]}
+    draws = _draws(8, seed=11)
+    got = hhmm_amd.gqs("hhmm-tayal2009", data, draws, pars=LIN, lib=engine, return_status=True)
+    ref = oracle.gqs("hhmm-tayal2009", data, draws, pars=FULL, return_status=True, nthreads=8)
+    nan_rows = int(np.isnan(ref["gamma_tk"]).any(axis=-1).sum())
+    print(f"oracle gamma NaN rows: {nan_rows} of {8 * T}")
+    assert nan_rows < 0.01 * 8 * T
+    compare_all(got, ref, [n for n in LIN if n != "gamma_tk"] + ["pair_status"])
+    from test_gpu_configs import compare_tayal_gamma
+    compare_tayal_gamma(got, ref, max_forgiven=64)
