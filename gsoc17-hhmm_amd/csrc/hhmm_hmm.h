@@ -1728,16 +1728,21 @@ __device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const P
     static_assert(CV == 8, "phased sweep: 8-step chunks");
     const int nfull = Tw_min / CV;
     const int nchunk = (Tw_max + CV - 1) / CV;
-    const uint32_t L = (uint32_t)a.L;
-    uint32_t oob = 0;
-    auto pack_put = [&](int c, const Obs (&cur)[CV]) {
+    /* the largest x - 1 as unsigned (x < 1 wraps above L): one sub and one max
+     * per symbol on the wave's full chunks, the length test on the rest */
+    uint32_t xm = 0;
+    auto pack_put = [&](int c, const Obs (&cur)[CV], auto full) {
         if (c * CV < Tp) {
             put_tmp(a.xpk + a.P * (int64_t)c, (uint32_t)p * 4u, pack_chunk<MODEL, K>(cur));
 #pragma unroll
-            for (int v = 0; v < CV; ++v)
-                oob |= ((uint32_t)(cur[v].x - 1) >= L) & (c * CV + v < Tp);
+            for (int v = 0; v < CV; ++v) {
+                const uint32_t xv = (uint32_t)(cur[v].x - 1);
+                xm = max(xm, (decltype(full)::value || c * CV + v < Tp) ? xv : 0u);
+            }
         }
     };
+    const std::true_type full;
+    const std::false_type tail;
     Obs cur[CV];
     load_chunk<MODEL, CV, false>(cur, sp, 0);
     constexpr int D = kVitGroup;
@@ -1753,7 +1758,7 @@ __device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const P
     dl[K - 1] = le[K - 1];
     word = 0;
     vit_fwd_chunk<MODEL, K, CV, false, true>(a, p, pp, slab, Tp, 0, cur, grp[0][0], le, dl, word);
-    pack_put(0, cur);
+    pack_put(0, cur, tail);
     int c = 1;
     for (; c + D <= nfull; c += D) {
         Obs nxt[D][CV];
@@ -1764,7 +1769,7 @@ __device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const P
         for (int i = 0; i < D; ++i) {
             vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c + i, grp[i],
                                               (i + 1 < D) ? grp[i + 1 < D ? i + 1 : 0][0] : nxt[0][0], le, dl, word);
-            pack_put(c + i, grp[i]);
+            pack_put(c + i, grp[i], full); /* c + i < nfull: every lane's steps are < Tp */
         }
 #pragma unroll
         for (int i = 0; i < D; ++i)
@@ -1779,12 +1784,12 @@ __device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const P
         Obs nxt[CV];
         load_chunk<MODEL, CV, false>(nxt, sp, (c + 1) * CV);
         vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
-        pack_put(c, cur);
+        pack_put(c, cur, tail);
 #pragma unroll
         for (int u = 0; u < CV; ++u)
             cur[u] = nxt[u];
     }
-    bad = oob != 0;
+    bad = xm >= (uint32_t)a.L;
 }
 
 /* Phase 2: the scaled filter over the packed symbols (FB_BIG checkpoints),
