@@ -74,7 +74,10 @@ __device__ __forceinline__ double lks_mfma4(double a, double b, double c)
 
 /* Columns of M'^T per wave: TPW tiles of 16.  RT row tiles of 16 states, KSM
  * k-steps of 4 states (K <= 16: 1 / 4; K <= 24: 2 / 6; K <= 32: 2 / 8). */
-constexpr int kLksTiles = 2;
+#ifndef HHMM_LKS_TILES
+#define HHMM_LKS_TILES 2 /* build knob: 16-column tiles per wave (independent accumulator chains) */
+#endif
+constexpr int kLksTiles = HHMM_LKS_TILES;
 
 template <int RT, int KSM, bool GS>
 __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
