@@ -18,6 +18,7 @@ ERR_NO_DEVICE = -5
 
 PAIR_OK = 0
 PAIR_INVALID_BACKPOINTER = 1
+PAIR_INVALID_DATA = 2  # hhmm_run_device: the series breaks a data-block bound (include/hhmm.h)
 
 MODELS = {
     "hmm": 1,                    # hmm/stan/hmm.stan

@@ -191,3 +191,27 @@ def test_segment_summary_validates_the_request_before_launching(engine):
     st = engine.hhmm_segment_summary_device(C.byref(pr.req), C.byref(seg), None, 0, None)
     assert st == _abi.ERR_INVALID_ARGUMENT
     assert b"A_ij" in engine.hhmm_last_error()
+
+
+def test_python_constants_match_header():
+    """Every HHMM_* integer #define / enum value of include/hhmm.h that hhmm_amd._abi
+    mirrors has the header's value (status codes, pair status, models, pairing, flags)."""
+    import re
+    from hhmm_amd import _abi
+    text = (REPO / "include" / "hhmm.h").read_text()
+    vals = {}
+    for name, v in re.findall(r"#define HHMM_(\w+)\s+\(?(\d+)u?\)?\s", text):
+        vals[name] = int(v)
+    for name, v in re.findall(r"#define HHMM_(\w+)\s+\(1u << (\d+)\)", text):
+        vals[name] = 1 << int(v)
+    for name, v in re.findall(r"HHMM_(\w+)\s*=\s*(-?\d+)", text):
+        vals[name] = int(v)
+    checked = 0
+    for name, hv in vals.items():
+        for py in (name, name.replace("MODEL_", "")):
+            if hasattr(_abi, py) and isinstance(getattr(_abi, py), int):
+                assert getattr(_abi, py) == hv, (name, getattr(_abi, py), hv)
+                checked += 1
+                break
+    assert _abi.PAIR_INVALID_DATA == vals["PAIR_INVALID_DATA"] == 2
+    assert checked >= 15, checked

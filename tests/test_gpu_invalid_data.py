@@ -18,7 +18,7 @@ from tolerances import compare
 
 pytestmark = pytest.mark.gpu
 
-INVALID_DATA = 2
+INVALID_DATA = _abi.PAIR_INVALID_DATA
 
 
 def _run(engine, oracle, model, data, bad_data, draws, pars, bad_series, pairing="grid", flags=0):
