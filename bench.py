@@ -307,9 +307,11 @@ class DeviceRun:
     request with HHMM_FLAG_FUSED: one fused forward-backward + Viterbi sweep),
     and the two halves alone ("fb", "viterbi")."""
 
-    def __init__(self, lib, x, draws, P, T, dev):
+    def __init__(self, lib, x, draws, P, T, dev, share=None):
+        """share: another DeviceRun whose output and workspace buffers this one
+        reuses (tools/ab_bench.py: every library variant on the same memory)."""
         self.lib = lib
-        self.out = {
+        self.out = share.out if share is not None else {
             "loglik": torch.empty(P, dtype=torch.float64, device=dev),
             "gamma_tk": torch.empty((K, T, P), dtype=torch.float64, device=dev),
             "zstar_t": torch.empty((T, P), dtype=torch.int32, device=dev),
@@ -318,7 +320,7 @@ class DeviceRun:
         }
         hot = ["loglik", "gamma_tk", "zstar_t", "logp_zstar"]
         self.reqs = {}
-        self._ws = {}
+        self._ws = share._ws if share is not None else {}
         for name, outs, flags in (("step", hot, 0), ("fused", hot, _abi.FLAG_FUSED),
                                   ("split", hot, _abi.FLAG_FB_SPLIT), ("vfb", hot, _abi.FLAG_VFB),
                                   ("two", hot, _abi.FLAG_VFB_OFF),
@@ -346,9 +348,11 @@ class DeviceRun:
             assert lib.hhmm_workspace_size(C.byref(r), C.byref(ws)) == 0
             # one workspace per size (the requests run one at a time on one stream)
             need = max(int(ws.value), 256)
-            if need not in self._ws:
+            fit = [k for k in self._ws if k >= need]
+            if not fit:
                 self._ws[need] = torch.empty(need, dtype=torch.uint8, device=dev)
-            self.reqs[name] = (r, res, self._ws[need])
+                fit = [need]
+            self.reqs[name] = (r, res, self._ws[min(fit)])
 
     def launch(self, name):
         r, res, ws = self.reqs[name]

@@ -741,6 +741,22 @@ __device__ __forceinline__ void emit_posteriors(const DevArgs &a, int64_t p, int
     }
 }
 
+#ifndef HHMM_INLINE_XCHECK
+#define HHMM_INLINE_XCHECK 1 /* A/B knob: 0 leaves x to the device entry's separate check pass */
+#endif
+
+/* The device entry's data check done inline by a whole-series sweep that reads
+ * x anyway (HHMM_PAIR_INVALID_DATA): the running max of x - 1 as unsigned (an
+ * x < 1 wraps above L), one sub and one max per symbol; steps at or past the
+ * lane's own length count only on the wave's partial chunks (FULL: none). */
+template <int C, bool FULL>
+__device__ __forceinline__ void xcheck_acc(uint32_t &xm, const Obs (&o)[C], int c, int Tp)
+{
+#pragma unroll
+    for (int v = 0; v < C * HHMM_INLINE_XCHECK; ++v)
+        xm = max(xm, (FULL || c * C + v < Tp) ? (uint32_t)(o[v].x - 1) : 0u);
+}
+
 /* Per-lane state of the forward-backward kernel. */
 template <int MODEL, int K>
 struct FbLane {
@@ -754,6 +770,7 @@ struct FbLane {
     int64_t q;   /* checkpoint column (the pair, or the scan lane) */
     int64_t Qs;  /* checkpoint row stride */
     bool noinit = false; /* step 0 is not the series' first (a segment window's chunk 0) */
+    int64_t n = 0;       /* the series (fb_block: the inline data check's flag) */
 };
 
 /* One forward chunk [t0, t0+C).  FULLC: every lane of the wave has all C
@@ -1056,6 +1073,9 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
         load_chunk<MODEL, C, AUX>(grp[i], sp, (cb + i) * C);
     Em<K> ecur;
     emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, grp[0][0], ecur);
+    /* whole-series sweeps over x alone check it inline (xcheck_acc) */
+    constexpr bool XCHK = !SCAN && !AUX && ModelTraits<MODEL>::kDiscrete && HHMM_INLINE_XCHECK;
+    uint32_t xm = 0;
     int c = cb;
     for (; c + D <= nfull; c += D) {
         Obs nxt[D][C];
@@ -1063,9 +1083,12 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
         for (int i = 0; i < D; ++i)
             load_chunk<MODEL, C, AUX>(nxt[i], sp, (c + D + i) * C);
 #pragma unroll
-        for (int i = 0; i < D; ++i)
+        for (int i = 0; i < D; ++i) {
             fwd_chunk<MODEL, K, C, MODE, true>(a, ln, c + i, grp[i], (i + 1 < D) ? grp[i + 1 < D ? i + 1 : 0][0]
                                                                               : nxt[0][0], ecur, al, lsc, ex);
+            if constexpr (XCHK)
+                xcheck_acc<C, true>(xm, grp[i], c + i, ln.Tp);
+        }
 #pragma unroll
         for (int i = 0; i < D; ++i)
 #pragma unroll
@@ -1079,10 +1102,15 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
         Obs nxt[C];
         load_chunk<MODEL, C, AUX>(nxt, sp, (c + 1) * C);
         fwd_chunk<MODEL, K, C, MODE, false>(a, ln, c, cur, nxt[0], ecur, al, lsc, ex);
+        if constexpr (XCHK)
+            xcheck_acc<C, false>(xm, cur, c, ln.Tp);
 #pragma unroll
         for (int u = 0; u < C; ++u)
             cur[u] = nxt[u];
     }
+    if constexpr (XCHK)
+        if (a.dc_flag && xm >= (uint32_t)ln.L)
+            a.dc_flag[ln.n] = 1;
     if (!SCAN && (a.outputs & HHMM_OUT_LOGLIK) && a.loglik)
         a.loglik[p] = log(vsum<K>(al)) + (lsc + kLn2 * ex);
     } /* forward sweep */
@@ -1186,6 +1214,7 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, int64_t gwave)
 
     FbLane<MODEL, K> ln;
     ln.p = p;
+    ln.n = n;
     ln.L = a.L;
     ln.t0 = 0;
     ln.Tp = pair_len(a, n);
@@ -1416,6 +1445,11 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
     uint32_t word = 0;
     /* chunk 0: the t = 1 row and the NaN step (Q3) */
     vit_fwd_chunk<MODEL, K, CV, false, true>(a, p, pp, slab, Tp, 0, cur, grp[0][0], le, dl, word);
+    /* decoding x itself: the data check inline (xcheck_acc) */
+    constexpr bool XCHK = !PK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete && HHMM_INLINE_XCHECK;
+    uint32_t xm = 0;
+    if constexpr (XCHK)
+        xcheck_acc<CV, false>(xm, cur, 0, Tp);
     int c = 1;
     for (; c + D <= nfull; c += D) {
         Obs nxt[D][CV];
@@ -1423,9 +1457,12 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
         for (int i = 0; i < D; ++i)
             vload(nxt[i], sp, (c + D + i) * CV);
 #pragma unroll
-        for (int i = 0; i < D; ++i)
+        for (int i = 0; i < D; ++i) {
             vit_fwd_chunk<MODEL, K, CV, true>(a, p, pp, slab, Tp, c + i, grp[i],
                                               (i + 1 < D) ? grp[i + 1 < D ? i + 1 : 0][0] : nxt[0][0], le, dl, word);
+            if constexpr (XCHK)
+                xcheck_acc<CV, true>(xm, grp[i], c + i, Tp);
+        }
 #pragma unroll
         for (int i = 0; i < D; ++i)
 #pragma unroll
@@ -1439,10 +1476,15 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
         Obs nxt[CV];
         vload(nxt, sp, (c + 1) * CV);
         vit_fwd_chunk<MODEL, K, CV, false>(a, p, pp, slab, Tp, c, cur, nxt[0], le, dl, word);
+        if constexpr (XCHK)
+            xcheck_acc<CV, false>(xm, cur, c, Tp);
 #pragma unroll
         for (int u = 0; u < CV; ++u)
             cur[u] = nxt[u];
     }
+    if constexpr (XCHK)
+        if (a.dc_flag && xm >= (uint32_t)a.L)
+            a.dc_flag[n] = 1;
     viterbi_epilogue<K>(a, p, Tp, Tw_min, Tw_max, dl, word);
 }
 
@@ -1573,6 +1615,7 @@ __device__ __forceinline__ void fbv_block(const DevArgs &a, uint32_t block)
 
     FbLane<MODEL, K> ln;
     ln.p = p;
+    ln.n = n;
     ln.L = a.L;
     ln.t0 = 0;
     ln.Tp = pair_len(a, n);
@@ -1728,17 +1771,12 @@ __device__ __forceinline__ void vfb_viterbi(const DevArgs &a, int64_t p, const P
     static_assert(CV == 8, "phased sweep: 8-step chunks");
     const int nfull = Tw_min / CV;
     const int nchunk = (Tw_max + CV - 1) / CV;
-    /* the largest x - 1 as unsigned (x < 1 wraps above L): one sub and one max
-     * per symbol on the wave's full chunks, the length test on the rest */
+    /* the data check inline (xcheck_acc) */
     uint32_t xm = 0;
     auto pack_put = [&](int c, const Obs (&cur)[CV], auto full) {
         if (c * CV < Tp) {
             put_tmp(a.xpk + a.P * (int64_t)c, (uint32_t)p * 4u, pack_chunk<MODEL, K>(cur));
-#pragma unroll
-            for (int v = 0; v < CV; ++v) {
-                const uint32_t xv = (uint32_t)(cur[v].x - 1);
-                xm = max(xm, (decltype(full)::value || c * CV + v < Tp) ? xv : 0u);
-            }
+            xcheck_acc<CV, decltype(full)::value>(xm, cur, c, Tp);
         }
     };
     const std::true_type full;
@@ -2865,13 +2903,13 @@ __device__ __forceinline__ void rowmat_prefix(RowMat<K> &P, int lane, int nb = 6
 {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        if (d >= nb)
-            break;
-        RowMat<K> X, R;
-        rowmat_shfl_up<K>(P, X, d);
-        rowmat_mul<K>(X, P, R);
-        if (lane >= d)
-            P = R;
+        if (d < nb) { /* wave-uniform; a guard, not a break, so the six levels unroll */
+            RowMat<K> X, R;
+            rowmat_shfl_up<K>(P, X, d);
+            rowmat_mul<K>(X, P, R);
+            if (lane >= d)
+                P = R;
+        }
     }
 }
 
@@ -3251,6 +3289,9 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
     s.lds = std::max(s.lds, std::min(lds_floor("HHMM_PROBE_FB_LDS_KB"), kLdsLimit));
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     const bool ffbs = (a.outputs & HHMM_OUT_FFBS) != 0;
+    constexpr bool xchk = HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
+    /* every fb_kernel below sweeps x forward over whole series (fb_sweep's inline check) */
+    t_data_checked_inline |= xchk && (ffbs || !(a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)));
     if (a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) {
         /* log-scale outputs: the log-space recursion; FFBS draws (if any)
          * from the linear filter of the contract in a second launch */
@@ -3376,10 +3417,13 @@ static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st, bool packed 
         return HHMM_ERR_UNSUPPORTED;
     }
     s.lds = std::max(s.lds, std::min(lds_floor("HHMM_PROBE_VIT_LDS_KB"), kLdsLimit));
-    if (packed && fbv_ok<MODEL, K>())
+    if (packed && fbv_ok<MODEL, K>()) {
         hipLaunchKernelGGL((viterbi_kernel<MODEL, K, fbv_ok<MODEL, K>()>), s.grid, s.block, s.lds, st, a);
-    else
+    } else {
+        /* decodes x itself: viterbi_block's inline check */
+        t_data_checked_inline |= HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
         hipLaunchKernelGGL((viterbi_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("viterbi_kernel launch: %s", hipGetErrorString(e));
@@ -3423,7 +3467,7 @@ static hhmm_status launch_vfb(const DevArgs &a, hipStream_t st)
     }
     hipError_t e = hipMemsetAsync(a.rnw, 0, sizeof(int32_t), st); /* the dense-wave list's count */
     if (e == hipSuccess) {
-        t_data_checked_inline = !ModelTraits<MODEL>::kAux; /* x (and T) checked in phase 1 */
+        t_data_checked_inline |= HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux; /* x (and T) checked in phase 1 */
         hipLaunchKernelGGL((vfb_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
         hipLaunchKernelGGL((vfb_dense_kernel<MODEL, K>), dim3(kDenseBlocks), dim3(64), s.lds / (s.block.x / 64), st,
                            a);
@@ -3449,6 +3493,8 @@ static hhmm_status launch_split(const DevArgs &a, hipStream_t st)
         set_error("emission table K*L = %d*%d does not fit in LDS", a.K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
+    /* the forward launch sweeps x over whole series (fb_sweep's inline check) */
+    t_data_checked_inline |= HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
     hipLaunchKernelGGL((fb_kernel<MODEL, K, MODE, FB_PH_FWD>), s.grid, s.block, s.lds, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -408,31 +408,79 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
 /* ------------------------------------------------------------------ */
 thread_local bool t_data_checked_inline = false;
 
+#ifndef HHMM_DATA_CHECK
+#define HHMM_DATA_CHECK 1 /* A/B knob: 0 drops the device entry's data-block checks */
+#endif
+
 constexpr int kDcSteps = 64; /* time steps per thread of data_check_kernel */
+constexpr int kDcSeries = 4; /* series per thread (one 16-byte load per step) */
 
 /* Flags series n when one of its steps t < T[n] breaks an int<lower=1,
- * upper=hi> bound: v (x, 1..L), w (sign 1..2 / g 1..G; null: none).  Lanes
- * run over series (the fastest index: coalesced rows), grid.y over strips of
- * kDcSteps steps.  A flag is a plain vector store of 1 (every writer stores
- * the same value). */
+ * upper=hi> bound: v (x, 1..L), w (sign 1..2 / g 1..G; null: none).  A
+ * thread takes kDcSeries consecutive series (the fastest index: a wave reads
+ * 1 KB of each row), grid.y strips of kDcSteps steps, 8 steps of independent
+ * loads in flight (HBM-bound: the pass reads each element once).  Steps at or
+ * past a series' own length are read (inside the T_max x N block) and masked.
+ * A flag is a plain vector store of 1 (every writer stores the same value). */
 __global__ void __launch_bounds__(256) data_check_kernel(const int32_t *v, int vhi, const int32_t *w, int whi,
                                                          const int32_t *T, int64_t N, int Tmax, int32_t *flag)
 {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= N)
+    const int64_t n0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kDcSeries;
+    if (n0 >= N)
         return;
-    const int Tn = T ? min(max(T[n], 1), Tmax) : Tmax; /* a length outside 1..T_max: data_mark_kernel */
+    const int nk = (int)min<int64_t>(kDcSeries, N - n0);
+    int Tn[kDcSeries];
+#pragma unroll
+    for (int j = 0; j < kDcSeries; ++j) /* a length outside 1..T_max: data_mark_kernel */
+        Tn[j] = j < nk ? (T ? min(max(T[n0 + j], 1), Tmax) : Tmax) : 0;
     const int t0 = (int)blockIdx.y * kDcSteps;
-    const int t1 = min(t0 + kDcSteps, Tn);
-    bool bad = false;
-    for (int t = t0; t < t1; ++t) {
-        const int64_t i = n + N * (int64_t)t;
-        bad |= (uint32_t)(v[i] - 1) >= (uint32_t)vhi;
+    const int t1 = min(t0 + kDcSteps, Tmax);
+    const bool vec = nk == kDcSeries && (N % kDcSeries) == 0 && ((uintptr_t)v % 16) == 0 &&
+                     (!w || ((uintptr_t)w % 16) == 0);
+    bool bad[kDcSeries] = {};
+    auto test = [&](int hi, int t, int j, int val) {
+        bad[j] |= (t < Tn[j]) & ((uint32_t)(val - 1) >= (uint32_t)hi);
+    };
+    if (vec) {
+        auto pass = [&](const int32_t *u, int hi) {
+            int t = t0;
+            for (; t + 8 <= t1; t += 8) {
+                int4 q[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    q[i] = *reinterpret_cast<const int4 *>(u + n0 + N * (int64_t)(t + i));
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    test(hi, t + i, 0, q[i].x);
+                    test(hi, t + i, 1, q[i].y);
+                    test(hi, t + i, 2, q[i].z);
+                    test(hi, t + i, 3, q[i].w);
+                }
+            }
+            for (; t < t1; ++t) {
+                const int4 q = *reinterpret_cast<const int4 *>(u + n0 + N * (int64_t)t);
+                test(hi, t, 0, q.x);
+                test(hi, t, 1, q.y);
+                test(hi, t, 2, q.z);
+                test(hi, t, 3, q.w);
+            }
+        };
+        pass(v, vhi);
         if (w)
-            bad |= (uint32_t)(w[i] - 1) >= (uint32_t)whi;
+            pass(w, whi);
+    } else {
+        for (int j = 0; j < nk; ++j)
+            for (int t = t0; t < min(t1, Tn[j]); ++t) {
+                const int64_t i = n0 + j + N * (int64_t)t;
+                test(vhi, t, j, v[i]);
+                if (w)
+                    test(whi, t, j, w[i]);
+            }
     }
-    if (bad)
-        flag[n] = 1;
+#pragma unroll
+    for (int j = 0; j < kDcSeries; ++j)
+        if (bad[j])
+            flag[n0 + j] = 1;
 }
 
 /* pair_status[p] = HHMM_PAIR_INVALID_DATA for the pairs of flagged series and
@@ -460,9 +508,10 @@ static hhmm_status launch_data_check(const DevArgs &a, const hhmm_request *req, 
     const bool discrete = m == HHMM_MODEL_HMM_MULTINOM || m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ||
                           m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE;
     const bool tayal = m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE;
-    hipError_t e = hipMemsetAsync(a.dc_flag, 0, (size_t)d.n_series * sizeof(int32_t), st);
+    hipError_t e = hipSuccess; /* a.dc_flag cleared by launch_all before the model's kernels */
     auto check = [&](const int32_t *v, int vhi, const int32_t *w, int whi, const int32_t *T, int Tmax) {
-        const dim3 grid((unsigned)((d.n_series + 255) / 256), (unsigned)((Tmax + kDcSteps - 1) / kDcSteps));
+        const int64_t thr = (d.n_series + kDcSeries - 1) / kDcSeries;
+        const dim3 grid((unsigned)((thr + 255) / 256), (unsigned)((Tmax + kDcSteps - 1) / kDcSteps));
         hipLaunchKernelGGL(data_check_kernel, grid, dim3(256), 0, st, v, vhi, w, whi, T, (int64_t)d.n_series, Tmax,
                            a.dc_flag);
     };
@@ -523,7 +572,7 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
 {
     DevArgs a = make_args(req, res, P);
     bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max, (uint32_t)req->flags);
-    const bool check = check_data && a.pair_status && a.dc_flag;
+    const bool check = HHMM_DATA_CHECK && check_data && a.pair_status && a.dc_flag;
     if (!check)
         a.dc_flag = nullptr;
     if (seg) {
@@ -539,6 +588,13 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
         }
     }
     t_data_checked_inline = false;
+    if (check) { /* series flags: the inline checks of the model's sweeps, then data_check_kernel */
+        const hipError_t e = hipMemsetAsync(a.dc_flag, 0, (size_t)req->data.n_series * sizeof(int32_t), st);
+        if (e != hipSuccess) {
+            set_error("data check: %s", hipGetErrorString(e));
+            return HHMM_ERR_HIP;
+        }
+    }
     hhmm_status s = launch_model(req, a, res, st);
     if (s != HHMM_OK || !check)
         return s;

@@ -110,3 +110,43 @@ def test_large_k_symbol_out_of_range(engine, oracle):
     data, draws = synth.hmm_multinom(N=6, S=16, T=200, K=12, L=9)
     bad = _corrupt(data, "x", 2, 150, 10)
     _run(engine, oracle, "hmm-multinom", data, bad, draws, ["loglik", "gamma_tk", "zstar_t"], [2])
+
+
+_LANES = _abi.FLAG_SCAN_OFF | _abi.FLAG_VIT_SCAN_OFF | _abi.FLAG_VIT_LANES
+SCHEDULES = [
+    # (id, outputs, flags): which kernels read x, hence which check runs
+    ("fb", ["loglik", "gamma_tk"], _LANES),                         # fb_kernel, inline
+    ("forward", ["loglik"], _LANES),                                # fb_kernel forward only, inline
+    ("alpha-beta", ["alpha_tk", "beta_tk"], _LANES),                # fb_kernel FB_FULL, inline
+    ("log-space", ["unalpha_tk"], _LANES),                          # fb_log_kernel: check pass
+    ("viterbi", ["zstar_t", "logp_zstar"], _LANES),                 # viterbi_kernel, inline
+    ("viterbi-states", ["zstar_t"], _abi.FLAG_VIT_STATES),          # viterbi_sp_kernel: check pass
+    ("two", C2_PARS, _LANES | _abi.FLAG_VFB_OFF),                   # both inline, two streams
+    ("split", C2_PARS, _LANES | _abi.FLAG_FB_SPLIT),                # forward launch inline
+    ("fused", C2_PARS, _LANES | _abi.FLAG_FUSED),                   # fbv_kernel: check pass
+    ("scan", ["loglik", "gamma_tk"], _abi.FLAG_SCAN_FORCE),         # T-scan: check pass
+]
+
+
+@pytest.mark.parametrize("outs,flags", [s[1:] for s in SCHEDULES], ids=[s[0] for s in SCHEDULES])
+def test_multinom_schedules_ragged(engine, oracle, outs, flags):
+    """Every schedule of the hmm-multinom request flags the same series: the sweeps
+    that read x over whole series check it inline (fb_sweep, viterbi_block, the phased
+    sweep), the others leave it to data_check_kernel.  Ragged lengths put violations
+    in a wave's full chunks, in its partial chunks, and in the padding past a
+    series' own length (not a violation)."""
+    N, T = 300, 203
+    data, draws = synth.hmm_multinom(N=N, S=N, T=T, K=4, L=9, seed=11)
+    rng = np.random.default_rng(5)
+    Tn = rng.integers(150, T + 1, size=N).astype(np.int32)
+    Tn[17] = 161
+    Tn[29] = 170
+    data = dict(data, T=Tn)
+    bad = dict(data, T=Tn.copy())
+    bad["T"][60] = T + 1                          # length past T_max
+    bad = _corrupt(bad, "x", 5, 3, 10)            # a full chunk (every lane's steps valid)
+    bad = _corrupt(bad, "x", 17, 160, 0)          # the series' last step (a partial chunk)
+    bad = _corrupt(bad, "x", 29, 170, 0)          # t = T[29]: padding, not a violation
+    bad = _corrupt(bad, "x", 41, 100, -3)
+    bad = _corrupt(bad, "x", 299, 149, 12)        # the last pair (the final wave's padded lanes)
+    _run(engine, oracle, "hmm-multinom", data, bad, draws, outs, [5, 17, 41, 60, 299], pairing="zip", flags=flags)

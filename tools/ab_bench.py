@@ -46,7 +46,12 @@ def main():
             envs[name] = dict(kv.split("=", 1) for kv in ev.split(","))
         libs[name] = hhmm_amd.load_library(path)
     x, draws = bench.make_batch(a.pairs, a.T, 9000, dev)
-    runs = {n: bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev) for n, lib in libs.items()}
+    # one set of output and workspace buffers for every variant: separate
+    # allocations measured up to 20% apart for the SAME library (r05g: a copy of
+    # the first-loaded build timed 6.79 vs 8.34 ms on fb_kernel)
+    runs = {}
+    for n, lib in libs.items():
+        runs[n] = bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev, share=next(iter(runs.values()), None))
     times = {n: {"fb": [], "vit": [], "pair": [], "step": [], "split": []} for n in runs}
     s0 = torch.cuda.current_stream()
     s1 = torch.cuda.Stream()
