@@ -9,17 +9,23 @@
  * reproducible at all), so instead of the correctly rounded hhmm_cr_exp /
  * hhmm_cr_log (table lookups, a rounding test, a rarely taken accurate phase)
  * the contract uses these: a fixed sequence of IEEE-754 operations -- +, -, *,
- * /, explicit fma, rint, bit moves -- each exactly rounded in round-to-nearest
- * on both sides, so the result is bit-identical wherever it is evaluated.  No
- * table, no branch (selects only), about 25 (exp) / 35 (log) instructions.
- * Accuracy: a few ulp (well inside the 1e-9 tolerance of the float outputs
- * computed from them).
+ * /, explicit fma, rint, bit moves, one read of a fixed table -- each exactly
+ * rounded in round-to-nearest on both sides, so the result is bit-identical
+ * wherever it is evaluated.  No branch (selects only), about 20 (exp) / 35
+ * (log) instructions.  Accuracy: about one ulp (well inside the 1e-9
+ * tolerance of the float outputs computed from them).
  *
- *   hhmm_det_exp: x = k ln2 + r (Cody-Waite, ln2 in two parts, k*LN2_HI exact
- *     for |k| < 2^11), |r| <= ln2/2, exp(r) by the degree-13 Taylor sum in
- *     Horner form (truncation < 2^-57), times 2^k by ldexp (one rounding, also
- *     for subnormal results; the same double as two exact power-of-two
- *     factors).
+ *   hhmm_det_exp (round 5): x = k ln2/128 + r (ln2/128 in two parts, k*HI
+ *     exact for |k| < 2^18), |r| <= ln2/256; exp(r) - 1 = r (1 + r/2 + r^2/6 +
+ *     r^3/24 + r^4/120) by Horner (truncation < 2^-60); times 2^(j/128) from
+ *     the double-double table hhmm_exp2_tab of hhmm_crmath.h (j = k mod 128):
+ *     T.hi + fma(T.hi, q, T.lo), within ~0.51 ulp; times 2^(k >> 7) by ldexp
+ *     (one rounding, also for subnormal results).  5 fma instead of the
+ *     degree-13 Taylor sum over |r| <= ln2/2 of rounds 2-4 (35 %
+ *     of C4's VALU).  hhmm_det_exp_tab takes the table's address, so a
+ *     kernel can read a copy staged in LDS (a global read on each exp's
+ *     dependency chain cost more than the 8 fma it saves: C4 32.0 vs 30.0 ms,
+ *     profiles/r05c_ab_c4.log); the entries, and so the results, are the same.
  *   hhmm_det_log: x = 2^e m, m in [sqrt(1/2), sqrt(2)); s = (m - 1) / (m + 1),
  *     log m = 2 s + s^3 (2/3 + 2/5 s^2 + ... + 2/21 s^18) (truncation < 2^-60),
  *     + e ln2 (two parts).
@@ -30,7 +36,6 @@
 #pragma once
 #include <stdint.h>
 
-#define HHMM_DET_INV_LN2 0x1.71547652b82fep+0
 #define HHMM_DET_LN2_HI 0x1.62e42feep-1 /* 32 significant bits */
 #define HHMM_DET_LN2_LO 0x1.a39ef35793c76p-33
 #define HHMM_DET_SQRT2 0x1.6a09e667f3bcdp+0
@@ -63,36 +68,33 @@ HHMM_MATH_FN double hhmm_det_pow2(int k)
 #define HHMM_DET_K(c) (c)
 #endif
 
-HHMM_MATH_FN double hhmm_det_exp(double x)
+HHMM_MATH_FN double hhmm_det_exp_tab(double x, const hhmm_exp2_entry *tab)
 {
     /* clamp into [-746, 710]: below, exp rounds to 0; above, to +inf -- the
      * clamped argument still gives exactly that (fmax / fmin take a NaN to a
      * bound; NaN is selected at the end) */
     const double xc = __builtin_fmin(__builtin_fmax(x, -746.0), 710.0);
-    const double kd = __builtin_rint(xc * HHMM_DET_INV_LN2);
-    double r = __builtin_fma(-kd, HHMM_DET_LN2_HI, xc);
-    r = __builtin_fma(-kd, HHMM_DET_LN2_LO, r);
-    double p = 0x1.6124613a86d09p-33;
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.1eed8eff8d898p-29));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.ae64567f544e4p-26));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.27e4fb7789f5cp-22));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.71de3a556c734p-19));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.a01a01a01a01ap-16));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.a01a01a01a01ap-13));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.6c16c16c16c17p-10));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.1111111111111p-7));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.5555555555555p-5));
-    p = __builtin_fma(p, r, HHMM_DET_K(0x1.5555555555555p-3));
+    const double kd = __builtin_rint(xc * HHMM_EXP_INV_L2); /* 128 / ln2 */
+    double r = __builtin_fma(-kd, HHMM_EXP_L2_HI, xc);      /* exact: HI has 35 bits, |k| < 2^18 */
+    r = __builtin_fma(-kd, HHMM_EXP_L2_MID, r);
+    const int k = (int)kd;
+    double p = 0x1.1111111111111p-7;                           /* 1/120 */
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.5555555555555p-5)); /* 1/24 */
+    p = __builtin_fma(p, r, HHMM_DET_K(0x1.5555555555555p-3)); /* 1/6 */
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
-    p = __builtin_fma(p, r, 1.0);
-    /* times 2^k, k in [-1077, 1025], rounded once (also for subnormal
-     * results): ldexp is exactly RN(p 2^k) on both sides (v_ldexp_f64; C's
-     * ldexp), the same double as the two-factor product (p 2^k1) 2^k2 with
-     * k1 = k / 2 (exact, normal) of the contract's statement (DESIGN.md §5;
-     * tests/test_detmath.py restates that form and checks bit identity) */
-    const double y = __builtin_ldexp(p, (int)kd);
+    const double q = p * r; /* exp(r) - 1 */
+    const hhmm_exp2_entry t = tab[k & 127]; /* 2^(j/128), double-double */
+    const double y0 = t.hi + __builtin_fma(t.hi, q, t.lo);
+    /* times 2^(k >> 7) (floor division), rounded once: ldexp is exactly
+     * RN(y0 2^m) on both sides (v_ldexp_f64; C's ldexp) */
+    const double y = __builtin_ldexp(y0, k >> 7);
     return x != x ? x + x : y;
+}
+
+HHMM_MATH_FN double hhmm_det_exp(double x)
+{
+    return hhmm_det_exp_tab(x, hhmm_exp2_tab);
 }
 
 HHMM_MATH_FN double hhmm_det_log(double x)

@@ -306,7 +306,7 @@ struct Em {
  * filter the draws come from is bit-reproducible by the oracle). */
 template <int MODEL, int K, bool DETEXP = false>
 __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const double2 *slab, int L,
-                                          const Obs &o, Em<K> &em)
+                                          const Obs &o, Em<K> &em, const hhmm_exp2_entry *etab = hhmm_exp2_tab)
 {
     if constexpr (ModelTraits<MODEL>::kGauss) {
         double lp[K];
@@ -318,7 +318,7 @@ __device__ __forceinline__ void emit_prob(const PairParams<MODEL, K> &pp, const 
         }
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            em.e[j] = DETEXP ? hhmm_det_exp(lp[j] - m) : exp(lp[j] - m);
+            em.e[j] = DETEXP ? hhmm_det_exp_tab(lp[j] - m, etab) : exp(lp[j] - m);
         em.m = m;
     } else {
         read_table<K>(slab, o.x, L, em.e);
@@ -771,6 +771,7 @@ struct FbLane {
     int64_t Qs;  /* checkpoint row stride */
     bool noinit = false; /* step 0 is not the series' first (a segment window's chunk 0) */
     int64_t n = 0;       /* the series (fb_block: the inline data check's flag) */
+    const hhmm_exp2_entry *etab = hhmm_exp2_tab; /* DETEXP: the LDS copy (fb_kernel) */
 };
 
 /* One forward chunk [t0, t0+C).  FULLC: every lane of the wave has all C
@@ -786,7 +787,7 @@ __device__ __forceinline__ void fwd_chunk(const DevArgs &a, const FbLane<MODEL, 
         const int t = t0 + u;
         Em<K> enx;
         emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, (u + 1 < C) ? cur[u + 1 < C ? u + 1 : 0] : nxt0,
-                                           enx);
+                                           enx, ln.etab);
         if (FULLC || t < ln.Tp) {
             if (u == 0 && c == 0 && !ln.noinit) {
                 fwd_init<MODEL, K>(al, ln.pp, ecur, cur[0], lsc, ex);
@@ -871,11 +872,11 @@ __device__ __forceinline__ void bwd_chunk(const DevArgs &a, const FbLane<MODEL, 
         double lsacc = 0.0;
         int exb = 0;
         Em<K> ecur;
-        emit_prob<MODEL, K, DETEXP>(ln.pp, ln.slab, ln.L, cur[1 < C ? 1 : 0], ecur);
+        emit_prob<MODEL, K, DETEXP>(ln.pp, ln.slab, ln.L, cur[1 < C ? 1 : 0], ecur, ln.etab);
 #pragma unroll
         for (int u = 1; u < C; ++u) {
             Em<K> enx;
-            emit_prob<MODEL, K, DETEXP>(ln.pp, ln.slab, ln.L, cur[u + 1 < C ? u + 1 : u], enx);
+            emit_prob<MODEL, K, DETEXP>(ln.pp, ln.slab, ln.L, cur[u + 1 < C ? u + 1 : u], enx, ln.etab);
             if (FULLC || t0 + u < ln.Tp) {
                 lsacc += ecur.m;
                 fwd_step_to<MODEL, K>(abuf[u - 1], abuf[u], ln.pp, ecur.e, cur[u], exb);
@@ -1072,7 +1073,7 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     for (int i = 0; i < D; ++i)
         load_chunk<MODEL, C, AUX>(grp[i], sp, (cb + i) * C);
     Em<K> ecur;
-    emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, grp[0][0], ecur);
+    emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, grp[0][0], ecur, ln.etab);
     /* whole-series sweeps over x alone check it inline (xcheck_acc) */
     constexpr bool XCHK = !SCAN && !AUX && ModelTraits<MODEL>::kDiscrete && HHMM_INLINE_XCHECK;
     uint32_t xm = 0;
@@ -1199,7 +1200,7 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
 /* One wave of the forward-backward: pairs [64 gwave, 64 gwave + 64) (gwave =
  * block * waves per block + wave in fb_kernel). */
 template <int MODEL, int K, int MODE, int PH>
-__device__ __forceinline__ void fb_block(const DevArgs &a, int64_t gwave)
+__device__ __forceinline__ void fb_block(const DevArgs &a, int64_t gwave, const hhmm_exp2_entry *etab = hhmm_exp2_tab)
 {
     constexpr bool AUX = ModelTraits<MODEL>::kAux;
     HIP_DYNAMIC_SHARED(double2, lds)
@@ -1222,6 +1223,7 @@ __device__ __forceinline__ void fb_block(const DevArgs &a, int64_t gwave)
     ln.q = p;
     ln.Qs = a.P;
     ln.slab = lds + (size_t)wave * a.L * KP * 64 + lane;
+    ln.etab = etab;
     load_params<MODEL, K, false>(ln.pp, a, d);
     if constexpr (ModelTraits<MODEL>::kDiscrete)
         ln.pp.skip_ok &= fill_table<K, false>(lds + (size_t)wave * a.L * KP * 64 + lane, a, d);
@@ -1268,10 +1270,25 @@ __global__ void __launch_bounds__(64) fb_dense_kernel(const DevArgs a)
     }
 }
 
+/* fb_exp2_lds: the FFBS contract's Gaussian exps (DETEXP) read their 2^(j/128)
+ * table from an LDS copy -- the Gaussian models have no emission slab, so the
+ * copy sits at the start of the launch's LDS (launch_fb sizes it) */
+template <int MODEL, int MODE>
+constexpr bool fb_exp2_lds() { return ModelTraits<MODEL>::kGauss && fb_ffbs(MODE); }
+constexpr size_t kExp2TabBytes = 128 * sizeof(hhmm_exp2_entry);
+
 template <int MODEL, int K, int MODE, int PH = FB_PH_BOTH>
 __global__ void __launch_bounds__(kBlock) fb_kernel(const DevArgs a)
 {
-    fb_block<MODEL, K, MODE, PH>(a, (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const hhmm_exp2_entry *etab = hhmm_exp2_tab;
+    if constexpr (fb_exp2_lds<MODEL, MODE>()) {
+        HIP_DYNAMIC_SHARED(hhmm_exp2_entry, t)
+        for (int i = threadIdx.x; i < 128; i += blockDim.x)
+            t[i] = hhmm_exp2_tab[i];
+        __syncthreads();
+        etab = t;
+    }
+    fb_block<MODEL, K, MODE, PH>(a, (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), etab);
 }
 
 /* ------------------------------------------------------------------ */
@@ -3289,6 +3306,8 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
     s.lds = std::max(s.lds, std::min(lds_floor("HHMM_PROBE_FB_LDS_KB"), kLdsLimit));
     const uint32_t extra = HHMM_OUT_ALPHA | HHMM_OUT_UNALPHA | HHMM_OUT_BETA | HHMM_OUT_UNBETA | HHMM_OUT_UNGAMMA;
     const bool ffbs = (a.outputs & HHMM_OUT_FFBS) != 0;
+    if (ModelTraits<MODEL>::kGauss && ffbs) /* fb_exp2_lds's table copy */
+        s.lds = std::max(s.lds, kExp2TabBytes);
     constexpr bool xchk = HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
     /* every fb_kernel below sweeps x forward over whole series (fb_sweep's inline check) */
     t_data_checked_inline |= xchk && (ffbs || !(a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)));

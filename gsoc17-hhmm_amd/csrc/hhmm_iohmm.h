@@ -41,8 +41,9 @@
  *            bit-exact with the oracle; the filter's e_t stays libm;
  *   IO_DET   FFBS draws requested: the same transcendentals, plus the
  *            filter's e_t, are the deterministic hhmm_det_exp / hhmm_det_log
- *            of the FFBS contract (cheap, table-free, and
- *            bit-identical in the oracle).
+ *            of the FFBS contract (cheap, no rounding test,
+ *            bit-identical in the oracle; the exp's table read from an LDS
+ *            copy, io_stage_exp2).
  * A request with both Viterbi and FFBS outputs runs an IO_CR sweep and an
  * IO_DET sweep (FFBS only).  log A_t is evaluated only when the Viterbi or the
  * logA_ij output consumes it.
@@ -62,13 +63,15 @@ enum IoFam { IO_REG = 0, IO_MIX = 1 };
 
 enum IoMath { IO_LIBM = 0, IO_CR = 1, IO_DET = 2 };
 
+/* tab: the FFBS contract's 2^(j/128) table (IO_DET; hhmm_det_exp_tab) -- the
+ * sweeps pass their LDS copy, staged by io_stage_exp2 */
 template <int MATH>
-__device__ __forceinline__ double io_exp(double x)
+__device__ __forceinline__ double io_exp(double x, const hhmm_exp2_entry *tab = hhmm_exp2_tab)
 {
     if constexpr (MATH == IO_CR)
         return dev_cr_exp(x);
     else if constexpr (MATH == IO_DET)
-        return hhmm_det_exp(x);
+        return hhmm_det_exp_tab(x, tab);
     else
         return exp(x);
 }
@@ -81,6 +84,25 @@ __device__ __forceinline__ double io_log(double x)
         return hhmm_det_log(x);
     else
         return log(x);
+}
+
+/* IO_DET: copy the FFBS contract exp's 2^(j/128) table (2 KB) to `dst` in LDS
+ * and return it; a read of the global table would sit on the dependency chain
+ * of every exp (C4's lane sweep 70.9 against 62.0 ms with the table form reading
+ * it from global memory, profiles/r05i_ab_c4.log).  Other modes: the global
+ * table, unread.  Every thread of the block calls it (a barrier). */
+template <int MATH>
+__device__ __forceinline__ const hhmm_exp2_entry *io_stage_exp2(void *dst)
+{
+    if constexpr (MATH == IO_DET) {
+        hhmm_exp2_entry *t = reinterpret_cast<hhmm_exp2_entry *>(dst);
+        for (int i = threadIdx.x; i < 128; i += blockDim.x)
+            t[i] = hhmm_exp2_tab[i];
+        __syncthreads();
+        return t;
+    } else {
+        return hhmm_exp2_tab;
+    }
 }
 
 /* row_vector * vector as Eigen evaluates it on x86-64 SSE2 (oracle stan_dot):
@@ -146,7 +168,8 @@ __device__ __forceinline__ int stan_categorical(const double (&th)[NMAX], int n,
 /* Stan Math softmax(v): theta = exp(v - max v); theta / sequential sum.
  * num: the numerators exp(v - max v) (the FFBS contract's weights). */
 template <int K, int MATH>
-__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K], double (&num)[K], double &den)
+__device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[K], double (&num)[K], double &den,
+                                             const hhmm_exp2_entry *tab = hhmm_exp2_tab)
 {
     double mx = v[0];
 #pragma unroll
@@ -156,7 +179,7 @@ __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[
     double sum = 0.0;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        num[i] = io_exp<MATH>(v[i] - mx);
+        num[i] = io_exp<MATH>(v[i] - mx, tab);
         sum += num[i];
     }
 #pragma unroll
@@ -308,7 +331,7 @@ struct IoStep {
 template <int FAM, int K, int MMAX, int MATH>
 __device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, const double2 *slab, int L, int M,
                                             double x, const double (&u)[MMAX], double (&o)[K],
-                                            const double2 *wb = nullptr)
+                                            const double2 *wb = nullptr, const hhmm_exp2_entry *tab = hhmm_exp2_tab)
 {
     if constexpr (FAM == IO_REG) {
 #pragma unroll
@@ -342,7 +365,7 @@ __device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, co
 #pragma unroll
             for (int l = 0; l < kIoLmax; ++l)
                 if (l < L && acc[l] != dev_ninf())
-                    sum += io_exp<MATH>(acc[l] - mx);
+                    sum += io_exp<MATH>(acc[l] - mx, tab);
             o[j] = mx + io_log<MATH>(sum);
         }
     }
@@ -354,7 +377,8 @@ __device__ __forceinline__ void io_emission(const IoParams<FAM, K, MMAX> &pp, co
  * log_sum_exp, m = fmax over j of max_l acc(j,l) (0 if -inf) -- exp(oblik(j) - m)
  * with K*L exps and no log (oracle ffbs_iohmm_emission). */
 template <int K, int MATH>
-__device__ __forceinline__ void io_mix_factor(const double2 *slab, int L, double x, double (&e)[K], double &m)
+__device__ __forceinline__ void io_mix_factor(const double2 *slab, int L, double x, double (&e)[K], double &m,
+                                              const hhmm_exp2_entry *tab = hhmm_exp2_tab)
 {
     double acc[K][kIoLmax];
     double mm = dev_ninf();
@@ -384,7 +408,7 @@ __device__ __forceinline__ void io_mix_factor(const double2 *slab, int L, double
 #pragma unroll
         for (int l = 0; l < kIoLmax; ++l)
             if (l < L && acc[j][l] != dev_ninf())
-                sum += io_exp<MATH>(acc[j][l] - mm);
+                sum += io_exp<MATH>(acc[j][l] - mm, tab);
         e[j] = sum;
     }
     m = mm;
@@ -394,7 +418,8 @@ __device__ __forceinline__ void io_mix_factor(const double2 *slab, int L, double
  * (iohmm-reg.stan:40-49; iohmm-mix.stan:42-51, :69; iohmm-hmix.stan:36-48). */
 template <int FAM, int K, int MMAX, int MATH>
 __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, int M, const double (&u)[MMAX],
-                                              IoStep<K> &st, bool need_lA, const double2 *wb = nullptr)
+                                              IoStep<K> &st, bool need_lA, const double2 *wb = nullptr,
+                                              const hhmm_exp2_entry *tab = hhmm_exp2_tab)
 {
     double v[K];
 #pragma unroll
@@ -410,7 +435,7 @@ __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, 
             return;
         }
     }
-    stan_softmax<K, MATH>(v, st.A, st.th, st.den);
+    stan_softmax<K, MATH>(v, st.A, st.th, st.den, tab);
     if (need_lA) {
 #pragma unroll
         for (int j = 0; j < K; ++j)
@@ -500,6 +525,9 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                     make_double2(io_log<MATH>(a.lambda_kl[ix]), HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(s));
             }
     }
+    /* IO_DET: the contract exp's table in LDS, after the waves' slabs */
+    const hhmm_exp2_entry *etab = io_stage_exp2<MATH>(
+        lds + (size_t)(blockDim.x >> 6) * (FAM == IO_MIX ? K * L * 2 * 64 : (io_wb_lds<FAM>() ? K * MMAX * 64 : 0)));
     const int Tw_min = wave_min(Tp);
     const int Tw_max = wave_max(Tp);
 
@@ -529,7 +557,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
              * where an output reads it */
             constexpr bool MIXF = (FAM == IO_MIX && MATH != IO_CR);
             if (!MIXF || (out & (HHMM_OUT_OBLIK_TK | HHMM_OUT_UNALPHA)))
-                io_emission<FAM, K, MMAX, MATH>(pp, slab, L, M, x, u, st.o, wb);
+                io_emission<FAM, K, MMAX, MATH>(pp, slab, L, M, x, u, st.o, wb, etab);
             if (t == 0) {
                 /* A_ij[1] = p_1k (filler, iohmm-reg.stan:41-42); logA_ij[1] = log(p_1k) (iohmm-hmix.stan:40) */
 #pragma unroll
@@ -539,7 +567,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
                 }
                 st.den = 1.0;
             } else {
-                io_transition<FAM, K, MMAX, MATH>(pp, M, u, st, need_lA, wb);
+                io_transition<FAM, K, MMAX, MATH>(pp, M, u, st, need_lA, wb, etab);
             }
             if ((out & HHMM_OUT_OBLIK_TK) && a.oblik)
                 store_tk<K>(a.oblik, a, p, t, st.o);
@@ -550,7 +578,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
             double m = 0.0;
             double e[K];
             if constexpr (MIXF) {
-                io_mix_factor<K, MATH>(slab, L, x, e, m);
+                io_mix_factor<K, MATH>(slab, L, x, e, m, etab);
             } else {
             m = st.o[0];
 #pragma unroll
@@ -561,7 +589,7 @@ __device__ __forceinline__ void iohmm_sweep(const DevArgs &a)
             if constexpr (MATH == IO_DET) { /* the FFBS contract's e_t */
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    e[k] = hhmm_det_exp(st.o[k] - m);
+                    e[k] = hhmm_det_exp_tab(st.o[k] - m, etab);
             } else {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -844,6 +872,12 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
             }
         }
     }
+    /* the FFBS contract's exp reads its 2^(j/128) table from a copy in LDS
+     * after the columns (hhmm_det_exp_tab): a global read would sit on the
+     * dependency chain of each of the step's exps */
+    const hhmm_exp2_entry *etab =
+        io_stage_exp2<MATH>(lds + (FAM == IO_MIX ? (blockDim.x >> 6) * (size_t)(2 * LM * 64) : 0));
+    auto sexp = [&](double v) -> double { return io_exp<MATH>(v, etab); };
     const int Tw_max = wave_max(Tp);
 
     double f[K];
@@ -903,7 +937,7 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
                 /* the numerators exp(v - max) only: the FFBS weights take them as
                  * they are (cat normalises), and the filter carries the sum in a
                  * separate log scale (psum, pex) instead of dividing */
-                quad_gather<K>(io_exp<MATH>(v - mx), AA);
+                quad_gather<K>(sexp(v - mx), AA);
                 double sum = 0.0;
 #pragma unroll
                 for (int i = 0; i < K; ++i)
@@ -923,13 +957,13 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
                 m = 0.0;
             double ej;
             if constexpr (FAM == IO_REG) {
-                ej = MATH == IO_DET ? hhmm_det_exp(o - m) : exp(o - m);
+                ej = MATH == IO_DET ? sexp(o - m) : exp(o - m);
             } else {
                 ej = 0.0;
 #pragma unroll
                 for (int l = 0; l < LM; ++l)
                     if (l < L && acc[l] != dev_ninf())
-                        ej += io_exp<MATH>(acc[l] - m);
+                        ej += sexp(acc[l] - m);
             }
             double ee[K];
             quad_gather<K>(ej, ee);
@@ -1040,19 +1074,20 @@ static hhmm_status launch_io5(const DevArgs &a, hipStream_t st)
 {
     const size_t per_wave = (FAM == IO_MIX) ? (size_t)K * a.L * 2 * 64 * sizeof(double2)
                                             : (io_wb_lds<FAM>() ? (size_t)K * MMAX * 64 * sizeof(double2) : 0);
+    const size_t tab = MATH == IO_DET ? 128 * sizeof(hhmm_exp2_entry) : 0; /* io_stage_exp2's copy */
     int waves = 4;
-    while (per_wave > 0 && waves > 1 && per_wave * waves > kLdsLimit)
+    while (per_wave > 0 && waves > 1 && per_wave * waves + tab > kLdsLimit)
         --waves;
-    if (per_wave * waves > kLdsLimit) {
+    if (per_wave * waves + tab > kLdsLimit) {
         set_error("IOHMM mixture table K*L = %d*%d does not fit in LDS", K, a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
     const int threads = 64 * waves;
     const dim3 grid((unsigned)((a.P + threads - 1) / threads));
     if constexpr (FAM == IO_REG)
-        hipLaunchKernelGGL((iohmm_reg_kernel<K, MMAX, MATH, HOT>), grid, dim3(threads), per_wave * waves, st, a);
+        hipLaunchKernelGGL((iohmm_reg_kernel<K, MMAX, MATH, HOT>), grid, dim3(threads), per_wave * waves + tab, st, a);
     else
-        hipLaunchKernelGGL((iohmm_mix_kernel<K, MMAX, MATH, HOT>), grid, dim3(threads), per_wave * waves, st, a);
+        hipLaunchKernelGGL((iohmm_mix_kernel<K, MMAX, MATH, HOT>), grid, dim3(threads), per_wave * waves + tab, st, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error("iohmm kernel launch: %s", hipGetErrorString(e));
@@ -1078,9 +1113,10 @@ static hhmm_status launch_io_sp(const DevArgs &a, hipStream_t st)
     const int64_t lanes = 4 * a.P;
     const dim3 grid((unsigned)((lanes + kBlock - 1) / kBlock));
     /* the mixture tables of a lane's state sit in registers: L <= 4 or <= 8 */
-    const size_t lds = (FAM == IO_MIX) ? (size_t)(kBlock / 64) * 2 * (a.L <= 4 ? 4 : kIoLmax) * 64 * sizeof(double2) : 0;
+    const size_t tab = MATH == IO_DET ? 128 * sizeof(hhmm_exp2_entry) : 0; /* hhmm_det_exp_tab's copy */
+    const size_t lds = ((FAM == IO_MIX) ? (size_t)(kBlock / 64) * 2 * (a.L <= 4 ? 4 : kIoLmax) * 64 * sizeof(double2) : 0) + tab;
     if (FAM == IO_REG)
-        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 1>), grid, dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 1>), grid, dim3(kBlock), tab, st, a);
     else if (a.L <= 4)
         hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 4>), grid, dim3(kBlock), lds, st, a);
     else

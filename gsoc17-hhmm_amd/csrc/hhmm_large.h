@@ -49,10 +49,16 @@ constexpr int kLBack = 16;  /* backtrack steps per back-pointer chunk */
 /* The filters renormalise (a group max, an exact power of two) every kLRenorm
  * steps, not every step: the group max is a five-level reduction on the
  * step's dependency chain, and between renormalisations the vectors shrink by
- * the per-step factor only (emission x transition mass, ~1e-4 over four
- * steps), far above the subnormal range.  A multiple-of-kLRenorm step (every
- * checkpoint step) is always renormalised. */
-constexpr int kLRenorm = 4;
+ * the per-step factor only (at least b >= 2^-39 per step below, so >= 2^-312
+ * over eight steps), far above the subnormal range; they grow by at most K per
+ * step.  A multiple-of-kLRenorm step (every checkpoint step: kLChunk is a
+ * multiple) is always renormalised.  Build knob HHMM_LK_RENORM (round 5: 8;
+ * rounds 3-4: 4). */
+#ifndef HHMM_LK_RENORM
+#define HHMM_LK_RENORM 8
+#endif
+constexpr int kLRenorm = HHMM_LK_RENORM;
+static_assert(kLChunk % kLRenorm == 0, "checkpoint steps are renormalisation steps");
 /* The cadence is taken only where the pair's parameters bound the shrink:
  * b = phi_min * min(min_i rowmax_i(A), min_i colmax_i(A)) >= 2^-39 (the lane
  * kernels' renorm_sparse_safe argument, hhmm_hmm.h).  Gaussian emissions have
@@ -149,6 +155,7 @@ struct LkLane {
     double mu, isig, c0, lsig; /* gauss, state j */
     double *xch;     /* this pair's LDS exchange slots: 2 x G doubles */
     const double *tab; /* multinomial: this pair's [L][G] emission table */
+    const hhmm_exp2_entry *etab = hhmm_exp2_tab; /* lk_ffbs_kernel (Gaussian): the det exp's LDS copy */
     bool dense;        /* wave-uniform: renormalise every step (kLRenormSafeBound) */
 };
 
@@ -555,7 +562,9 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
                 const double ug = av * be;
                 const double sg = grp_sum<G>(ug);
                 if (sg > 0x1p-960) {
-                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug / sg);
+                    /* times the refined reciprocal (fast_rcp: within an ulp; gamma
+                     * is a tolerance output) instead of an IEEE division */
+                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug * fast_rcp(sg));
                 } else {
                     const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
                     const double un = (av / sa) * (be / sb);
@@ -797,7 +806,7 @@ __device__ __forceinline__ double lkf_emit(const LkLane<MODEL, G, KM> &ln, int x
     if constexpr (LkTraits<MODEL>::kGauss) {
         const double lp = ln.on ? lk_lpdf<MODEL, G, KM>(ln, xr) : dev_ninf();
         const double m = grp_max<G>(lp);
-        return ln.on ? hhmm_det_exp(lp - m) : 0.0;
+        return ln.on ? hhmm_det_exp_tab(lp - m, ln.etab) : 0.0;
     } else {
         const int xc = min(max(x, 1), ln.L);
         return ln.on ? ln.tab[(xc - 1) * G + ln.j] : 0.0;
@@ -810,6 +819,15 @@ __global__ void __launch_bounds__(kBlock) lk_ffbs_kernel(const DevArgs a)
     HIP_DYNAMIC_SHARED(double, lds)
     LkLane<MODEL, G, KM> ln;
     lk_setup<MODEL, G, KM>(ln, a, lds, false, lk_group<G>(a.P));
+    if constexpr (LkTraits<MODEL>::kGauss) {
+        /* the FFBS contract exp's 2^(j/128) table after the exchange slots (no
+         * emission tables here; run_large_model sizes the launch for it) */
+        hhmm_exp2_entry *t = reinterpret_cast<hhmm_exp2_entry *>(lds + (size_t)(blockDim.x / G) * 2 * G);
+        for (int i = threadIdx.x; i < 128; i += blockDim.x)
+            t[i] = hhmm_exp2_tab[i];
+        __syncthreads();
+        ln.etab = t;
+    }
     const int Tp = ln.Tp, K = ln.K;
     double w[KM];
     int slot = 0;

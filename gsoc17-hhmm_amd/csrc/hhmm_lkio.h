@@ -119,6 +119,9 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
             mix[(l * 4 + 3) * G + j] = HHMM_NEG_LOG_SQRT_TWO_PI - io_log<MATH>(s);
         }
     }
+    /* IO_DET: the contract exp's table in LDS after the mixture rows (io_stage_exp2) */
+    const hhmm_exp2_entry *etab =
+        io_stage_exp2<MATH>(lds + (size_t)gpb * 3 * G + (FAM == IO_MIX ? (size_t)gpb * L * 4 * G : 0));
     __syncthreads();
 
     /* oblik_t(j): reg normal_lpdf(x | u' b_j, s_j) (iohmm-reg.stan:51-57); mix
@@ -147,7 +150,7 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
 #pragma unroll
             for (int l = 0; l < kIoLmax; ++l)
                 if (l < L && acc[l] != dev_ninf())
-                    sum += io_exp<MATH>(acc[l] - mx);
+                    sum += io_exp<MATH>(acc[l] - mx, etab);
             return mx + io_log<MATH>(sum);
         }
     };
@@ -192,7 +195,7 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
                     double m = grp_max<G>(o);
                     if (m == dev_ninf())
                         m = 0.0;
-                    e = on ? hhmm_det_exp(o - m) : 0.0;
+                    e = on ? hhmm_det_exp_tab(o - m, etab) : 0.0;
                 } else { /* io_mix_factor: the largest summand over every state and component */
                     double acc[kIoLmax];
                     double mx = dev_ninf();
@@ -214,7 +217,7 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
 #pragma unroll
                     for (int l = 0; l < kIoLmax; ++l)
                         if (l < L && acc[l] != dev_ninf())
-                            sum += hhmm_det_exp(acc[l] - mm);
+                            sum += hhmm_det_exp_tab(acc[l] - mm, etab);
                     e = on ? sum : 0.0;
                 }
                 if (t == 0) {
@@ -227,7 +230,7 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
                     for (int i = 1; i < KM; ++i)
                         if (i < K && vx[i] > mx)
                             mx = vx[i];
-                    const double th = on ? hhmm_det_exp(v - mx) : 0.0;
+                    const double th = on ? hhmm_det_exp_tab(v - mx, etab) : 0.0;
                     grp_exchange<G, KM>(xch, 1, j, vprev * th, vx);
                     const int z = lkio_cat<KM>(vx, K, uprev);
                     if (j == 0)
@@ -260,7 +263,7 @@ __global__ void __launch_bounds__(kBlock) lkio_kernel(const DevArgs a)
                 for (int i = 1; i < KM; ++i)
                     if (i < K && vx[i] > mx)
                         mx = vx[i];
-                const double num = on ? io_exp<MATH>(v - mx) : 0.0;
+                const double num = on ? io_exp<MATH>(v - mx, etab) : 0.0;
                 grp_exchange<G, KM>(xch, 1, j, num, vx);
                 double sum = 0.0;
 #pragma unroll
@@ -438,7 +441,8 @@ static hhmm_status launch_lkio_g(const DevArgs &a, hipStream_t st)
 {
     const int gpb = kBlock / G;
     const size_t lds = ((size_t)gpb * 3 * G + (FAM == IO_MIX ? (size_t)gpb * a.L * 4 * G : 0)) * sizeof(double);
-    if (lds > kLdsLimit) {
+    const size_t tab = 128 * sizeof(hhmm_exp2_entry); /* the IO_DET launch's io_stage_exp2 copy */
+    if (lds + tab > kLdsLimit) {
         set_error("large-K IOHMM: mixture table L = %d does not fit in LDS", a.L);
         return HHMM_ERR_UNSUPPORTED;
     }
@@ -446,7 +450,7 @@ static hhmm_status launch_lkio_g(const DevArgs &a, hipStream_t st)
     if (a.outputs & HHMM_OUT_FFBS) { /* the draws in their own sweep (the contract's arithmetic) */
         DevArgs f = a;
         f.outputs = HHMM_OUT_FFBS;
-        hipLaunchKernelGGL((lkio_kernel<FAM, G, KM, IO_DET>), grid, dim3(kBlock), lds, st, f);
+        hipLaunchKernelGGL((lkio_kernel<FAM, G, KM, IO_DET>), grid, dim3(kBlock), lds + tab, st, f);
     }
     DevArgs b = a;
     b.outputs &= ~HHMM_OUT_FFBS;

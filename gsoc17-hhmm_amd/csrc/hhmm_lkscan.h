@@ -78,6 +78,13 @@ __device__ __forceinline__ double lks_mfma4(double a, double b, double c)
 #define HHMM_LKS_TILES 2 /* build knob: 16-column tiles per wave (independent accumulator chains) */
 #endif
 constexpr int kLksTiles = HHMM_LKS_TILES;
+/* Build knob: steps between the chunk products' renormalisations where the
+ * pair's parameters bound the shrink (lks_prod_kernel); 1 = every step. */
+#ifndef HHMM_LKS_RENORM
+#define HHMM_LKS_RENORM 4
+#endif
+constexpr int kLksRenorm = HHMM_LKS_RENORM;
+static_assert(8 % kLksRenorm == 0, "the cadence divides the observation block kB = 8");
 
 template <int RT, int KSM, bool GS>
 __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
@@ -144,6 +151,34 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
         }
 #endif
     __syncthreads();
+    /* Renormalisation cadence: a column is renormalised (its max to [1/2, 1),
+     * an exact power of two) every kLksRenorm-th step where the pair bounds the
+     * per-step shrink of the max, b = phi_min * min(min_i rowmax_i(A),
+     * min_j colmax_j(A)) >= kLRenormSafeBound (lk_setup's test; the growth is at
+     * most K per step), else every step ("dense": Gaussian emissions, or a NaN /
+     * unsafe draw).  Power-of-two scalings are exact, and every column is
+     * renormalised after its last step, so M'_c and its exponents are the same
+     * bits at either cadence. */
+    bool dense = GS;
+    if constexpr (!GS) {
+        const int jr = lane < K ? lane : 0; /* lane = state: its phi column, A row and A column */
+        double emin = 1.0 / 0.0, rmax = 0.0, cmax = 0.0;
+        for (int l = 0; l < a.L; ++l)
+            emin = fmin(emin, tab[l * KR + jr]);
+        for (int i = 0; i < K; ++i) {
+            rmax = fmax(rmax, a.A_ij[d + S * ((int64_t)jr + (int64_t)K * i)]);
+            cmax = fmax(cmax, a.A_ij[d + S * ((int64_t)i + (int64_t)K * jr)]);
+        }
+        const double inf = 1.0 / 0.0;
+        double ge = lane < K ? emin : inf, gm = lane < K ? fmin(rmax, cmax) : inf;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            ge = fmin(ge, __shfl_xor(ge, o));
+            gm = fmin(gm, __shfl_xor(gm, o));
+        }
+        const bool bad = !(ge * gm >= kLRenormSafeBound) || (lane < K && !(emin * fmin(rmax, cmax) >= 0.0));
+        dense = __builtin_amdgcn_readfirstlane((int)(__ballot(bad) != 0)) != 0;
+    }
 
     /* this lane's column in each tile: (chunk c, initial state i); B operand
      * Q[u][kk] = row 4kk + (lane >> 4) of the column; gls: the chunk's Gaussian
@@ -275,19 +310,26 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
                         em[kk] = row[4 * kk];
                 }
                 double nv[KSM];
-                double mx = 0.0;
-#pragma unroll
-                for (int kk = 0; kk < KSM; ++kk) {
-                    nv[kk] = accv(u, kk) * em[kk];
-                    mx = fmax(mx, nv[kk]);
-                }
-                mx = fmax(mx, __shfl_xor(mx, 16));
-                mx = fmax(mx, __shfl_xor(mx, 32));
-                const int e2 = __builtin_amdgcn_frexp_exp(mx);
 #pragma unroll
                 for (int kk = 0; kk < KSM; ++kk)
-                    q[u][kk] = on ? ldexp(nv[kk], -e2) : q[u][kk];
-                ex[u] += on ? e2 : 0;
+                    nv[kk] = accv(u, kk) * em[kk];
+                if ((v % kLksRenorm) == kLksRenorm - 1 || dense) { /* v: compile-time; dense: wave-uniform */
+                    double mx = 0.0;
+#pragma unroll
+                    for (int kk = 0; kk < KSM; ++kk)
+                        mx = fmax(mx, nv[kk]);
+                    mx = fmax(mx, __shfl_xor(mx, 16));
+                    mx = fmax(mx, __shfl_xor(mx, 32));
+                    const int e2 = __builtin_amdgcn_frexp_exp(mx);
+#pragma unroll
+                    for (int kk = 0; kk < KSM; ++kk)
+                        q[u][kk] = on ? ldexp(nv[kk], -e2) : q[u][kk];
+                    ex[u] += on ? e2 : 0;
+                } else {
+#pragma unroll
+                    for (int kk = 0; kk < KSM; ++kk)
+                        q[u][kk] = on ? nv[kk] : q[u][kk];
+                }
             }
         }
 #pragma unroll
@@ -295,6 +337,24 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
 #pragma unroll
             for (int v = 0; v < kB; ++v)
                 xb[u][v] = xn[u][v];
+    }
+    /* the renormalisation after each column's last step (a no-op where that
+     * step was a renormalised one: its max is already in [1/2, 1)) */
+    if (!dense) {
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            double mx = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < KSM; ++kk)
+                mx = fmax(mx, q[u][kk]);
+            mx = fmax(mx, __shfl_xor(mx, 16));
+            mx = fmax(mx, __shfl_xor(mx, 32));
+            const int e2 = __builtin_amdgcn_frexp_exp(mx);
+#pragma unroll
+            for (int kk = 0; kk < KSM; ++kk)
+                q[u][kk] = ldexp(q[u][kk], -e2);
+            ex[u] += e2;
+        }
     }
     /* M'_c[i][j] (row i = this column, j = 4kk + (lane >> 4)) and the row
      * exponent (-inf: the filter died, the row is zero) */
@@ -995,7 +1055,9 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
          * first on the caller's stream */
         DevArgs f = a;
         f.outputs = HHMM_OUT_FFBS;
-        hipLaunchKernelGGL((lk_ffbs_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, f);
+        const size_t tab = discrete ? 0 : 128 * sizeof(hhmm_exp2_entry); /* lk_ffbs_kernel's det-exp table */
+        hipLaunchKernelGGL((lk_ffbs_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete) + tab, st,
+                           f);
         e = hipGetLastError();
     }
     const bool mfma_fb = lkm_ok(a);

@@ -33,7 +33,6 @@ _INV_LN2 = float.fromhex("0x1.71547652b82fep+0")
 _LN2_HI = float.fromhex("0x1.62e42feep-1")
 _LN2_LO = float.fromhex("0x1.a39ef35793c76p-33")
 _SQRT2 = float.fromhex("0x1.6a09e667f3bcdp+0")
-_EXP_C = [1.0 / math.factorial(n) for n in range(13, 1, -1)]  # 1/13! .. 1/2!, each correctly rounded
 _LOG_C = [2.0 / (2 * n + 1) for n in range(10, 0, -1)]       # 2/21 .. 2/3
 NEG_LOG_SQRT_TWO_PI = onp.NEG_LOG_SQRT_TWO_PI
 
@@ -46,21 +45,53 @@ def _f64(u):
     return struct.unpack("<d", struct.pack("<Q", u))[0]
 
 
+def _exp2_table():
+    """2^(j/128) as a double-double (hi = RN(v), lo = RN(v - hi)), from 60-digit decimals."""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 60
+    tab = []
+    for j in range(128):
+        v = Decimal(2) ** (Decimal(j) / Decimal(128))
+        hi = float(v)  # float(Decimal) is correctly rounded
+        tab.append((hi, float(v - Decimal(hi))))
+    return tab
+
+
+_EXP2 = _exp2_table()
+# hhmm_crlog_table.h: ln2/128 in parts (HI with 35 significant bits) and 128/ln2
+_L2_HI = float.fromhex("0x1.62e42fef80000p-8")
+_L2_MID = float.fromhex("0x1.1cf79abc80000p-43")
+_INV_L2 = float.fromhex("0x1.71547652b82fep+7")
+_EXP_P = [1.0 / 120, 1.0 / 24, 1.0 / 6, 0.5, 1.0]  # each correctly rounded
+
+
 def det_exp(x):
-    """k = rint(x / ln2), r = x - k ln2 (two fma), Taylor to r^13 (Horner, fma),
-    times 2^k1 * 2^k2 (k1 = k / 2 truncated)."""
+    """k = rint(x 128/ln2), r = x - k ln2/128 (two fma), q = r (1 + r/2 + ... + r^4/120)
+    (Horner, fma), 2^(j/128) (T.hi + fma(T.hi, q, T.lo)), times 2^(k >> 7) rounded once."""
     if math.isnan(x):
         return x + x
     xc = -746.0 if x < -746.0 else (710.0 if x > 710.0 else x)
-    kd = float(round(xc * _INV_LN2))  # round(): ties to even, as rint
-    r = fma(-kd, _LN2_HI, xc)
-    r = fma(-kd, _LN2_LO, r)
-    p = _EXP_C[0]
-    for c in _EXP_C[1:] + [1.0, 1.0]:
+    kd = float(round(xc * _INV_L2))  # round(): ties to even, as rint
+    r = fma(-kd, _L2_HI, xc)
+    r = fma(-kd, _L2_MID, r)
+    p = _EXP_P[0]
+    for c in _EXP_P[1:]:
         p = fma(p, r, c)
+    q = p * r
     k = int(kd)
-    k1 = int(k / 2)
-    return (p * 2.0 ** k1) * 2.0 ** (k - k1)
+    hi, lo = _EXP2[k & 127]
+    y0 = hi + fma(hi, q, lo)
+    m = k >> 7
+    # y0 2^m rounded once: exact scaling in the normal range; where the result is
+    # subnormal the exact rational y0 2^m is rounded by float() (correctly rounded
+    # int / int division), past the top it overflows to +inf
+    if m < -1000:
+        v = Fraction(y0) * Fraction(1, 2 ** -m)
+        return float(v.numerator / v.denominator) if v.numerator else 0.0
+    try:
+        return math.ldexp(y0, m)
+    except OverflowError:
+        return math.inf
 
 
 def det_log(x):
