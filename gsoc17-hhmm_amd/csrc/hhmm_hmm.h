@@ -683,7 +683,7 @@ __device__ __forceinline__ void emit_posteriors(const DevArgs &a, int64_t p, int
             ug[k] = al[k] * be[k];
         double sg = vsum<K>(ug);
         double r;
-        if (__builtin_expect(sg > 0x1p-960, 1)) {
+        if (__builtin_expect(sg > kGammaDirect, 1)) {
             r = fast_rcp(sg);
         } else {
             /* alpha and beta nearly disjoint (e.g. the Tayal masks of Q6 on a

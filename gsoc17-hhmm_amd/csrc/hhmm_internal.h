@@ -180,6 +180,15 @@ constexpr double kIoWeak = 0x1p-960;
 /* t = 0: f_0 = p .* e_0 keeps every component above 2^-1074, i.e. down to
  * 2^-834 (below the 1e-250 tolerance floor) of a max of at least 2^-240 */
 constexpr double kIoWeak0 = 0x1p-240;
+/* gamma = (alpha .* beta) * (1 / sum) straight from the scaled vectors while
+ * the sum sg exceeds kGammaDirect; below it the reference's normalised-vector
+ * form.  A product alpha_j beta_j = gamma_j sg that falls into the subnormal
+ * range is off by at most 2^-1075, i.e. gamma_j by 2^-1075 / sg < 2^-835 --
+ * under the 1e-250 absolute floor of the tolerance -- exactly when sg >
+ * 2^-240 (round 5; rounds 1-4 took 2^-960, which let gamma_j below ~2^-114
+ * of the sum flush: tests/test_gpu_large_k.py::test_gamma_only_large_K_disjoint_filters
+ * at lk_fb_kernel's 8-step renormalisation cadence). */
+constexpr double kGammaDirect = 0x1p-240;
 hhmm_status launch_iohmm_log(const DevArgs &a, hipStream_t stream);
 /* Fitted-output draws hatpi / hatz / hatl / hatx (hhmm_fitted.hip). */
 hhmm_status launch_fitted(const DevArgs &a, hipStream_t stream);

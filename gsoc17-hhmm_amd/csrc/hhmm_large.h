@@ -561,7 +561,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
                  * product underflows (group-uniform test) */
                 const double ug = av * be;
                 const double sg = grp_sum<G>(ug);
-                if (sg > 0x1p-960) {
+                if (sg > kGammaDirect) {
                     /* times the refined reciprocal (fast_rcp: within an ulp; gamma
                      * is a tolerance output) instead of an IEEE division */
                     lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug * fast_rcp(sg));

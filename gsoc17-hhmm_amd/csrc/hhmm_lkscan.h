@@ -691,7 +691,7 @@ __global__ void __launch_bounds__(64) lks_seg_summary_kernel(const DevArgs a)
  *   backward  chunk by chunk from the end: the chunk's alphas recomputed from
  *             its checkpoint into registers, then gamma_t = alpha .* beta / sum
  *             (the reference's normalised-vector formula where that sum is
- *             below 2^-960, as lk_fb_kernel) and the beta step.
+ *             below kGammaDirect, as lk_fb_kernel) and the beta step.
  * Outputs: loglik, gamma_tk (the hot profile); ragged T per series. ---- */
 constexpr int kLmChunk = 8;
 
@@ -905,7 +905,7 @@ __global__ void __launch_bounds__(256) lkm_fb_kernel(const DevArgs a)
             if (t >= Tw) /* wave-uniform */
                 continue;
             const bool on = t < Tn;
-            /* gamma_t = alpha .* beta / sum, the normalised-vector form below 2^-960 */
+            /* gamma_t = alpha .* beta / sum, the normalised-vector form below kGammaDirect */
             double ug[KSM], sg = 0.0;
 #pragma unroll
             for (int kk = 0; kk < KSM; ++kk) {
@@ -913,7 +913,7 @@ __global__ void __launch_bounds__(256) lkm_fb_kernel(const DevArgs a)
                 sg += ug[kk];
             }
             sg = colsum(sg);
-            const bool small = !(sg > 0x1p-960);
+            const bool small = !(sg > kGammaDirect);
             double rg = 1.0 / sg;
             if (__builtin_amdgcn_readfirstlane((int)(__ballot(small) != 0))) { /* rare, wave-uniform */
                 double sa = 0.0, sb = 0.0;
