@@ -85,9 +85,24 @@ constexpr int kLksTiles = HHMM_LKS_TILES;
 #endif
 constexpr int kLksRenorm = HHMM_LKS_RENORM;
 static_assert(8 % kLksRenorm == 0, "the cadence divides the observation block kB = 8");
+/* Build knob: blocks of steps that every column of the wave takes in full run
+ * without the per-column step predicates (lks_prod_kernel). */
+#ifndef HHMM_LKS_FULLBLK
+#define HHMM_LKS_FULLBLK 1
+#endif
 
+/* Build knob: cap lks_prod_kernel's registers for this many waves per SIMD
+ * (0: the compiler's choice). */
+#ifndef HHMM_LKS_WAVES
+#define HHMM_LKS_WAVES 0
+#endif
+#if HHMM_LKS_WAVES
+#define HHMM_LKS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(HHMM_LKS_WAVES)))
+#else
+#define HHMM_LKS_WAVES_ATTR
+#endif
 template <int RT, int KSM, bool GS>
-__global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
+__global__ void __launch_bounds__(256) HHMM_LKS_WAVES_ATTR lks_prod_kernel(const DevArgs a)
 {
     constexpr int TPW = kLksTiles;
     constexpr int KR = 16 * RT; /* padded rows of the emission table */
@@ -229,10 +244,19 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
 #pragma unroll
             for (int v = 0; v < kB; ++v)
                 xn[u][v] = ldx(u, s0 + kB + v);
+        /* a block in which every column of the wave takes all kB steps (the
+         * common case) runs without the per-column step predicates */
+        bool full = s0 + kB <= smax;
+#pragma unroll
+        for (int u = 0; u < TPW; ++u)
+            full &= (t0[u] + s0 >= 1 || a.seg_nofirst) && t0[u] + s0 + kB <= t1[u];
+        full = HHMM_LKS_FULLBLK && __builtin_amdgcn_readfirstlane((int)(__ballot(!full) == 0)) != 0;
+        auto block = [&](auto full_c) {
+        constexpr bool FULL = decltype(full_c)::value;
 #pragma unroll
         for (int v = 0; v < kB; ++v) {
             const int s = s0 + v;
-            if (s >= smax)
+            if (!FULL && s >= smax)
                 break;
             /* D = A^T Q for every tile (independent accumulators interleaved);
              * accv(u, kk): state 4kk + (lane >> 4) of the lane's column */
@@ -283,7 +307,7 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
                 /* t = 0 is the init (phase 2 applies p_1k .* phi), except in a
                  * segment window that starts inside the series: there every
                  * step is a transition */
-                const bool on = (t >= 1 || a.seg_nofirst) && t < t1[u];
+                const bool on = FULL || ((t >= 1 || a.seg_nofirst) && t < t1[u]);
                 double em[KSM];
                 if constexpr (GS) {
                     /* e_t(j) = exp(lpdf_j - m_t), m_t = max_j lpdf_j (emit_prob's
@@ -332,6 +356,11 @@ __global__ void __launch_bounds__(256) lks_prod_kernel(const DevArgs a)
                 }
             }
         }
+        };
+        if (full)
+            block(std::true_type{});
+        else
+            block(std::false_type{});
 #pragma unroll
         for (int u = 0; u < TPW; ++u)
 #pragma unroll
