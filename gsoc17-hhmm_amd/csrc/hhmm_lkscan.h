@@ -75,7 +75,7 @@ __device__ __forceinline__ double lks_mfma4(double a, double b, double c)
 /* Columns of M'^T per wave: TPW tiles of 16.  RT row tiles of 16 states, KSM
  * k-steps of 4 states (K <= 16: 1 / 4; K <= 24: 2 / 6; K <= 32: 2 / 8). */
 #ifndef HHMM_LKS_TILES
-#define HHMM_LKS_TILES 2 /* build knob: 16-column tiles per wave (independent accumulator chains) */
+#define HHMM_LKS_TILES 1 /* build knob: 16-column tiles per wave (independent accumulator chains) */
 #endif
 constexpr int kLksTiles = HHMM_LKS_TILES;
 /* Build knob: steps between the chunk products' renormalisations where the
@@ -91,18 +91,18 @@ static_assert(8 % kLksRenorm == 0, "the cadence divides the observation block kB
 #define HHMM_LKS_FULLBLK 1
 #endif
 
-/* Build knob: cap lks_prod_kernel's registers for this many waves per SIMD
- * (0: the compiler's choice). */
+/* Build knob: registers of lks_prod_kernel capped for this many waves per SIMD
+ * where the A operand leaves room (K <= 24, multinomial: 158 registers without
+ * a spill at one tile per wave; 0: the compiler's choice everywhere).  N2
+ * 188.6 against 195.8 ms with two tiles at two waves (profiles/r05l_ab_n2.log). */
 #ifndef HHMM_LKS_WAVES
-#define HHMM_LKS_WAVES 0
+#define HHMM_LKS_WAVES 3
 #endif
-#if HHMM_LKS_WAVES
-#define HHMM_LKS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(HHMM_LKS_WAVES)))
-#else
-#define HHMM_LKS_WAVES_ATTR
-#endif
+template <int KSM, bool GS>
+constexpr int lks_waves() { return (HHMM_LKS_WAVES > 0 && KSM <= 6 && !GS) ? HHMM_LKS_WAVES : 1; }
 template <int RT, int KSM, bool GS>
-__global__ void __launch_bounds__(256) HHMM_LKS_WAVES_ATTR lks_prod_kernel(const DevArgs a)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lks_waves<KSM, GS>())))
+lks_prod_kernel(const DevArgs a)
 {
     constexpr int TPW = kLksTiles;
     constexpr int KR = 16 * RT; /* padded rows of the emission table */
