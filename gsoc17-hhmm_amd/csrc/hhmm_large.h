@@ -422,6 +422,74 @@ __device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLa
         out[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
 }
 
+/* ---- split columns (lk_fb_kernel at G = 32, HHMM_LK_SPLIT) ----
+ * A pair takes the whole wave: lane (h, j) = 32 h + j holds state j and the
+ * half h of the K-vectors' index range, i in [h KH, h KH + KH), KH = KM / 2:
+ * half of the column and row of A, half of the exchanged vector, half of each
+ * dot product, the two halves' partial sums added across the wave halves by
+ * v_permlane32_swap.  The K^2 FMAs per pair-step are the same; the registers
+ * (col, row and the exchanged vector: 3 KM doubles -> 3 KH) drop below the
+ * three-waves-per-SIMD line, and each step's dependent chain is half as long.
+ * Each half keeps its own exchange slots and emission table (lk_setup's
+ * 32-lane groups), both halves hold every state's value, and only half 0
+ * stores. */
+#ifndef HHMM_LK_SPLIT
+#define HHMM_LK_SPLIT 1
+#endif
+template <int G>
+constexpr int lk_fb_split() { return (G == 32 && HHMM_LK_SPLIT) ? 2 : 1; }
+
+/* lower-half value + upper-half value, in every lane of the wave (the same bits
+ * in both halves) */
+__device__ __forceinline__ double half_sum(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    const double lower = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]));
+    const double upper = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]));
+    return lower + upper;
+}
+
+/* the other wave half's value (lane ^ 32) */
+__device__ __forceinline__ int half_other_i(int v)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
+}
+__device__ __forceinline__ double half_other(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = half_other_i((int)b), hi = half_other_i((int)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+/* lk_viterbi_kernel with split columns (HHMM_LK_VSPLIT): each half scans its
+ * half of the candidates i, and the halves' winners combine as the sequential
+ * strict-'>' scan would (the upper half's only if strictly greater) */
+#ifndef HHMM_LK_VSPLIT
+#define HHMM_LK_VSPLIT 1
+#endif
+template <int G>
+constexpr int lk_vit_split() { return (G == 32 && HHMM_LK_VSPLIT) ? 2 : 1; }
+
+/* the half h of the group's vector v through LDS slot `slot` (grp_exchange) */
+template <int G, int KH>
+__device__ __forceinline__ void grp_exchange_half(double *xch, int slot, int j, int h, double v, double (&w)[KH])
+{
+    static_assert(KH % 2 == 0, "16-byte reads");
+    double *s = xch + slot * G;
+    s[j] = v;
+    __asm__ __volatile__("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const double *sh = s + h * KH;
+#pragma unroll
+    for (int i = 0; i < KH; i += 2) {
+        const double2 q = *reinterpret_cast<const double2 *>(sh + i);
+        w[i] = q.x;
+        w[i + 1] = q.y;
+    }
+}
+
 /* Forward-backward: loglik, alpha, beta, ungamma, gamma.  One group sweeps a
  * whole series, or -- under the parallel scan over T (a.scan_cl > 0,
  * hhmm_lkscan.h) -- one T-chunk [t0, t1) of a pair (group q = pair + P *
@@ -433,11 +501,48 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     HIP_DYNAMIC_SHARED(double, lds)
     const bool scan = a.scan_cl > 0;
     const int64_t nq = scan ? a.P * (int64_t)a.scan_nc : a.P;
-    const int64_t q = lk_group<G>(nq);
+    constexpr int SP = lk_fb_split<G>(); /* split columns (see half_sum) */
+    constexpr int KH = KM / SP;
+    const int64_t q = lk_group<G * SP>(nq);
     const int64_t pq = scan ? q % a.P : q;
     const int cq = scan ? (int)(q / a.P) : 0;
     LkLane<MODEL, G, KM> ln;
     lk_setup<MODEL, G, KM>(ln, a, lds, false, pq);
+    const int h = SP == 2 ? (int)((threadIdx.x >> 5) & 1) : 0;
+    const bool st = ln.on && h == 0; /* the lane that stores state j's outputs */
+    double colh[KH], rowh[KH];
+#pragma unroll
+    for (int i = 0; i < KH; ++i) {
+        if constexpr (SP == 2) {
+            colh[i] = h ? ln.col[KH + i] : ln.col[i];
+            rowh[i] = h ? ln.row[KH + i] : ln.row[i];
+        } else {
+            colh[i] = ln.col[i];
+            rowh[i] = ln.row[i];
+        }
+    }
+    auto fwd = [&](const double (&wv)[KH], double e) -> double {
+        double d = lk_dot<KH>(wv, colh);
+        if constexpr (SP == 2)
+            d = half_sum(d);
+        return ln.on ? d * e : 0.0;
+    };
+    auto bwd = [&](const double (&wv)[KH]) -> double {
+        double d = lk_dot<KH>(wv, rowh);
+        if constexpr (SP == 2)
+            d = half_sum(d);
+        return ln.on ? d : 0.0;
+    };
+    auto xchg = [&](int sl, double v, double (&wv)[KH]) {
+        if constexpr (SP == 2)
+            grp_exchange_half<G, KH>(ln.xch, sl, ln.j, h, v, wv);
+        else
+            grp_exchange<G, KM>(ln.xch, sl, ln.j, v, wv);
+    };
+    auto put = [&](double *o, int t, double v) {
+        if (st && o)
+            o[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
+    };
     const uint32_t out = a.outputs;
     const bool need_bwd = (out & (HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) != 0;
     const bool gamma_only = (out & (HHMM_OUT_ALPHA | HHMM_OUT_BETA | HHMM_OUT_UNGAMMA | HHMM_OUT_GAMMA)) ==
@@ -447,7 +552,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     const int t1 = scan ? max(min(t0 + a.scan_cl, ln.Tp), t0) : ln.Tp;
     const int K = ln.K;
     const int64_t sbase = ((int64_t)pq * a.scan_nc + cq) * K + (ln.on ? ln.j : 0); /* scan vectors */
-    double w[KM];
+    double w[KH];
     int slot = 0;
     auto ckpt = [&](int c) -> double & { return a.ckpt[q + nq * ((int64_t)c * K + (ln.on ? ln.j : 0))]; };
 
@@ -487,21 +592,21 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
             al = grp_renorm<G>(al, ex);
         } else {
             const double e = lk_emit<MODEL, G, KM>(ln, x, xr, m);
-            grp_exchange<G, KM>(ln.xch, slot, ln.j, al, w);
+            xchg(slot, al, w);
             slot ^= 1;
             lsc += m;
-            al = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, e), ex, t, ln.dense);
+            al = grp_renorm_at<G>(fwd(w, e), ex, t, ln.dense);
         }
         if (!need_bwd) {
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
-                lk_put<MODEL, G, KM>(a.alpha, a, ln, t, al / grp_sum<G>(al));
-        } else if ((t - t0) % kLChunk == 0 && ln.on) {
+                put(a.alpha, t, al / grp_sum<G>(al));
+        } else if ((t - t0) % kLChunk == 0 && st) {
             ckpt((t - t0) / kLChunk) = al;
         }
     }
     if (!scan) {
         const double sa = grp_sum<G>(al); /* every lane takes part in the shuffle */
-        if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0)
+        if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0 && h == 0)
             a.loglik[ln.p] = log(sa) + (lsc + kLn2 * ex);
     }
     if (!need_bwd || t1 <= t0)
@@ -543,9 +648,9 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
         for (int u = 1; u < kLChunk; ++u) {
             abuf[u] = 0.0;
             if (tc + u < t1) { /* group-uniform */
-                grp_exchange<G, KM>(ln.xch, slot, ln.j, abuf[u - 1], w);
+                xchg(slot, abuf[u - 1], w);
                 slot ^= 1;
-                abuf[u] = grp_renorm_at<G>(lk_fwd<MODEL, G, KM>(ln, w, es[u]), exb, tc + u, ln.dense);
+                abuf[u] = grp_renorm_at<G>(fwd(w, es[u]), exb, tc + u, ln.dense);
             }
         }
 #pragma unroll
@@ -564,33 +669,33 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
                 if (sg > kGammaDirect) {
                     /* times the refined reciprocal (fast_rcp: within an ulp; gamma
                      * is a tolerance output) instead of an IEEE division */
-                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug * fast_rcp(sg));
+                    put(a.gamma, t, ug * fast_rcp(sg));
                 } else {
                     const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
                     const double un = (av / sa) * (be / sb);
-                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, un / grp_sum<G>(un));
+                    put(a.gamma, t, un / grp_sum<G>(un));
                 }
             } else {
             const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
             if ((out & HHMM_OUT_ALPHA) && a.alpha)
-                lk_put<MODEL, G, KM>(a.alpha, a, ln, t, av / sa);
+                put(a.alpha, t, av / sa);
             if ((out & HHMM_OUT_BETA) && a.beta)
-                lk_put<MODEL, G, KM>(a.beta, a, ln, t, be / sb);
+                put(a.beta, t, be / sb);
             if (out & (HHMM_OUT_GAMMA | HHMM_OUT_UNGAMMA)) {
                 /* gamma = normalize(alpha .* beta) from the normalised vectors (hmm.stan:89-96) */
                 const double ug = (av / sa) * (be / sb);
                 if ((out & HHMM_OUT_UNGAMMA) && a.ungamma)
-                    lk_put<MODEL, G, KM>(a.ungamma, a, ln, t, ug);
+                    put(a.ungamma, t, ug);
                 if ((out & HHMM_OUT_GAMMA) && a.gamma) {
                     const double sg = grp_sum<G>(ug);
-                    lk_put<MODEL, G, KM>(a.gamma, a, ln, t, ug / sg);
+                    put(a.gamma, t, ug / sg);
                 }
             }
             }
             if (t > t0) {
-                grp_exchange<G, KM>(ln.xch, slot, ln.j, es[u] * be, w);
+                xchg(slot, es[u] * be, w);
                 slot ^= 1;
-                be = grp_renorm_at<G>(lk_bwd<MODEL, G, KM>(ln, w), bex, t, ln.dense);
+                be = grp_renorm_at<G>(bwd(w), bex, t, ln.dense);
             }
         }
     }
@@ -640,11 +745,23 @@ template <int MODEL, int G, int KM>
 __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
+    constexpr int SP = lk_vit_split<G>(); /* split columns (half_sum's layout) */
+    constexpr int KH = KM / SP;
     LkLane<MODEL, G, KM> ln;
-    lk_setup<MODEL, G, KM>(ln, a, lds, true, lk_group<G>(a.P));
+    lk_setup<MODEL, G, KM>(ln, a, lds, true, lk_group<G * SP>(a.P));
+    const int h = SP == 2 ? (int)((threadIdx.x >> 5) & 1) : 0;
+    const bool st = ln.on && h == 0; /* the lane that stores */
+    double colh[KH];
+#pragma unroll
+    for (int i = 0; i < KH; ++i) {
+        if constexpr (SP == 2)
+            colh[i] = h ? ln.col[KH + i] : ln.col[i];
+        else
+            colh[i] = ln.col[i];
+    }
     const int Tp = ln.Tp;
     const int K = ln.K;
-    double w[KM];
+    double w[KH];
     int slot = 0;
     auto emit_log = [&](int x, double xr) -> double {
         if constexpr (LkTraits<MODEL>::kGauss)
@@ -685,36 +802,51 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
             if (t < Tp) { /* group-uniform */
                 lk_get<MODEL, G>(bcur, u, x, xr);
                 const double le = emit_log(x, xr);
-                grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
+                if constexpr (SP == 2)
+                    grp_exchange_half<G, KH>(ln.xch, slot, ln.j, h, dl, w);
+                else
+                    grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
                 slot ^= 1;
                 /* candidate (delta + log A) + emission, strict '>' from -inf; the
                  * running max as fmax (vit_step): NaN never wins, first i on ties */
                 double best = dev_ninf();
                 int arg = 0;
 #pragma unroll
-                for (int i = 0; i < KM; ++i) { /* idle i: delta -inf, never greater */
-                    const double cand = (w[i] + ln.col[i]) + le;
+                for (int i = 0; i < KH; ++i) { /* idle i: delta -inf, never greater */
+                    const double cand = (w[i] + colh[i]) + le;
                     const bool gt = cand > best;
                     best = fmax(best, cand);
                     arg = gt ? i : arg;
+                }
+                if constexpr (SP == 2) {
+                    /* the halves' winners: the upper one only if strictly greater
+                     * (the first i on ties, as the sequential scan); fmax is exact */
+                    arg += h * KH;
+                    const double bo = half_other(best);
+                    const int ao = half_other_i(arg);
+                    const double blo = h ? bo : best, bhi = h ? best : bo;
+                    const int alo = h ? ao : arg, ahi = h ? arg : ao;
+                    arg = bhi > blo ? ahi : alo;
+                    best = fmax(blo, bhi);
                 }
                 dl = ln.on ? best : dev_ninf();
                 wd[v >> 2] |= (uint32_t)arg << (8 * (v & 3));
             }
         }
-        if (ln.on && b * kLBack < Tp)
+        if (st && b * kLBack < Tp)
             *reinterpret_cast<uint4 *>(bp_at(b)) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     }
     /* logp_zstar = max(delta_T) (SSE2 order); zstar_T = LAST j attaining it */
-    grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
-    const double lp = stan_max_rt<KM>(w, K);
+    double wf[KM];
+    grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, wf);
+    const double lp = stan_max_rt<KM>(wf, K);
     int z = -1;
 #pragma unroll
     for (int j = 0; j < KM; ++j)
-        if (j < K && w[j] == lp)
+        if (j < K && wf[j] == lp)
             z = j;
     const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
-    if (ln.j == 0) {
+    if (ln.j == 0 && h == 0) {
         if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
             a.logp_zstar[ln.p] = lp;
         if (a.pair_status)
@@ -723,8 +855,9 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
     if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
         return;
     if (invalid) {
-        for (int t = ln.j; t < Tp; t += G)
-            a.zstar[ln.p + a.P * (int64_t)t] = 0;
+        if (h == 0)
+            for (int t = ln.j; t < Tp; t += G)
+                a.zstar[ln.p + a.P * (int64_t)t] = 0;
         return;
     }
     /* backtrack, kLBack steps at a time: lane s holds state s's bytes of the
@@ -751,7 +884,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
             }
         }
         const int t = c * kLBack + (ln.j & (kLBack - 1));
-        if (ln.j < kLBack && t < Tp)
+        if (ln.j < kLBack && t < Tp && h == 0)
             a.zstar[ln.p + a.P * (int64_t)t] = mine;
         q0 = q1;
         q1 = q2;

@@ -1035,6 +1035,8 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_UNSUPPORTED;
     }
     const int gpb = threads / G;
+    const int gpb_fb = threads / (G * lk_fb_split<G>()); /* lk_fb_kernel: pairs (or chunks) per workgroup */
+    const int gpb_vit = threads / (G * lk_vit_split<G>());
     if (a.seg_phase) {
         /* one window of a series split over ranks along T (hhmm_segment):
          * phase 1 + the window's summary, or phases 2 + 3 from the caller's
@@ -1054,7 +1056,7 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
             hipLaunchKernelGGL((lks_bound_kernel<KM, GS>), dim3((unsigned)a.P), dim3(64), 0, st, a);
             const int64_t nq = a.P * (int64_t)a.scan_nc;
             if (out & (fb & ~HHMM_OUT_LOGLIK))
-                hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)),
+                hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb_fb - 1) / gpb_fb)),
                                    dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
         }
         const hipError_t e = hipGetLastError();
@@ -1076,7 +1078,8 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
             return r;
     }
     if (out & vit)
-        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), vs, a);
+        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), dim3((unsigned)((a.P + gpb_vit - 1) / gpb_vit)), dim3(threads),
+                           lk_lds<G>(a, threads, discrete), vs, a);
     hipError_t e = hipGetLastError();
     if ((out & ffbs) && e == hipSuccess) {
         /* the FFBS contract's filter and draws (sequential per pair); its
@@ -1105,7 +1108,7 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         hipLaunchKernelGGL((lks_bound_kernel<KM, GS>), dim3((unsigned)a.P), dim3(64), 0, st, a);
         const int64_t nq = a.P * (int64_t)a.scan_nc;
         if (out & (fb & ~HHMM_OUT_LOGLIK)) /* the chunks' sweeps: posteriors (the loglik is phase 2's) */
-            hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)), dim3(threads),
+            hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb_fb - 1) / gpb_fb)), dim3(threads),
                                lk_lds<G>(a, threads, discrete), st, a);
         e = hipGetLastError();
     } else if ((out & fb) && mfma_fb && e == hipSuccess) {
@@ -1115,7 +1118,8 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         hipLaunchKernelGGL((lkm_fb_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
         e = hipGetLastError();
     } else if ((out & fb) && e == hipSuccess) {
-        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), grid, dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
+        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((a.P + gpb_fb - 1) / gpb_fb)), dim3(threads),
+                           lk_lds<G>(a, threads, discrete), st, a);
         e = hipGetLastError();
     }
     const hhmm_status j = (vs != st) ? join_stream(st, vs) : HHMM_OK;
