@@ -432,9 +432,14 @@ __device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLa
  * three-waves-per-SIMD line, and each step's dependent chain is half as long.
  * Each half keeps its own exchange slots and emission table (lk_setup's
  * 32-lane groups), both halves hold every state's value, and only half 0
- * stores. */
+ * stores.  Off by default: everything besides the dot products (emission
+ * pick, exchange write, renormalisation and gamma reductions, stores) is now
+ * issued once per pair instead of once per two pairs, and that outweighs the
+ * occupancy: N1 55.5 (both kernels split) / 50.7 (lk_fb only) against 40.5 ms,
+ * N2 213.9 against 190.9 (profiles/r05n_ab_n{1,2}.log; GPU parity green with
+ * both on, profiles/r05n_large_k.log). */
 #ifndef HHMM_LK_SPLIT
-#define HHMM_LK_SPLIT 1
+#define HHMM_LK_SPLIT 0
 #endif
 template <int G>
 constexpr int lk_fb_split() { return (G == 32 && HHMM_LK_SPLIT) ? 2 : 1; }
@@ -467,7 +472,7 @@ __device__ __forceinline__ double half_other(double v)
  * half of the candidates i, and the halves' winners combine as the sequential
  * strict-'>' scan would (the upper half's only if strictly greater) */
 #ifndef HHMM_LK_VSPLIT
-#define HHMM_LK_VSPLIT 1
+#define HHMM_LK_VSPLIT 0
 #endif
 template <int G>
 constexpr int lk_vit_split() { return (G == 32 && HHMM_LK_VSPLIT) ? 2 : 1; }
