@@ -721,7 +721,16 @@ def compute_rooflines(name, B, units, dev_ms, src, algo_flops=None):
         r["valu_frac_definition"] = ("SQ_INSTS_VALU per step x 4 cycles / (1024 SIMDs x 2.4 GHz x live step "
                                      "time); every VALU op priced at the fp64 issue rate")
     mi = pm.get("mfma_f64_insts_per_step")
-    if mi:
+    mo = pm.get("mfma_f64_mops_per_step")
+    if mo:
+        # round 5: the chunk products issue v_mfma_f64_4x4x4_16b (512 FLOP per instruction), so the
+        # FLOPs come from the MOPS counter (512 FLOP units) rather than instructions x 2048
+        r["mfma_f64_insts_per_step"] = mi
+        r["mfma_f64_mops_per_step"] = mo
+        r["mfma_frac"] = mo * 512.0 / t / F64_PEAK
+        r["mfma_frac_definition"] = ("f64 MFMA work per step (PMC SQ_INSTS_VALU_MFMA_MOPS_F64, units of 512 FLOP) "
+                                     "x 512 / live step time / 78.6 TFLOP/s")
+    elif mi:
         r["mfma_f64_insts_per_step"] = mi
         r["mfma_frac"] = mi * 2048.0 / t / F64_PEAK
         r["mfma_frac_definition"] = ("v_mfma_f64_16x16x4_f64 instructions per step (PMC SQ_INSTS_VALU_MFMA_F64) x "

@@ -96,6 +96,9 @@ def main():
         wl[w] = {"source": f"profiles/{tag}_workloads_pmc.json", "src": v["src"],
                  "hbm_bytes_per_step": ps.get("hbm_bytes"), "valu_insts_per_step": ps.get("SQ_INSTS_VALU"),
                  "mfma_f64_insts_per_step": ps.get("SQ_INSTS_VALU_MFMA_F64"),
+                 # MOPS: f64 MFMA work in units of 512 FLOP (a v_mfma_f64_16x16x4 counts 4, a
+                 # v_mfma_f64_4x4x4_16b 1), whatever the instruction mix
+                 "mfma_f64_mops_per_step": ps.get("SQ_INSTS_VALU_MFMA_MOPS_F64"),
                  "kernel_ns_per_step": ps.get("kernel_ns")}
     bt_path.write_text(json.dumps(bt, indent=1))
     print(json.dumps({w: v["per_step"] for w, v in out.items()}, indent=1))
