@@ -78,3 +78,20 @@ def test_c2_line_finds_its_pmc_traffic(tmp_path, monkeypatch):
     assert t is None and "00112233aabbccdd" in note, note
     t, note = bench.load_traffic(dom, 1_000, 1000, "00112233aabbccdd")
     assert t is None and "shape" in note, note
+
+
+def test_mfma_fraction_counts_flops_not_instructions(monkeypatch):
+    """roofline.mfma_frac prices the f64 MFMA work by the MOPS counter (512-FLOP
+    units): N2's chunk products issue v_mfma_f64_4x4x4_16b (512 FLOP each), so
+    instructions x 2048 -- the 16x16x4 rule -- would report 4x the work."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    pm = {"source": "test", "src": "s", "hbm_bytes_per_step": 1.0e9, "valu_insts_per_step": 1.0e9,
+          "mfma_f64_insts_per_step": 1.0e10, "mfma_f64_mops_per_step": 1.0e10}
+    monkeypatch.setattr(bench, "load_workload_pmc", lambda name, src: pm)
+    r = bench.compute_rooflines("n2", 184.0, 2.5e8, 100.0, "s", algo_flops=5.0e12)
+    assert abs(r["mfma_frac"] - 1.0e10 * 512 / 0.1 / bench.F64_PEAK) < 1e-12
+    assert r["mfma_frac"] <= 1.0
+    # a 16x16x4 build: 4 MOPS per instruction, the same FLOPs either way
+    pm.update(mfma_f64_insts_per_step=2.5e9)
+    assert abs(bench.compute_rooflines("n2", 184.0, 2.5e8, 100.0, "s")["mfma_frac"] - r["mfma_frac"]) < 1e-12
