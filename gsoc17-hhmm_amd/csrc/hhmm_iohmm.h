@@ -833,7 +833,9 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
     int64_t n, d;
     pair_coords(a, p, n, d);
     const int Tp = pair_len(a, n);
-    const int M = a.M, L = a.L;
+    /* LM == 3 is launched for L == 3 exactly (launch_io_sp): the mixture loops
+     * are straight-line code, so the step's three exps interleave */
+    const int M = a.M, L = (FAM == IO_MIX && LM == 3) ? 3 : a.L;
     const uint32_t out = a.outputs;
     const bool want_ffbs = MATH == IO_DET && (out & HHMM_OUT_FFBS) && a.z_ffbs;
     const bool gate = (out & kIoFilt) && a.io_redo; /* iohmm_sweep's underflow check */
@@ -959,11 +961,18 @@ __device__ __forceinline__ void iohmm_sp_sweep(const DevArgs &a)
             if constexpr (FAM == IO_REG) {
                 ej = MATH == IO_DET ? sexp(o - m) : exp(o - m);
             } else {
+                /* every summand's exp first (independent: their table reads
+                 * overlap), then the model's sum over the finite ones in order
+                 * (a skipped -inf summand and an added +0 give the same bits) */
+                double ye[LM];
+#pragma unroll
+                for (int l = 0; l < LM; ++l)
+                    ye[l] = (l < L) ? sexp(acc[l] - m) : 0.0;
                 ej = 0.0;
 #pragma unroll
                 for (int l = 0; l < LM; ++l)
-                    if (l < L && acc[l] != dev_ninf())
-                        ej += sexp(acc[l] - m);
+                    if (l < L)
+                        ej += (acc[l] != dev_ninf()) ? ye[l] : 0.0;
             }
             double ee[K];
             quad_gather<K>(ej, ee);
@@ -1114,9 +1123,12 @@ static hhmm_status launch_io_sp(const DevArgs &a, hipStream_t st)
     const dim3 grid((unsigned)((lanes + kBlock - 1) / kBlock));
     /* the mixture tables of a lane's state sit in registers: L <= 4 or <= 8 */
     const size_t tab = MATH == IO_DET ? 128 * sizeof(hhmm_exp2_entry) : 0; /* hhmm_det_exp_tab's copy */
-    const size_t lds = ((FAM == IO_MIX) ? (size_t)(kBlock / 64) * 2 * (a.L <= 4 ? 4 : kIoLmax) * 64 * sizeof(double2) : 0) + tab;
+    const int lm = (FAM == IO_MIX && a.L == 3) ? 3 : (a.L <= 4 ? 4 : kIoLmax);
+    const size_t lds = ((FAM == IO_MIX) ? (size_t)(kBlock / 64) * 2 * lm * 64 * sizeof(double2) : 0) + tab;
     if (FAM == IO_REG)
         hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 1>), grid, dim3(kBlock), tab, st, a);
+    else if (lm == 3)
+        hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 3>), grid, dim3(kBlock), lds, st, a);
     else if (a.L <= 4)
         hipLaunchKernelGGL((iohmm_sp_kernel<FAM, K, MMAX, MATH, 4>), grid, dim3(kBlock), lds, st, a);
     else
