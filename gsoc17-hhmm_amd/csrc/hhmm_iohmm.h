@@ -227,7 +227,11 @@ __device__ __forceinline__ void softmax_cr_log(const double (&v)[K], double (&A)
             mx = v[i];
     double y[K], th[K], rho[K];
     bool ok[K];
-    double sum = 0.0;
+    bool all_ok = true;
+    /* the K quick phases first, straight-line (independent chains that
+     * interleave), then one branch for the rare lanes whose rounding test
+     * failed, then the sum in order: the same doubles as calling dev_cr_exp
+     * per state */
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         y[i] = v[i] - mx;
@@ -236,13 +240,20 @@ __device__ __forceinline__ void softmax_cr_log(const double (&v)[K], double (&A)
         int e;
         const hhmm_dd f = hhmm_cr_exp_quick_dd(in ? y[i] : 0.0, &e);
         ok[i] = in & cr_fast_ok(f.hi, f.lo, kCrExpC);
-        double r = f.hi * hhmm_bits_to_double((uint64_t)(e + 1023) << 52);
+        th[i] = f.hi * hhmm_bits_to_double((uint64_t)(e + 1023) << 52);
         rho[i] = f.lo * rcp_refined(f.hi);
-        if (!ok[i])
-            r = cr_exp_cold(y[i]);
-        th[i] = r;
-        sum += th[i];
+        all_ok &= ok[i];
     }
+    if (!all_ok) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (!ok[i])
+                th[i] = cr_exp_cold(y[i]);
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        sum += th[i];
 #pragma unroll
     for (int i = 0; i < K; ++i)
         A[i] = th[i] / sum;
@@ -253,16 +264,23 @@ __device__ __forceinline__ void softmax_cr_log(const double (&v)[K], double (&A)
     if (one)
         ls = hhmm_dd_make(0.0, 0.0);
     const double err = __builtin_fabs(ls.hi) * 0x1p-71 + 0x1p-76;
+    bool lok[K];
+    bool all_lok = true;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         const double rem = fma(A[i], sum, -th[i]);
         const double corr = (rem * rcp_refined(th[i]) - rho[i]) - ls.lo;
         const hhmm_dd s = hhmm_two_sum(y[i], -ls.hi);
         const hhmm_dd r = hhmm_two_sum(s.hi, s.lo + corr);
-        double l = r.hi;
-        if (!(ok[i] & sok & cr_round_safe(r.hi, r.lo, err)))
-            l = cr_log_cold(A[i]);
-        lA[i] = l;
+        lA[i] = r.hi;
+        lok[i] = ok[i] & sok & cr_round_safe(r.hi, r.lo, err);
+        all_lok &= lok[i];
+    }
+    if (!all_lok) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (!lok[i])
+                lA[i] = cr_log_cold(A[i]);
     }
 }
 
