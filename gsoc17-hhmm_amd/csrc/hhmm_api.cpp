@@ -1026,7 +1026,9 @@ static hhmm_status segment_run(const hhmm_request *req, hhmm_result *res, const 
         set_error("workspace of %zu bytes < %zu required (hhmm_segment_workspace_size)", wsb, need);
         return HHMM_ERR_INVALID_ARGUMENT;
     }
-    return launch_all(&r2, rr, npairs(&r2), ws, (hipStream_t)stream, seg, phase, phase == 2);
+    /* both calls check the window's data: the summary marks a bad pair's record
+     * (NaN log scale) so that every rank chaining it flags the pair */
+    return launch_all(&r2, rr, npairs(&r2), ws, (hipStream_t)stream, seg, phase, true);
 }
 
 hhmm_status hhmm_segment_summary_device(const hhmm_request *req, const hhmm_segment *seg, void *workspace,

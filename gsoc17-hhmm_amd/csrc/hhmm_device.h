@@ -194,27 +194,19 @@ __device__ __forceinline__ void put_out(T *row, uint32_t byte_off, T v)
 }
 
 /* Scratch written by one sweep and read back once by the next (alpha
- * checkpoints, Viterbi back-pointer words).  HHMM_NT_TMP puts streaming hints
- * on both sides; it is off because it cost the forward-backward 6.5 % at C2
- * (7.97 against 7.48 ms, the checkpoints are re-read out of the caches) and
- * left the Viterbi unchanged. */
+ * checkpoints, Viterbi back-pointer words): plain stores and loads.  Streaming
+ * hints on both sides cost the forward-backward 6.5 % at C2 (7.97 against 7.48
+ * ms: the checkpoints are re-read out of the caches) and left the Viterbi
+ * unchanged. */
 template <typename T>
 __device__ __forceinline__ void put_tmp(T *row, uint32_t byte_off, T v)
 {
-#ifdef HHMM_NT_TMP
-    __builtin_nontemporal_store(v, reinterpret_cast<T *>(reinterpret_cast<char *>(row) + byte_off));
-#else
     at(row, byte_off) = v;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ T get_tmp(const T *row, uint32_t byte_off)
 {
-#ifdef HHMM_NT_TMP
-    return __builtin_nontemporal_load(reinterpret_cast<const T *>(reinterpret_cast<const char *>(row) + byte_off));
-#else
     return at(row, byte_off);
-#endif
 }
 
 /* Power-of-two renormalisation of a K-vector after every step: the largest

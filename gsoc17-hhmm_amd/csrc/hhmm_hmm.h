@@ -741,9 +741,6 @@ __device__ __forceinline__ void emit_posteriors(const DevArgs &a, int64_t p, int
     }
 }
 
-#ifndef HHMM_INLINE_XCHECK
-#define HHMM_INLINE_XCHECK 1 /* A/B knob: 0 leaves x to the device entry's separate check pass */
-#endif
 
 /* The device entry's data check done inline by a whole-series sweep that reads
  * x anyway (HHMM_PAIR_INVALID_DATA): the running max of x - 1 as unsigned (an
@@ -753,7 +750,7 @@ template <int C, bool FULL>
 __device__ __forceinline__ void xcheck_acc(uint32_t &xm, const Obs (&o)[C], int c, int Tp)
 {
 #pragma unroll
-    for (int v = 0; v < C * HHMM_INLINE_XCHECK; ++v)
+    for (int v = 0; v < C; ++v)
         xm = max(xm, (FULL || c * C + v < Tp) ? (uint32_t)(o[v].x - 1) : 0u);
 }
 
@@ -1075,7 +1072,7 @@ __device__ __forceinline__ void fb_sweep(const DevArgs &a, const FbLane<MODEL, K
     Em<K> ecur;
     emit_prob<MODEL, K, fb_ffbs(MODE)>(ln.pp, ln.slab, ln.L, grp[0][0], ecur, ln.etab);
     /* whole-series sweeps over x alone check it inline (xcheck_acc) */
-    constexpr bool XCHK = !SCAN && !AUX && ModelTraits<MODEL>::kDiscrete && HHMM_INLINE_XCHECK;
+    constexpr bool XCHK = !SCAN && !AUX && ModelTraits<MODEL>::kDiscrete;
     uint32_t xm = 0;
     int c = cb;
     for (; c + D <= nfull; c += D) {
@@ -1463,7 +1460,7 @@ __device__ __forceinline__ void viterbi_block(const DevArgs &a, uint32_t block)
     /* chunk 0: the t = 1 row and the NaN step (Q3) */
     vit_fwd_chunk<MODEL, K, CV, false, true>(a, p, pp, slab, Tp, 0, cur, grp[0][0], le, dl, word);
     /* decoding x itself: the data check inline (xcheck_acc) */
-    constexpr bool XCHK = !PK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete && HHMM_INLINE_XCHECK;
+    constexpr bool XCHK = !PK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
     uint32_t xm = 0;
     if constexpr (XCHK)
         xcheck_acc<CV, false>(xm, cur, 0, Tp);
@@ -3308,7 +3305,7 @@ static hhmm_status launch_fb(const DevArgs &a, bool fwd_only, hipStream_t st)
     const bool ffbs = (a.outputs & HHMM_OUT_FFBS) != 0;
     if (ModelTraits<MODEL>::kGauss && ffbs) /* fb_exp2_lds's table copy */
         s.lds = std::max(s.lds, kExp2TabBytes);
-    constexpr bool xchk = HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
+    constexpr bool xchk = !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
     /* every fb_kernel below sweeps x forward over whole series (fb_sweep's inline check) */
     t_data_checked_inline |= xchk && (ffbs || !(a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)));
     if (a.outputs & (HHMM_OUT_UNALPHA | HHMM_OUT_UNBETA)) {
@@ -3440,7 +3437,7 @@ static hhmm_status launch_viterbi(const DevArgs &a, hipStream_t st, bool packed 
         hipLaunchKernelGGL((viterbi_kernel<MODEL, K, fbv_ok<MODEL, K>()>), s.grid, s.block, s.lds, st, a);
     } else {
         /* decodes x itself: viterbi_block's inline check */
-        t_data_checked_inline |= HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
+        t_data_checked_inline |= !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
         hipLaunchKernelGGL((viterbi_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
     }
     hipError_t e = hipGetLastError();
@@ -3486,7 +3483,7 @@ static hhmm_status launch_vfb(const DevArgs &a, hipStream_t st)
     }
     hipError_t e = hipMemsetAsync(a.rnw, 0, sizeof(int32_t), st); /* the dense-wave list's count */
     if (e == hipSuccess) {
-        t_data_checked_inline |= HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux; /* x (and T) checked in phase 1 */
+        t_data_checked_inline |= !ModelTraits<MODEL>::kAux; /* x (and T) checked in phase 1 */
         hipLaunchKernelGGL((vfb_kernel<MODEL, K>), s.grid, s.block, s.lds, st, a);
         hipLaunchKernelGGL((vfb_dense_kernel<MODEL, K>), dim3(kDenseBlocks), dim3(64), s.lds / (s.block.x / 64), st,
                            a);
@@ -3513,7 +3510,7 @@ static hhmm_status launch_split(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_UNSUPPORTED;
     }
     /* the forward launch sweeps x over whole series (fb_sweep's inline check) */
-    t_data_checked_inline |= HHMM_INLINE_XCHECK && !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
+    t_data_checked_inline |= !ModelTraits<MODEL>::kAux && ModelTraits<MODEL>::kDiscrete;
     hipLaunchKernelGGL((fb_kernel<MODEL, K, MODE, FB_PH_FWD>), s.grid, s.block, s.lds, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

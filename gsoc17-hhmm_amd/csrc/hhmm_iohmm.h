@@ -202,14 +202,11 @@ __device__ __forceinline__ void stan_softmax(const double (&v)[K], double (&th)[
  * of log A_i, so where the rounding test passes the rounded head IS the
  * correctly rounded log; elsewhere (the rounding test fails, the exp took its
  * accurate phase, A_i within ~2^-18 of 1) the lane calls the full function. */
-/* Build knob (default on).  With w / b in registers it measured slower at C3
- * (60.95 against 58.6 ms: the sweep is capped at 256 registers and the extra
- * live doubles grew its spill from 144 to 224 bytes); with w / b in the LDS
- * slab (io_wb_lds, 245 registers, no spill) it measured 53.8 against 58.5 ms
- * (tools/ab_workload.py, one box, profiles/r02zh_ab_c3.log). */
-#ifndef HHMM_IO_ONELOG
-#define HHMM_IO_ONELOG 1
-#endif
+/* Always on for the correctly rounded profile.  With w / b in registers it
+ * measured slower at C3 (60.95 against 58.6 ms: the sweep is capped at 256
+ * registers and the extra live doubles grew its spill from 144 to 224 bytes);
+ * with w / b in the LDS slab (io_wb_lds, 245 registers, no spill) it measured
+ * 53.8 against 58.5 ms (tools/ab_workload.py, one box, profiles/r02zh_ab_c3.log). */
 __device__ __forceinline__ double rcp_refined(double x)
 {
     double r = __builtin_amdgcn_rcp(x);
@@ -301,11 +298,8 @@ __device__ __forceinline__ const double2 *mix_row(const double2 *slab, int L, in
  * LDS slab instead of registers: the correctly rounded functions of the
  * Viterbi profile need the registers (two waves per SIMD, 256 of them), and
  * the slab costs 16 ds_read_b128 per step against ~1,400 VALU. */
-#ifndef HHMM_IO_REG_LDSWB
-#define HHMM_IO_REG_LDSWB 1
-#endif
 template <int FAM>
-constexpr bool io_wb_lds() { return FAM == IO_REG && HHMM_IO_REG_LDSWB; }
+constexpr bool io_wb_lds() { return FAM == IO_REG; }
 
 /* Row `row` of the w / b slab (rows 0..K-1: w_j, K..2K-1: b_j). */
 template <int MMAX>
@@ -447,7 +441,7 @@ __device__ __forceinline__ void io_transition(const IoParams<FAM, K, MMAX> &pp, 
             wb_row<MMAX>(wb, j, wr);
         v[j] = sse_dot<MMAX>(u, io_wb_lds<FAM>() ? wr : pp.w[j], M);
     }
-    if constexpr (MATH == IO_CR && HHMM_IO_ONELOG) {
+    if constexpr (MATH == IO_CR) {
         if (need_lA) { /* the Viterbi's log A from the softmax's own exps */
             softmax_cr_log<K>(v, st.A, st.lA);
             return;

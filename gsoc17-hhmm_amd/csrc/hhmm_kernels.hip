@@ -408,17 +408,15 @@ DevArgs make_args(const hhmm_request *req, const hhmm_result *res, int64_t P)
 /* ------------------------------------------------------------------ */
 thread_local bool t_data_checked_inline = false;
 
-#ifndef HHMM_DATA_CHECK
-#define HHMM_DATA_CHECK 1 /* A/B knob: 0 drops the device entry's data-block checks */
-#endif
-
-constexpr int kDcSteps = 64; /* time steps per thread of data_check_kernel */
+constexpr int kDcSteps = 64; /* time steps per thread of data_check_kernel (per strip) */
+constexpr unsigned kDcMaxStrips = 32768; /* grid.y cap: longer series loop over strips */
 constexpr int kDcSeries = 4; /* series per thread (one 16-byte load per step) */
 
 /* Flags series n when one of its steps t < T[n] breaks an int<lower=1,
  * upper=hi> bound: v (x, 1..L), w (sign 1..2 / g 1..G; null: none).  A
  * thread takes kDcSeries consecutive series (the fastest index: a wave reads
- * 1 KB of each row), grid.y strips of kDcSteps steps, 8 steps of independent
+ * 1 KB of each row), strips of kDcSteps steps (strip blockIdx.y, then every
+ * gridDim.y-th strip: grid.y is capped at kDcMaxStrips), 8 steps of independent
  * loads in flight (HBM-bound: the pass reads each element once).  Steps at or
  * past a series' own length are read (inside the T_max x N block) and masked.
  * A flag is a plain vector store of 1 (every writer stores the same value). */
@@ -433,14 +431,15 @@ __global__ void __launch_bounds__(256) data_check_kernel(const int32_t *v, int v
 #pragma unroll
     for (int j = 0; j < kDcSeries; ++j) /* a length outside 1..T_max: data_mark_kernel */
         Tn[j] = j < nk ? (T ? min(max(T[n0 + j], 1), Tmax) : Tmax) : 0;
-    const int t0 = (int)blockIdx.y * kDcSteps;
-    const int t1 = min(t0 + kDcSteps, Tmax);
     const bool vec = nk == kDcSeries && (N % kDcSeries) == 0 && ((uintptr_t)v % 16) == 0 &&
                      (!w || ((uintptr_t)w % 16) == 0);
     bool bad[kDcSeries] = {};
     auto test = [&](int hi, int t, int j, int val) {
         bad[j] |= (t < Tn[j]) & ((uint32_t)(val - 1) >= (uint32_t)hi);
     };
+    for (int64_t s0 = (int64_t)blockIdx.y * kDcSteps; s0 < Tmax; s0 += (int64_t)gridDim.y * kDcSteps) {
+    const int t0 = (int)s0;
+    const int t1 = min(t0 + kDcSteps, Tmax);
     if (vec) {
         auto pass = [&](const int32_t *u, int hi) {
             int t = t0;
@@ -477,6 +476,7 @@ __global__ void __launch_bounds__(256) data_check_kernel(const int32_t *v, int v
                     test(whi, t, j, w[i]);
             }
     }
+    }
 #pragma unroll
     for (int j = 0; j < kDcSeries; ++j)
         if (bad[j])
@@ -484,7 +484,11 @@ __global__ void __launch_bounds__(256) data_check_kernel(const int32_t *v, int v
 }
 
 /* pair_status[p] = HHMM_PAIR_INVALID_DATA for the pairs of flagged series and
- * of series whose T[n] / T_oos[n] lies outside 1..T_max / 1..T_oos_max. */
+ * of series whose T[n] / T_oos[n] lies outside 1..T_max / 1..T_oos_max.
+ * Segment windows: the summary call has no pair_status, so a bad
+ * pair's summary carries a NaN log scale (field 2K^2 + 1) instead; every rank
+ * that chains it (hhmm_amd.segment.boundaries) then receives a NaN in the
+ * entering state or the leaving beta, and the finish call flags the pair. */
 __global__ void __launch_bounds__(256) data_mark_kernel(const DevArgs a, const int32_t *T_oos, int Toos_max)
 {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -497,6 +501,19 @@ __global__ void __launch_bounds__(256) data_mark_kernel(const DevArgs a, const i
         bad |= a.T[n] < 1 || a.T[n] > a.Tmax;
     if (T_oos)
         bad |= T_oos[n] < 1 || T_oos[n] > Toos_max;
+    if (a.seg_phase == 1) {
+        if (bad && a.seg_sum)
+            a.seg_sum[p + a.P * (int64_t)(2 * a.K * a.K + 1)] = __builtin_nan("");
+        return;
+    }
+    if (a.seg_phase == 2) {
+        for (int f = 0; f <= a.K; ++f) {
+            if (a.seg_nofirst && a.seg_enter)
+                bad |= isnan(a.seg_enter[p + a.P * (int64_t)f]);
+            if (a.seg_nolast && a.seg_leave)
+                bad |= isnan(a.seg_leave[p + a.P * (int64_t)f]);
+        }
+    }
     if (bad)
         a.pair_status[p] = HHMM_PAIR_INVALID_DATA;
 }
@@ -511,11 +528,13 @@ static hhmm_status launch_data_check(const DevArgs &a, const hhmm_request *req, 
     hipError_t e = hipSuccess; /* a.dc_flag cleared by launch_all before the model's kernels */
     auto check = [&](const int32_t *v, int vhi, const int32_t *w, int whi, const int32_t *T, int Tmax) {
         const int64_t thr = (d.n_series + kDcSeries - 1) / kDcSeries;
-        const dim3 grid((unsigned)((thr + 255) / 256), (unsigned)((Tmax + kDcSteps - 1) / kDcSteps));
+        const dim3 grid((unsigned)((thr + 255) / 256),
+                        std::min((unsigned)((Tmax + kDcSteps - 1) / kDcSteps), kDcMaxStrips));
         hipLaunchKernelGGL(data_check_kernel, grid, dim3(256), 0, st, v, vhi, w, whi, T, (int64_t)d.n_series, Tmax,
                            a.dc_flag);
     };
-    if (e == hipSuccess && discrete && !inline_checked)
+    /* the summary call's sweeps are not the ones that check x inline */
+    if (e == hipSuccess && discrete && (!inline_checked || a.seg_phase == 1))
         check(d.x_int, d.L, tayal ? d.sign : (m == HHMM_MODEL_HMM_MULTINOM_SEMISUP ? d.g : nullptr),
               tayal ? 2 : d.G, d.T, d.T_max);
     if (e == hipSuccess && m == HHMM_MODEL_TAYAL_LITE)
@@ -572,7 +591,7 @@ hhmm_status launch_all(const hhmm_request *req, const hhmm_result *res, int64_t 
 {
     DevArgs a = make_args(req, res, P);
     bind_workspace(a, ws, req->data.T_max, req->data.T_oos_max, (uint32_t)req->flags);
-    const bool check = HHMM_DATA_CHECK && check_data && a.pair_status && a.dc_flag;
+    const bool check = check_data && a.dc_flag && (a.pair_status || (seg && seg_phase == 1 && seg->summary));
     if (!check)
         a.dc_flag = nullptr;
     if (seg) {

@@ -89,27 +89,13 @@ __device__ __forceinline__ double lk_dpp(double v)
     const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
-/* Build knob: lane ^ 16 by v_permlane16_swap (0: ds_swizzle).  N1 40.94 against
- * 41.19 ms interleaved on one box (outputs identical; profiles/r04g_ab_n1.log).
- * The MFMA chunk-product kernel keeps its ds_bpermute column reductions
- * (__shfl_xor): there the VALU form measured 168.8 against 156.8 ms. */
-#ifndef HHMM_LK_PERMLANE
-#define HHMM_LK_PERMLANE 1
-#endif
-__device__ __forceinline__ double lk_xor16(double v)
-{
-#if HHMM_LK_PERMLANE
-    /* a VALU exchange (lane_xor16) instead of a ds_swizzle round trip through
-     * the LDS crossbar, on the dependency chain of every group reduction */
-    return lane_xor16(v);
-#else
-    const long long b = __double_as_longlong(v);
-    constexpr int kXor16 = 0x1F | (0x10 << 10); /* ds_swizzle bit mode: and 0x1F, or 0, xor 0x10 */
-    const int l = __builtin_amdgcn_ds_swizzle((int)b, kXor16);
-    const int h = __builtin_amdgcn_ds_swizzle((int)(b >> 32), kXor16);
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)h << 32) | (unsigned)l));
-#endif
-}
+/* lane ^ 16 by v_permlane16_swap: a VALU exchange (lane_xor16) instead of a
+ * ds_swizzle round trip through the LDS crossbar, on the dependency chain of
+ * every group reduction (N1 40.94 against 41.19 ms with ds_swizzle, outputs
+ * identical; profiles/r04g_ab_n1.log).  The MFMA chunk-product kernel keeps its
+ * ds_bpermute column reductions (__shfl_xor): there the VALU form measured
+ * 168.8 against 156.8 ms. */
+__device__ __forceinline__ double lk_xor16(double v) { return lane_xor16(v); }
 constexpr int kDppXor1 = 0xB1;       /* quad_perm [1,0,3,2] */
 constexpr int kDppXor2 = 0x4E;       /* quad_perm [2,3,0,1] */
 constexpr int kDppHalfMirror = 0x141;
@@ -422,79 +408,6 @@ __device__ __forceinline__ void lk_put(double *out, const DevArgs &a, const LkLa
         out[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
 }
 
-/* ---- split columns (lk_fb_kernel at G = 32, HHMM_LK_SPLIT) ----
- * A pair takes the whole wave: lane (h, j) = 32 h + j holds state j and the
- * half h of the K-vectors' index range, i in [h KH, h KH + KH), KH = KM / 2:
- * half of the column and row of A, half of the exchanged vector, half of each
- * dot product, the two halves' partial sums added across the wave halves by
- * v_permlane32_swap.  The K^2 FMAs per pair-step are the same; the registers
- * (col, row and the exchanged vector: 3 KM doubles -> 3 KH) drop below the
- * three-waves-per-SIMD line, and each step's dependent chain is half as long.
- * Each half keeps its own exchange slots and emission table (lk_setup's
- * 32-lane groups), both halves hold every state's value, and only half 0
- * stores.  Off by default: everything besides the dot products (emission
- * pick, exchange write, renormalisation and gamma reductions, stores) is now
- * issued once per pair instead of once per two pairs, and that outweighs the
- * occupancy: N1 55.5 (both kernels split) / 50.7 (lk_fb only) against 40.5 ms,
- * N2 213.9 against 190.9 (profiles/r05n_ab_n{1,2}.log; GPU parity green with
- * both on, profiles/r05n_large_k.log). */
-#ifndef HHMM_LK_SPLIT
-#define HHMM_LK_SPLIT 0
-#endif
-template <int G>
-constexpr int lk_fb_split() { return (G == 32 && HHMM_LK_SPLIT) ? 2 : 1; }
-
-/* lower-half value + upper-half value, in every lane of the wave (the same bits
- * in both halves) */
-__device__ __forceinline__ double half_sum(double v)
-{
-    const long long b = __double_as_longlong(v);
-    const auto lo = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
-    const double lower = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]));
-    const double upper = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]));
-    return lower + upper;
-}
-
-/* the other wave half's value (lane ^ 32) */
-__device__ __forceinline__ int half_other_i(int v)
-{
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (threadIdx.x & 32) ? r[0] : r[1];
-}
-__device__ __forceinline__ double half_other(double v)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = half_other_i((int)b), hi = half_other_i((int)(b >> 32));
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-/* lk_viterbi_kernel with split columns (HHMM_LK_VSPLIT): each half scans its
- * half of the candidates i, and the halves' winners combine as the sequential
- * strict-'>' scan would (the upper half's only if strictly greater) */
-#ifndef HHMM_LK_VSPLIT
-#define HHMM_LK_VSPLIT 0
-#endif
-template <int G>
-constexpr int lk_vit_split() { return (G == 32 && HHMM_LK_VSPLIT) ? 2 : 1; }
-
-/* the half h of the group's vector v through LDS slot `slot` (grp_exchange) */
-template <int G, int KH>
-__device__ __forceinline__ void grp_exchange_half(double *xch, int slot, int j, int h, double v, double (&w)[KH])
-{
-    static_assert(KH % 2 == 0, "16-byte reads");
-    double *s = xch + slot * G;
-    s[j] = v;
-    __asm__ __volatile__("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const double *sh = s + h * KH;
-#pragma unroll
-    for (int i = 0; i < KH; i += 2) {
-        const double2 q = *reinterpret_cast<const double2 *>(sh + i);
-        w[i] = q.x;
-        w[i + 1] = q.y;
-    }
-}
-
 /* Forward-backward: loglik, alpha, beta, ungamma, gamma.  One group sweeps a
  * whole series, or -- under the parallel scan over T (a.scan_cl > 0,
  * hhmm_lkscan.h) -- one T-chunk [t0, t1) of a pair (group q = pair + P *
@@ -506,44 +419,22 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     HIP_DYNAMIC_SHARED(double, lds)
     const bool scan = a.scan_cl > 0;
     const int64_t nq = scan ? a.P * (int64_t)a.scan_nc : a.P;
-    constexpr int SP = lk_fb_split<G>(); /* split columns (see half_sum) */
-    constexpr int KH = KM / SP;
-    const int64_t q = lk_group<G * SP>(nq);
+    constexpr int KH = KM;
+    const int64_t q = lk_group<G>(nq);
     const int64_t pq = scan ? q % a.P : q;
     const int cq = scan ? (int)(q / a.P) : 0;
     LkLane<MODEL, G, KM> ln;
     lk_setup<MODEL, G, KM>(ln, a, lds, false, pq);
-    const int h = SP == 2 ? (int)((threadIdx.x >> 5) & 1) : 0;
-    const bool st = ln.on && h == 0; /* the lane that stores state j's outputs */
-    double colh[KH], rowh[KH];
-#pragma unroll
-    for (int i = 0; i < KH; ++i) {
-        if constexpr (SP == 2) {
-            colh[i] = h ? ln.col[KH + i] : ln.col[i];
-            rowh[i] = h ? ln.row[KH + i] : ln.row[i];
-        } else {
-            colh[i] = ln.col[i];
-            rowh[i] = ln.row[i];
-        }
-    }
+    const bool st = ln.on; /* the lane that stores state j's outputs */
     auto fwd = [&](const double (&wv)[KH], double e) -> double {
-        double d = lk_dot<KH>(wv, colh);
-        if constexpr (SP == 2)
-            d = half_sum(d);
+        const double d = lk_dot<KH>(wv, ln.col);
         return ln.on ? d * e : 0.0;
     };
     auto bwd = [&](const double (&wv)[KH]) -> double {
-        double d = lk_dot<KH>(wv, rowh);
-        if constexpr (SP == 2)
-            d = half_sum(d);
+        const double d = lk_dot<KH>(wv, ln.row);
         return ln.on ? d : 0.0;
     };
-    auto xchg = [&](int sl, double v, double (&wv)[KH]) {
-        if constexpr (SP == 2)
-            grp_exchange_half<G, KH>(ln.xch, sl, ln.j, h, v, wv);
-        else
-            grp_exchange<G, KM>(ln.xch, sl, ln.j, v, wv);
-    };
+    auto xchg = [&](int sl, double v, double (&wv)[KH]) { grp_exchange<G, KM>(ln.xch, sl, ln.j, v, wv); };
     auto put = [&](double *o, int t, double v) {
         if (st && o)
             o[ln.p + a.P * ((int64_t)t + (int64_t)a.Tout * ln.j)] = v;
@@ -611,7 +502,7 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
     }
     if (!scan) {
         const double sa = grp_sum<G>(al); /* every lane takes part in the shuffle */
-        if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0 && h == 0)
+        if ((out & HHMM_OUT_LOGLIK) && a.loglik && ln.j == 0)
             a.loglik[ln.p] = log(sa) + (lsc + kLn2 * ex);
     }
     if (!need_bwd || t1 <= t0)
@@ -750,20 +641,11 @@ template <int MODEL, int G, int KM>
 __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
 {
     HIP_DYNAMIC_SHARED(double, lds)
-    constexpr int SP = lk_vit_split<G>(); /* split columns (half_sum's layout) */
-    constexpr int KH = KM / SP;
+    constexpr int KH = KM;
     LkLane<MODEL, G, KM> ln;
-    lk_setup<MODEL, G, KM>(ln, a, lds, true, lk_group<G * SP>(a.P));
-    const int h = SP == 2 ? (int)((threadIdx.x >> 5) & 1) : 0;
-    const bool st = ln.on && h == 0; /* the lane that stores */
-    double colh[KH];
-#pragma unroll
-    for (int i = 0; i < KH; ++i) {
-        if constexpr (SP == 2)
-            colh[i] = h ? ln.col[KH + i] : ln.col[i];
-        else
-            colh[i] = ln.col[i];
-    }
+    lk_setup<MODEL, G, KM>(ln, a, lds, true, lk_group<G>(a.P));
+    const bool st = ln.on; /* the lane that stores */
+    const double (&colh)[KH] = ln.col;
     const int Tp = ln.Tp;
     const int K = ln.K;
     double w[KH];
@@ -807,10 +689,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
             if (t < Tp) { /* group-uniform */
                 lk_get<MODEL, G>(bcur, u, x, xr);
                 const double le = emit_log(x, xr);
-                if constexpr (SP == 2)
-                    grp_exchange_half<G, KH>(ln.xch, slot, ln.j, h, dl, w);
-                else
-                    grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
+                grp_exchange<G, KM>(ln.xch, slot, ln.j, dl, w);
                 slot ^= 1;
                 /* candidate (delta + log A) + emission, strict '>' from -inf; the
                  * running max as fmax (vit_step): NaN never wins, first i on ties */
@@ -822,17 +701,6 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
                     const bool gt = cand > best;
                     best = fmax(best, cand);
                     arg = gt ? i : arg;
-                }
-                if constexpr (SP == 2) {
-                    /* the halves' winners: the upper one only if strictly greater
-                     * (the first i on ties, as the sequential scan); fmax is exact */
-                    arg += h * KH;
-                    const double bo = half_other(best);
-                    const int ao = half_other_i(arg);
-                    const double blo = h ? bo : best, bhi = h ? best : bo;
-                    const int alo = h ? ao : arg, ahi = h ? arg : ao;
-                    arg = bhi > blo ? ahi : alo;
-                    best = fmax(blo, bhi);
                 }
                 dl = ln.on ? best : dev_ninf();
                 wd[v >> 2] |= (uint32_t)arg << (8 * (v & 3));
@@ -851,7 +719,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
         if (j < K && wf[j] == lp)
             z = j;
     const bool invalid = (z < 0) || (Tp >= 2 && lp == dev_ninf());
-    if (ln.j == 0 && h == 0) {
+    if (ln.j == 0) {
         if ((a.outputs & HHMM_OUT_LOGP_ZSTAR) && a.logp_zstar)
             a.logp_zstar[ln.p] = lp;
         if (a.pair_status)
@@ -860,9 +728,8 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
     if (!((a.outputs & HHMM_OUT_ZSTAR) && a.zstar))
         return;
     if (invalid) {
-        if (h == 0)
-            for (int t = ln.j; t < Tp; t += G)
-                a.zstar[ln.p + a.P * (int64_t)t] = 0;
+        for (int t = ln.j; t < Tp; t += G)
+            a.zstar[ln.p + a.P * (int64_t)t] = 0;
         return;
     }
     /* backtrack, kLBack steps at a time: lane s holds state s's bytes of the
@@ -889,7 +756,7 @@ __global__ void __launch_bounds__(kBlock) lk_viterbi_kernel(const DevArgs a)
             }
         }
         const int t = c * kLBack + (ln.j & (kLBack - 1));
-        if (ln.j < kLBack && t < Tp && h == 0)
+        if (ln.j < kLBack && t < Tp)
             a.zstar[ln.p + a.P * (int64_t)t] = mine;
         q0 = q1;
         q1 = q2;

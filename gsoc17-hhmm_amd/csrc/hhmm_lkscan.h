@@ -65,12 +65,10 @@ __device__ __forceinline__ double lks_mfma4(double a, double b, double c)
 {
     return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
-/* Build knob: the chunk products on v_mfma_f64_4x4x4 (1) or 16x16x4 (0).  With
- * the 4 x 4 blocks the state dimension pads to a multiple of 4 instead of 16
- * (K = 23: 24 x 24 instead of 32 x 24 per step, VERDICT r4's 1.45x padding). */
-#ifndef HHMM_LKS_MFMA4
-#define HHMM_LKS_MFMA4 1
-#endif
+/* The chunk products run on v_mfma_f64_4x4x4: with the 4 x 4 blocks the state
+ * dimension pads to a multiple of 4 instead of 16 (K = 23: 24 x 24 instead of
+ * 32 x 24 per step, VERDICT r4's 1.45x padding; the 16x16x4 form measured
+ * slower at N2, round 5). */
 
 /* Columns of M'^T per wave: TPW tiles of 16.  RT row tiles of 16 states, KSM
  * k-steps of 4 states (K <= 16: 1 / 4; K <= 24: 2 / 6; K <= 32: 2 / 8). */
@@ -142,7 +140,6 @@ lks_prod_kernel(const DevArgs a)
             tab[idx] = j < K ? a.phi_k[d + S * ((int64_t)j + (int64_t)K * l)] : 0.0;
         }
     }
-#if HHMM_LKS_MFMA4
     /* A operand of the 4 x 4 blocks: every block takes the same 4 x 4 block of
      * A^T, aop4[so][si] = A^T[4so + r][4si + k] = A(4si + k, 4so + r) with
      * r = lane & 3, k = lane >> 4 */
@@ -154,17 +151,6 @@ lks_prod_kernel(const DevArgs a)
             const int i = 4 * si + (lane >> 4), j = 4 * so + (lane & 3);
             aop4[so][si] = (i < K && j < K) ? a.A_ij[d + S * ((int64_t)i + (int64_t)K * j)] : 0.0;
         }
-#else
-    /* A operand: Aop[rt][kk] = A^T[j][i] = A(i, j), i = 4kk + (lane >> 4), j = 16rt + (lane & 15) */
-    double aop[RT][KSM];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int kk = 0; kk < KSM; ++kk) {
-            const int i = 4 * kk + (lane >> 4), j = 16 * rt + (lane & 15);
-            aop[rt][kk] = (i < K && j < K) ? a.A_ij[d + S * ((int64_t)i + (int64_t)K * j)] : 0.0;
-        }
-#endif
     __syncthreads();
     /* Renormalisation cadence: a column is renormalised (its max to [1/2, 1),
      * an exact power of two) every kLksRenorm-th step where the pair bounds the
@@ -173,13 +159,19 @@ lks_prod_kernel(const DevArgs a)
      * most K per step), else every step ("dense": Gaussian emissions, or a NaN /
      * unsafe draw).  Power-of-two scalings are exact, and every column is
      * renormalised after its last step, so M'_c and its exponents are the same
-     * bits at either cadence. */
+     * bits at either cadence up to the subnormal floor: between
+     * renormalisations the max stays above b^3 >= 2^-117, and only an entry
+     * ~2^-900 below it can lose bits sooner than under per-step
+     * renormalisation (far below the 1e-250 tolerance floor).  The growth bound
+     * needs A and phi entries <= 1, which the test below also requires. */
     bool dense = GS;
     if constexpr (!GS) {
         const int jr = lane < K ? lane : 0; /* lane = state: its phi column, A row and A column */
-        double emin = 1.0 / 0.0, rmax = 0.0, cmax = 0.0;
-        for (int l = 0; l < a.L; ++l)
+        double emin = 1.0 / 0.0, emax = 0.0, rmax = 0.0, cmax = 0.0;
+        for (int l = 0; l < a.L; ++l) {
             emin = fmin(emin, tab[l * KR + jr]);
+            emax = fmax(emax, tab[l * KR + jr]);
+        }
         for (int i = 0; i < K; ++i) {
             rmax = fmax(rmax, a.A_ij[d + S * ((int64_t)jr + (int64_t)K * i)]);
             cmax = fmax(cmax, a.A_ij[d + S * ((int64_t)i + (int64_t)K * jr)]);
@@ -191,7 +183,9 @@ lks_prod_kernel(const DevArgs a)
             ge = fmin(ge, __shfl_xor(ge, o));
             gm = fmin(gm, __shfl_xor(gm, o));
         }
-        const bool bad = !(ge * gm >= kLRenormSafeBound) || (lane < K && !(emin * fmin(rmax, cmax) >= 0.0));
+        /* the growth bound (at most K per step) needs every A and phi entry <= 1 */
+        const bool big = lane < K && !(emax <= 1.0 && fmax(rmax, cmax) <= 1.0);
+        const bool bad = !(ge * gm >= kLRenormSafeBound) || (lane < K && !(emin * fmin(rmax, cmax) >= 0.0)) || big;
         dense = __builtin_amdgcn_readfirstlane((int)(__ballot(bad) != 0)) != 0;
     }
 
@@ -260,7 +254,6 @@ lks_prod_kernel(const DevArgs a)
                 break;
             /* D = A^T Q for every tile (independent accumulators interleaved);
              * accv(u, kk): state 4kk + (lane >> 4) of the lane's column */
-#if HHMM_LKS_MFMA4
             double acc4[TPW][KSM];
 #pragma unroll
             for (int u = 0; u < TPW; ++u)
@@ -281,25 +274,6 @@ lks_prod_kernel(const DevArgs a)
                 }
             }
             auto accv = [&](int u, int kk) -> double { return acc4[u][kk]; };
-#else
-            lks_d4 acc[TPW][RT];
-#pragma unroll
-            for (int u = 0; u < TPW; ++u)
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt)
-                    acc[u][rt] = lks_d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int kk = 0; kk < KSM; ++kk) {
-                if (kk < ks) {
-#pragma unroll
-                    for (int u = 0; u < TPW; ++u)
-#pragma unroll
-                        for (int rt = 0; rt < RT; ++rt)
-                            acc[u][rt] = lks_mfma(aop[rt][kk], q[u][kk], acc[u][rt]);
-                }
-            }
-            auto accv = [&](int u, int kk) -> double { return acc[u][kk >> 2][kk & 3]; };
-#endif
             /* emission of the column's step, renormalisation of the column */
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
@@ -1035,8 +1009,6 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         return HHMM_ERR_UNSUPPORTED;
     }
     const int gpb = threads / G;
-    const int gpb_fb = threads / (G * lk_fb_split<G>()); /* lk_fb_kernel: pairs (or chunks) per workgroup */
-    const int gpb_vit = threads / (G * lk_vit_split<G>());
     if (a.seg_phase) {
         /* one window of a series split over ranks along T (hhmm_segment):
          * phase 1 + the window's summary, or phases 2 + 3 from the caller's
@@ -1056,7 +1028,7 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
             hipLaunchKernelGGL((lks_bound_kernel<KM, GS>), dim3((unsigned)a.P), dim3(64), 0, st, a);
             const int64_t nq = a.P * (int64_t)a.scan_nc;
             if (out & (fb & ~HHMM_OUT_LOGLIK))
-                hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb_fb - 1) / gpb_fb)),
+                hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)),
                                    dim3(threads), lk_lds<G>(a, threads, discrete), st, a);
         }
         const hipError_t e = hipGetLastError();
@@ -1078,7 +1050,7 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
             return r;
     }
     if (out & vit)
-        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), dim3((unsigned)((a.P + gpb_vit - 1) / gpb_vit)), dim3(threads),
+        hipLaunchKernelGGL((lk_viterbi_kernel<MODEL, G, KM>), dim3((unsigned)((a.P + gpb - 1) / gpb)), dim3(threads),
                            lk_lds<G>(a, threads, discrete), vs, a);
     hipError_t e = hipGetLastError();
     if ((out & ffbs) && e == hipSuccess) {
@@ -1108,7 +1080,7 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         hipLaunchKernelGGL((lks_bound_kernel<KM, GS>), dim3((unsigned)a.P), dim3(64), 0, st, a);
         const int64_t nq = a.P * (int64_t)a.scan_nc;
         if (out & (fb & ~HHMM_OUT_LOGLIK)) /* the chunks' sweeps: posteriors (the loglik is phase 2's) */
-            hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb_fb - 1) / gpb_fb)), dim3(threads),
+            hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((nq + gpb - 1) / gpb)), dim3(threads),
                                lk_lds<G>(a, threads, discrete), st, a);
         e = hipGetLastError();
     } else if ((out & fb) && mfma_fb && e == hipSuccess) {
@@ -1118,7 +1090,7 @@ static hhmm_status run_large_model(const DevArgs &a, hipStream_t st)
         hipLaunchKernelGGL((lkm_fb_kernel<RT, KSM>), dim3((unsigned)((waves + 3) / 4)), dim3(256), plds, st, a);
         e = hipGetLastError();
     } else if ((out & fb) && e == hipSuccess) {
-        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((a.P + gpb_fb - 1) / gpb_fb)), dim3(threads),
+        hipLaunchKernelGGL((lk_fb_kernel<MODEL, G, KM>), dim3((unsigned)((a.P + gpb - 1) / gpb)), dim3(threads),
                            lk_lds<G>(a, threads, discrete), st, a);
         e = hipGetLastError();
     }

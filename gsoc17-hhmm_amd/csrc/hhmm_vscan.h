@@ -54,22 +54,14 @@
 namespace hhmm {
 
 constexpr int32_t kVsTie = 1 << 30;     /* vs_k: a grid rounding tie inside the chunk */
-#ifndef HHMM_VS_APPROX_F32
-#define HHMM_VS_APPROX_F32 1 /* the approximate product pass in float */
-#endif
-/* Discrete models' tie products inside the grid pass (1) or in
- * vs_prod_tie_kernel (0).  Out of line the grid pass drops from 293 VGPRs and
- * 31k instructions to ~125 VGPRs: the first out-of-line version launched the
- * tie kernel over every (pair, chunk, parity) lane and cost more at C5 than the
- * occupancy gained (14.17 against 13.78 ms, profiles/r02zl_ab_c5.log); the grid
- * pass can append its tie chunks to a list (vs_tl: an atomic count, then
- * lane ids g = p + P c) for the tie kernel to walk (round 3), but that too
- * measured slower at C5: 15.21 against 13.52 ms inline, interleaved on one box
- * (profiles/r03j_ab_c5.log).  Inline stays the default; Gaussian models
- * always use the list. */
-#ifndef HHMM_VS_TIE_INLINE
-#define HHMM_VS_TIE_INLINE 1
-#endif
+/* Discrete models' tie products run inside the grid pass.  Out of line the
+ * grid pass drops from 293 VGPRs and 31k instructions to ~125 VGPRs: the first
+ * out-of-line version launched the tie kernel over every (pair, chunk, parity)
+ * lane and cost more at C5 than the occupancy gained (14.17 against 13.78 ms,
+ * profiles/r02zl_ab_c5.log); a list the tie kernel walks (round 3) measured
+ * slower too: 15.21 against 13.52 ms inline, interleaved on one box
+ * (profiles/r03j_ab_c5.log).  Gaussian models always use the list (a tie shows
+ * up during their pass). */
 constexpr int32_t kVsNoGrid = -(1 << 20); /* vs_k: no finite magnitude estimate */
 constexpr int32_t kVsSeq = -(1 << 21);    /* vs_k after the exact scan: the chunk was decoded step by step */
 
@@ -262,7 +254,7 @@ __device__ __forceinline__ void vs_tie_product(const DevArgs &a, const VsLane &v
 
 /* The tie chunks' two parity products, one lane per parity, for the chunks
  * the grid pass flagged (kVsTie): Gaussian emissions (a tie shows up during
- * the pass), and discrete models when HHMM_VS_TIE_INLINE is 0. */
+ * the pass). */
 constexpr int kVsTieBlocks = 512;
 template <int MODEL, int K>
 __global__ void __launch_bounds__(kBlock) vs_prod_tie_kernel(const DevArgs a)
@@ -360,15 +352,10 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
                 any = any || vs_term(e.x, iu).tie || (2 * kp + 1 < K && vs_term(e.y, iu).tie);
             }
         if (any) {
-            /* the two parity products (HHMM_VS_TIE_INLINE) */
-            if (HHMM_VS_TIE_INLINE) {
-                vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 0.0, a.vs_m);
-                vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 1.0, a.vs_m1);
-            }
-            if (HHMM_VS_TIE_INLINE)
-                a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
-            else
-                vs_list_tie(a, v, kc);
+            /* the two parity products, inline */
+            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 0.0, a.vs_m);
+            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 1.0, a.vs_m1);
+            a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
             return;
         }
     }
@@ -383,7 +370,7 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
      * chunk's entry for the exact pass, which checks it: its products run in
      * float (half the registers; the exact scan decodes a chunk whose entry
      * misses the predicted binade step by step) */
-    using V = typename std::conditional<GRID || !HHMM_VS_APPROX_F32, double, float>::type;
+    using V = typename std::conditional<GRID, double, float>::type;
     V Av[K][K];
 #pragma unroll
     for (int i = 0; i < K; ++i)
@@ -1428,7 +1415,7 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
         else
             hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K, true>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, true>), gc, bc, lds_c, st, a);
-        if (ModelTraits<MODEL>::kGauss || !HHMM_VS_TIE_INLINE) /* the listed tie chunks */
+        if (ModelTraits<MODEL>::kGauss) /* the listed tie chunks */
             hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3(kVsTieBlocks), bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_scan1_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_replay_kernel<MODEL, K>), gc, bc, lds_c, st, a);

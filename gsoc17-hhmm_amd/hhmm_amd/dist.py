@@ -160,7 +160,9 @@ def gqs_tsplit(model, data, draws, pars, group=None, pairing="grid", lib=None):
 
     Returns (window, outputs, loglik): window = (t0, t1); outputs = the
     window's requested [P, t1 - t0, ...] arrays (P-first, as api.PreparedRequest
-    lays them out); loglik = the whole series' log-likelihood per pair (every
+    lays them out) and "pair_status" [P] (HHMM_PAIR_INVALID_DATA where any
+    rank's window breaks a data-block bound: its summary carries a NaN log
+    scale, and loglik is NaN for that pair); loglik = the whole series' log-likelihood per pair (every
     rank computes it from the same gathered summaries)."""
     import torch
     import torch.distributed as dist

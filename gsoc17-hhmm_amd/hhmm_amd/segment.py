@@ -145,7 +145,8 @@ class SegmentWindow:
     def finish(self, enter=None, leave=None):
         """enter / leave: [K + 1, P] float64 (device or host) for a window that
         is not first / not last.  Returns the window's outputs as host arrays
-        shaped like api.gqs before reshaping (P-first, Fortran order)."""
+        shaped like api.gqs before reshaping (P-first, Fortran order), and
+        "pair_status" [P]."""
         import torch
         keep = []
 
@@ -166,6 +167,9 @@ class SegmentWindow:
             flat = np.frombuffer(t.cpu().numpy().tobytes(), dtype=arr.dtype)
             out[name] = np.ndarray(arr.shape, dtype=arr.dtype, buffer=flat.copy(),
                                    order="F" if arr.flags.f_contiguous else "C")
+        # per pair: HHMM_PAIR_INVALID_DATA where this window's data, or a chained
+        # summary of another window (a NaN log scale), breaks a data-block bound
+        out["pair_status"] = self.status.cpu().numpy()
         return out
 
 

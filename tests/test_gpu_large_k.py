@@ -74,7 +74,7 @@ def test_gamma_only_large_K_ragged(engine, oracle, K):
 def test_gamma_only_large_K_disjoint_filters(engine, oracle):
     """alpha and beta nearly disjoint (states that the forward pass makes
     improbable are the ones the backward pass favours) so the product's sum
-    drops below 2^-960 and the gamma-only branch takes the reference's
+    drops below kGammaDirect = 2^-240 (hhmm_internal.h) and the gamma-only branch takes the reference's
     normalised-vector formula."""
     K = 12
     data, draws = synth.hmm_multinom(N=1, S=4, T=600, K=K, L=9)

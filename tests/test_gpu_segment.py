@@ -150,3 +150,41 @@ def test_two_ranks_gqs_tsplit(engine, oracle, tmp_path, model, kw):
     compare("loglik", parts[1]["loglik"], ref["loglik"])
     gamma = np.concatenate([p["gamma"] for p in parts], axis=1)
     compare("gamma_tk", gamma, ref["gamma_tk"])
+
+
+@pytest.mark.parametrize("bad_window", [0, 1, 2])
+@pytest.mark.parametrize("model,K", [("hmm-multinom", 4), ("hmm-multinom", 12)])
+def test_segment_bad_data_in_one_window(engine, oracle, model, K, bad_window):
+    """an out-of-range symbol in ONE window's slice of one
+    series.  Its summary carries a NaN log scale, so every window's finish call
+    flags that series' pairs HHMM_PAIR_INVALID_DATA (not only the window that
+    holds the bad step) and the chained loglik is NaN there; every other pair
+    is OK and equal to the clean run."""
+    from hhmm_amd import _abi, segment
+    data, draws = synth.hmm_multinom(N=3, S=2, T=600, K=K, L=9)
+    bad = {k: (np.array(v, copy=True) if k == "x" else v) for k, v in data.items()}
+    R = 3
+    wins = segment.windows(600, R)
+    t0, t1 = wins[bad_window]
+    bad["x"][1, (t0 + t1) // 2] = 10  # L + 1, series n = 1
+    pars = ["loglik", "gamma_tk"]
+
+    def run(d):
+        runs = [segment.SegmentWindow(engine, model, segment.slice_time(d, a, b), draws, pars, i == 0, i == R - 1)
+                for i, (a, b) in enumerate(wins)]
+        sums = [w.summary().cpu().numpy() for w in runs]
+        enter, leave, loglik = segment.boundaries(sums, K)
+        return [w.finish(enter[i], leave[i]) for i, w in enumerate(runs)], loglik
+
+    clean, ll_clean = run(data)
+    got, ll_bad = run(bad)
+    S = 2
+    series = np.arange(3 * S) // S  # grid pairing: p = s + S n
+    hit = series == 1
+    for i in range(R):
+        st = got[i]["pair_status"]
+        assert np.all(st[hit] == _abi.PAIR_INVALID_DATA), (i, st)
+        assert np.all(st[~hit] == _abi.PAIR_OK), (i, st)
+        assert np.all(clean[i]["pair_status"] == _abi.PAIR_OK)
+        assert np.array_equal(got[i]["gamma_tk"][~hit], clean[i]["gamma_tk"][~hit])
+    assert np.all(np.isnan(ll_bad[hit])) and np.array_equal(ll_bad[~hit], ll_clean[~hit])

@@ -3,15 +3,17 @@
 (VERDICT r4 item 2): `bench.py --gpus 1 --steps K --warmup W` run as
 `rocprofv3 --kernel-trace --stats --output-format csv -d DIR -o trace -- python3 bench.py ...`.
 
-  python tools/trace_vs_line.py gpurun_out/TAG/bench_traced.json gpurun_out/TAG/trace TAG
+  python tools/trace_vs_line.py gpurun_out/TAG/bench_traced.json gpurun_out/TAG/trace TAG [OUT.json]
 
 The bench launches the roofline kernel W times (warm-up), K times (the timed
 steps, each bracketed by HIP events on the launch stream: the line's
 roofline.duration_ms is their mean) and then the other schedules once each
 after the timed region.  The dominant kernel's dispatches in the trace are
 therefore [W warm-up][K timed][rest]; this script takes the K timed ones,
-recomputes the roofline fraction from their mean duration, and writes
-profiles/TAG_trace_vs_line.json with both figures and their ratio.
+recomputes the roofline fraction from their mean duration, and writes one
+JSON object with both figures and their ratio to OUT.json (default
+gpurun_out/TAG/trace_vs_line.json; copy it into profiles/ to commit it), replacing
+the file, never appending to it.
 """
 import csv
 import glob
@@ -66,8 +68,12 @@ def main():
         "line_ms_per_step": line["ms_per_step"],
         "line_value": line["value"],
     }
-    dst = ROOT / "profiles" / f"{tag}_trace_vs_line.json"
-    dst.write_text(json.dumps(out, indent=1) + "\n")
+    dst = pathlib.Path(sys.argv[4]) if len(sys.argv) > 4 else ROOT / "gpurun_out" / tag / "trace_vs_line.json"
+    dst.parent.mkdir(parents=True, exist_ok=True)
+    tmp = dst.with_suffix(".tmp")
+    tmp.write_text(json.dumps(out, indent=1) + "\n")
+    json.loads(tmp.read_text())
+    tmp.replace(dst)
     print(json.dumps({k: v for k, v in out.items() if k != "timed_dispatch_ms"}, indent=1))
 
 
