@@ -64,12 +64,14 @@ def parse():
     ap.add_argument("--check-at", default="after", choices=["after", "before"],
                     help="C2: the oracle check on the last timed step's outputs (after) or between the warmup "
                          "and the timed steps (before: the device idles while the host checks)")
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "n1", "n2", "f1"],
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c2-host", "c3", "c4", "c5", "n1", "n2", "f1"],
                     help="c2 (default, the metric's config) or one of the other BASELINE configs, each "
                          "printed as its own line: c1 hmm Gaussian K=3 T=500, c3 iohmm-reg grid, c4 iohmm-hmix "
                          "+ FFBS, c5 Tayal T=1e6 (parallel scan over T); n1 = hmm-multinom at K=23 (SURVEY §8 N1); "
                          "n2 = hmm-multinom K=23, T=1e6, 250 pairs (the large-K parallel scan, MFMA chunk products); "
-                         "f1 = the tick -> leg feature extractor (SURVEY §8 F1)")
+                         "f1 = the tick -> leg feature extractor (SURVEY §8 F1); c2-host = the C2 request "
+                         "through hhmm_run from pageable host arrays to host arrays (the R .Call path, "
+                         "SURVEY §8b; --pairs defaults to 200000 there)")
     ap.add_argument("--ticks", type=int, default=100_000_000, help="f1: ticks per GPU")
     ap.add_argument("--pars", default=None,
                     help="c3-c5 probes: comma-separated outputs instead of the workload's")
@@ -463,6 +465,8 @@ def main():
         assert lib.hhmm_init(1) == 0, lib.hhmm_last_error().decode()
         if a.workload == "f1":
             return features_workload(a, lib, rk)
+        if a.workload == "c2-host":
+            return c2_host_workload(a, lib, rk)
         if a.workload != "c2":
             return other_workload(a, lib, rk)
         return c2_workload(a, lib, rk)
@@ -579,6 +583,143 @@ def c2_workload(a, lib, rk):
         }
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(T, a.cpu_seconds, a.seed)
+        print(json.dumps(line), flush=True)
+
+
+def link_rates(dev, nbytes=1 << 30, reps=3):
+    """Pinned host <-> device copy rates (B/s) of one nbytes buffer, each way
+    alone and both ways at once (PCIe is full duplex)."""
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    h2 = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    out = {}
+    for name in ("h2d", "d2h", "both"):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            if name in ("h2d", "both"):
+                with torch.cuda.stream(s1):
+                    d.copy_(h, non_blocking=True)
+            if name in ("d2h", "both"):
+                with torch.cuda.stream(s2):
+                    h2.copy_(d2, non_blocking=True)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        out[name] = nbytes / min(ts)
+    del h, h2, d, d2
+    return out
+
+
+def c2_host_workload(a, lib, rk):
+    """The C2 request (hmm-multinom K=4, gamma_tk + loglik + zstar_t +
+    logp_zstar) through hhmm_run: pageable host arrays in, pageable host arrays
+    out, as R's .Call hands over REAL() buffers (SURVEY §8b).  The library's
+    host pipeline (HHMM_FLAG_HOST_CHUNKS, automatic) overlaps chunk i+1's
+    upload and kernels with chunk i's download; the line states the bound the
+    host link sets and the one-chunk (no overlap) time beside it."""
+    world, rank, dev = rk.world, rk.rank, rk.dev
+    P = a.pairs if a.pairs != 1_000_000 else 200_000
+    T = a.T
+    x_d, draws_d = make_batch(P, T, a.seed + 7919 * rank, dev)
+    x = x_d.cpu().numpy()
+    draws = {k: v.cpu().numpy() for k, v in draws_d.items()}
+    out = {
+        "loglik": np.empty(P, dtype=np.float64),
+        "gamma_tk": np.empty((K, T, P), dtype=np.float64),
+        "zstar_t": np.empty((T, P), dtype=np.int32),
+        "logp_zstar": np.empty(P, dtype=np.float64),
+    }
+    status = np.zeros(P, dtype=np.int32)
+
+    def request(flags):
+        r = _abi.Request()
+        r.abi_version = _abi.ABI_VERSION
+        r.model = _abi.MODELS["hmm-multinom"]
+        r.pairing = _abi.PAIR_ZIP
+        r.device = -1
+        r.flags = flags
+        r.data.n_series, r.data.T_max, r.data.K, r.data.L = P, T, K, L
+        r.data.x_int = x.ctypes.data
+        r.draws.n_draws = P
+        for k, v in draws.items():
+            setattr(r.draws, k, v.ctypes.data)
+        res = _abi.Result()
+        for o, arr in out.items():
+            r.outputs |= _abi.OUT[o]
+            setattr(res, o, arr.ctypes.data)
+        res.pair_status = status.ctypes.data
+        return r, res
+
+    def call(flags):
+        r, res = request(flags)
+        st = lib.hhmm_run(C.byref(r), C.byref(res))
+        if st < 0:
+            raise RuntimeError(lib.hhmm_last_error().decode())
+
+    rates = link_rates(dev)
+    fresh_t0 = time.perf_counter()
+    call(0)  # first call: pinned staging and device buffers come from the library's pools after this
+    first_s = time.perf_counter() - fresh_t0
+    for _ in range(max(0, a.warmup - 1)):
+        call(0)
+    elapsed_rank, elapsed, per_rank = timed_region(rk, lambda i: call(0), a.steps, 0)
+    one_chunk = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        call(_abi.flag_host_chunks(1))
+        one_chunk.append(time.perf_counter() - t0)
+    # the same request on the device entry: bit-identical outputs
+    run = DeviceRun(lib, x_d, draws_d, P, T, dev)
+    run.launch("step")
+    torch.cuda.synchronize(dev)
+    same = {
+        "loglik": bool(np.array_equal(run.out["loglik"].cpu().numpy(), out["loglik"])),
+        "logp_zstar": bool(np.array_equal(run.out["logp_zstar"].cpu().numpy(), out["logp_zstar"])),
+        "zstar_t": bool(np.array_equal(run.out["zstar_t"].cpu().numpy(), out["zstar_t"])),
+        "gamma_tk": bool(np.array_equal(run.out["gamma_tk"].cpu().numpy(), out["gamma_tk"])),
+        "pair_status": bool(np.array_equal(run.out["pair_status"].cpu().numpy(), status)),
+    }
+    del run
+    up = x.nbytes + sum(v.nbytes for v in draws.values())
+    down = sum(v.nbytes for v in out.values()) + status.nbytes
+    t_bound = max(up / rates["h2d"], down / rates["d2h"])
+    if rank == 0:
+        value = world * P * T * a.steps / elapsed
+        step_s = elapsed / a.steps
+        line = {
+            "metric": "series-timesteps/sec forward-backward+Viterbi (K=4), host arrays to host arrays "
+                      "(hhmm_run, the R .Call path)",
+            "value": value,
+            "unit": "series-timesteps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": step_s * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded HMM of hmm/main-multinom-semisup.R, Dirichlet-jittered draws), pageable "
+                    "numpy arrays",
+            "config": {"workload": f"C2-host hmm-multinom K=4 L=9, {P} pairs x T={T} per GPU (zip), "
+                                   "gamma_tk zstar_t loglik logp_zstar, host to host",
+                       "pairs_per_gpu": P, "T": T, "parallelism": f"pairs sharded over {world} GPU(s)"},
+            "host_link": {"bytes_up": up, "bytes_down": down,
+                          "pinned_GBps": {k: v / 1e9 for k, v in rates.items()},
+                          "bound_ms": t_bound * 1e3,
+                          "frac_of_link_bound": t_bound / step_s,
+                          "end_to_end_GBps": (up + down) / step_s / 1e9,
+                          "bound": "max(bytes_up / pinned H2D rate, bytes_down / pinned D2H rate): the "
+                                   "transfers overlapped, each at the rate torch's pinned copy reaches"},
+            "one_chunk_ms": [t * 1e3 for t in one_chunk],
+            "first_call_ms": first_s * 1e3,
+            "bit_identical_to_device_entry": same,
+            "library": lib.hhmm_version().decode(),
+            "rank_ms_per_step": [v / a.steps * 1e3 for v in per_rank],
+        }
         print(json.dumps(line), flush=True)
 
 

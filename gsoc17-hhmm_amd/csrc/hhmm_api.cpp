@@ -601,19 +601,7 @@ static ShardRows shard_rows(const void *host, const ArrayDesc &a, const Shard &s
     return ShardRows{(char *)host + (size_t)sh.off[a.cls] * es, a.elems / lead, cnt * es, lead * es};
 }
 
-/* Host <-> device copy of one array's shard: rows of cnt elements at a pitch
- * of lead on the host, packed on the device. */
-static hipError_t copy_shard(void *dev, const void *host, const ArrayDesc &a, const Shard &sh, bool to_device)
-{
-    const ShardRows r = shard_rows(host, a, sh);
-    if (r.width == r.pitch)
-        return to_device ? hipMemcpy(dev, r.base, r.rows * r.width, hipMemcpyHostToDevice)
-                         : hipMemcpy(r.base, dev, r.rows * r.width, hipMemcpyDeviceToHost);
-    return to_device ? hipMemcpy2D(dev, r.width, r.base, r.pitch, r.width, r.rows, hipMemcpyHostToDevice)
-                     : hipMemcpy2D(r.base, r.pitch, dev, r.width, r.width, r.rows, hipMemcpyDeviceToHost);
-}
-
-/* copy_shard's host-only twin for hhmm_selftest_shards (memcpy per row). */
+/* A shard's rows packed / unpacked on the host for hhmm_selftest_shards (memcpy per row). */
 static void copy_shard_host(void *packed, const void *host, const ArrayDesc &a, const Shard &sh, bool to_packed)
 {
     const ShardRows r = shard_rows(host, a, sh);
@@ -626,9 +614,251 @@ static void copy_shard_host(void *packed, const void *host, const ArrayDesc &a, 
     }
 }
 
-/* Runs one shard of a host request on the current device: uploads its slices,
- * launches, downloads its output slices in place.  status: the caller's
- * [P] host array, written at the shard's pairs; *failures counts them. */
+/* ---------------- the R path: a pipelined host request ----------------
+ * hhmm_run's caller hands over pageable host arrays (R's REAL() buffers,
+ * SURVEY §8b).  A device's shard is split into chunks of series (or draws),
+ * and chunk i's upload and kernels overlap chunk i-1's download: per device
+ * three non-blocking streams (upload, compute, download), two slots of
+ * device buffers and two pinned staging slots per direction.  The host thread
+ * gathers chunk i's input rows into a pinned slot (threads over rows), the
+ * upload stream DMAs the slot to the device in one copy, the compute stream
+ * runs the chunk's sub-request, the download stream DMAs its outputs and
+ * pair_status into the other pinned slot in one copy, and the host thread
+ * scatters chunk i-1's rows into the caller's arrays meanwhile.  Every array
+ * of a chunk sits at the same offset in its device slot and its pinned slot,
+ * so each direction is one DMA per chunk. */
+
+struct HostPool { /* pinned staging blocks, reused across calls (hhmm_shutdown frees them) */
+    std::mutex mu;
+    std::multimap<size_t, void *> free_blocks;
+    std::map<void *, size_t> live;
+};
+static HostPool &host_pool()
+{
+    static HostPool p;
+    return p;
+}
+static void *host_get(size_t bytes)
+{
+    bytes = (std::max<size_t>(bytes, 4096) + 4095) & ~(size_t)4095;
+    HostPool &p = host_pool();
+    {
+        std::lock_guard<std::mutex> g(p.mu);
+        auto it = p.free_blocks.lower_bound(bytes);
+        if (it != p.free_blocks.end() && it->first <= bytes + bytes / 4) {
+            void *ptr = it->second;
+            p.live[ptr] = it->first;
+            p.free_blocks.erase(it);
+            return ptr;
+        }
+    }
+    void *ptr = nullptr;
+    if (hipHostMalloc(&ptr, bytes, hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(p.mu);
+    p.live[ptr] = bytes;
+    return ptr;
+}
+static void host_put(void *ptr)
+{
+    if (!ptr)
+        return;
+    HostPool &p = host_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    auto it = p.live.find(ptr);
+    if (it == p.live.end())
+        return;
+    p.free_blocks.emplace(it->second, ptr);
+    p.live.erase(it);
+}
+static void host_release_all()
+{
+    HostPool &p = host_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    for (auto &kv : p.free_blocks)
+        (void)hipHostFree(kv.second);
+    p.free_blocks.clear();
+}
+
+struct PipeStreams {
+    std::mutex mu;
+    std::map<int, std::vector<hipStream_t>> by_dev; /* upload, compute, download */
+};
+static PipeStreams &pipe_streams()
+{
+    static PipeStreams s;
+    return s;
+}
+static hhmm_status get_pipe_streams(int dev, hipStream_t (&st)[3])
+{
+    PipeStreams &ps = pipe_streams();
+    std::lock_guard<std::mutex> g(ps.mu);
+    auto it = ps.by_dev.find(dev);
+    if (it == ps.by_dev.end()) {
+        std::vector<hipStream_t> v(3, nullptr);
+        for (auto &x : v)
+            if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) {
+                set_error("device %d: stream creation failed", dev);
+                return HHMM_ERR_HIP;
+            }
+        it = ps.by_dev.emplace(dev, v).first;
+    }
+    for (int i = 0; i < 3; ++i)
+        st[i] = it->second[(size_t)i];
+    return HHMM_OK;
+}
+
+/* rows x width bytes between pitched buffers, split over host threads when
+ * the copy is large (the staging copies run beside the GPU's DMA) */
+static void par_copy_rows(char *dst, size_t dpitch, const char *src, size_t spitch, size_t width, size_t rows)
+{
+    const size_t total = width * rows;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = total < ((size_t)8 << 20) ? 1 : std::min<size_t>(std::min(8u, hw), std::max<size_t>(rows, 1));
+    auto run = [&](size_t r0, size_t r1) {
+        if (dpitch == width && spitch == width) {
+            memcpy(dst + r0 * width, src + r0 * width, (r1 - r0) * width);
+            return;
+        }
+        for (size_t r = r0; r < r1; ++r)
+            memcpy(dst + r * dpitch, src + r * spitch, width);
+    };
+    if (nt <= 1) {
+        run(0, rows);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < nt; ++i)
+        th.emplace_back(run, rows * i / nt, rows * (i + 1) / nt);
+    run(0, rows / nt);
+    for (auto &t : th)
+        t.join();
+}
+
+/* A chunk: its shard, its sub-request, and where each array sits in the slot. */
+struct ChunkLayout {
+    Shard sh;
+    std::vector<size_t> off;   /* per array of `arrays`, bytes from the slot base */
+    size_t status_off = 0;
+    size_t in_end = 0;         /* [0, in_end): uploaded */
+    size_t out_begin = 0;      /* [out_begin, total): downloaded */
+    size_t total = 0;
+    int64_t P = 0;
+};
+
+static size_t shard_bytes(const ArrayDesc &a, const Shard &sh)
+{
+    return a.elems / (size_t)sh.lead[a.cls] * (size_t)sh.cnt[a.cls] * a.esize;
+}
+
+static ChunkLayout chunk_layout(const hhmm_request *req, const std::vector<ArrayDesc> &arrays, const Shard &sh,
+                                bool ragged)
+{
+    ChunkLayout L;
+    L.sh = sh;
+    hhmm_request r = *req;
+    r.data.n_series = sh.cnt[SERIES];
+    r.draws.n_draws = sh.cnt[DRAWS];
+    L.P = npairs(&r);
+    L.off.assign(arrays.size(), 0);
+    size_t o = 0;
+    auto place = [&](size_t bytes) {
+        const size_t at = o;
+        o += (bytes + 255) & ~(size_t)255;
+        return at;
+    };
+    for (size_t i = 0; i < arrays.size(); ++i) /* inputs first */
+        if (!arrays[i].output)
+            L.off[i] = place(shard_bytes(arrays[i], sh));
+    const size_t outs = o;
+    for (size_t i = 0; i < arrays.size(); ++i)
+        if (arrays[i].output)
+            L.off[i] = place(shard_bytes(arrays[i], sh));
+    L.status_off = place((size_t)L.P * sizeof(int32_t));
+    L.total = o;
+    /* outputs travel up too where padded steps must round-trip untouched */
+    L.in_end = ragged ? L.status_off : outs;
+    L.out_begin = outs;
+    return L;
+}
+
+/* Sub-shards of a device shard: `n` contiguous ranges of its units (series,
+ * or draws for a GRID request split by draws), each a Shard of the request. */
+static std::vector<Shard> split_shard(const hhmm_request *r, const Shard &sh, int64_t n)
+{
+    const int64_t S = r->draws.n_draws;
+    /* a GRID shard holding every series splits by draws (rows of the chunk's
+     * draws at a pitch of S pairs) when it is a draws shard already or has
+     * fewer series than chunks; every other shard splits by series */
+    const bool all_series = sh.cnt[SERIES] == r->data.n_series;
+    const bool draws_shard = sh.lead[PAIRS] == S && sh.cnt[DRAWS] < S;
+    const bool by_draws = r->pairing == HHMM_PAIR_GRID && all_series && (draws_shard || sh.cnt[SERIES] < n);
+    const int64_t u0 = by_draws ? sh.off[DRAWS] : sh.off[SERIES];
+    const int64_t units = by_draws ? sh.cnt[DRAWS] : sh.cnt[SERIES];
+    const int64_t ns = std::max<int64_t>(1, std::min(n, units));
+    std::vector<Shard> v;
+    for (int64_t i = 0; i < ns; ++i) {
+        const int64_t a = u0 + units * i / ns, b = u0 + units * (i + 1) / ns;
+        Shard c = sh;
+        if (by_draws) {
+            c.lead[PAIRS] = S;
+            c.off[DRAWS] = c.off[PAIRS] = a;
+            c.cnt[DRAWS] = c.cnt[PAIRS] = b - a;
+        } else {
+            const int64_t per = sh.cnt[SERIES] > 0 ? sh.cnt[PAIRS] / sh.cnt[SERIES] : 0; /* pairs per series */
+            const int64_t dper = sh.cnt[SERIES] > 0 ? sh.cnt[DRAWS] / sh.cnt[SERIES] : 0;
+            c.off[SERIES] = a;
+            c.cnt[SERIES] = b - a;
+            c.off[PAIRS] = sh.off[PAIRS] + (a - u0) * per;
+            c.cnt[PAIRS] = (b - a) * per;
+            if (r->pairing != HHMM_PAIR_GRID) { /* ZIP / BLOCK: the series' own draws */
+                c.off[DRAWS] = sh.off[DRAWS] + (a - u0) * dper;
+                c.cnt[DRAWS] = (b - a) * dper;
+            }
+        }
+        v.push_back(c);
+    }
+    return v;
+}
+
+/* Chunks of a device shard: about kChunkBytes of staged traffic each, with at
+ * least kChunkMinPairs pairs (256 waves) so a chunk's kernels still fill the
+ * chip, and only where the whole request runs no parallel scan over T: the
+ * chunks then take the same sequential recursions (SCAN_OFF / VIT_SCAN_OFF
+ * pin it) and the outputs are bit-identical to one device call.
+ * HHMM_FLAG_HOST_CHUNKS(n) asks for n chunks. */
+constexpr size_t kChunkBytes = (size_t)512 << 20;
+constexpr int64_t kChunkMinPairs = 16384;
+
+static int64_t choose_chunks(const hhmm_request *req, const std::vector<ArrayDesc> &arrays, const Shard &sh,
+                             bool ragged, bool &pin_flags)
+{
+    pin_flags = false;
+    const hhmm_data &d = req->data;
+    const int64_t Pw = npairs(req);
+    const bool seq = scan_plan(req->model, d.K, d.T_max, Pw, req->outputs, (uint32_t)req->flags).cl == 0 &&
+                     vscan_chunks(req->model, d.K, req->model == HHMM_MODEL_TAYAL_LITE ? d.T_oos_max : d.T_max, Pw,
+                                  req->outputs, (uint32_t)req->flags) == 0;
+    if (!seq)
+        return 1;
+    const int64_t forced = (int64_t)(((uint32_t)req->flags >> 20) & 0xffu);
+    size_t bytes = 0; /* staged bytes of the shard, both directions */
+    for (const ArrayDesc &a : arrays)
+        bytes += shard_bytes(a, sh) * ((a.output && ragged) ? 2 : 1);
+    const int64_t P = sh.cnt[PAIRS];
+    int64_t n = forced > 0 ? forced : (int64_t)((bytes + kChunkBytes - 1) / kChunkBytes);
+    if (forced == 0)
+        n = std::min<int64_t>(n, std::max<int64_t>(1, P / kChunkMinPairs));
+    n = std::max<int64_t>(1, n);
+    pin_flags = n > 1;
+    return n;
+}
+
+/* Runs one shard of a host request on the current device (the pipeline
+ * above).  status: the caller's [P] host array, written at the shard's pairs;
+ * *failures counts them. */
 static hhmm_status run_on_device(const hhmm_request *req, hhmm_result *res, const Shard &sh, int32_t *status,
                                  int64_t *failures)
 {
@@ -641,99 +871,181 @@ static hhmm_status run_on_device(const hhmm_request *req, hhmm_result *res, cons
     dres.pair_status = nullptr;
     std::vector<ArrayDesc> arrays;
     describe(req, res, &dreq, &dres, arrays);
-    dreq.data.n_series = sh.cnt[SERIES];
-    dreq.draws.n_draws = sh.cnt[DRAWS];
-    const int64_t P = npairs(&dreq);
-    if (P < 1) {
-        set_error("internal: shard describes no pairs");
-        return HHMM_ERR_INVALID_ARGUMENT;
-    }
     const bool ragged = req->data.T != nullptr || req->data.T_oos != nullptr;
-
-    std::vector<void *> owned;
+    bool pin = false;
+    const int64_t nch = choose_chunks(req, arrays, sh, ragged, pin);
+    const std::vector<Shard> chunks = split_shard(req, sh, nch);
+    std::vector<ChunkLayout> lay;
+    size_t slot_bytes = 0, in_bytes = 0, out_bytes = 0, wsb = 0;
+    for (const Shard &c : chunks) {
+        lay.push_back(chunk_layout(req, arrays, c, ragged));
+        const ChunkLayout &L = lay.back();
+        if (L.P < 1) {
+            set_error("internal: shard describes no pairs");
+            return HHMM_ERR_INVALID_ARGUMENT;
+        }
+        slot_bytes = std::max(slot_bytes, L.total);
+        in_bytes = std::max(in_bytes, L.in_end);
+        out_bytes = std::max(out_bytes, L.total - L.out_begin);
+        wsb = std::max(wsb, workspace_bytes(dreq.model, dreq.data.K, dreq.data.L, dreq.data.T_max,
+                                            dreq.data.T_oos_max, L.P, dreq.outputs, (uint32_t)dreq.flags,
+                                            c.cnt[SERIES], dreq.pairing));
+    }
+    if (pin)
+        dreq.flags |= (int32_t)(HHMM_FLAG_SCAN_OFF | HHMM_FLAG_VIT_SCAN_OFF);
+    const int nslot = chunks.size() > 1 ? 2 : 1;
+    hipStream_t st[3];
+    hhmm_status s = get_pipe_streams(dev, st);
+    if (s != HHMM_OK)
+        return s;
+    void *dslot[2] = {nullptr, nullptr}, *hin[2] = {nullptr, nullptr}, *hout[2] = {nullptr, nullptr};
+    void *ws = nullptr;
+    hipEvent_t ev[3][2] = {}; /* uploaded, computed, downloaded -- per slot */
     auto cleanup = [&]() {
-        for (void *p : owned)
-            pool_put(p);
+        for (int k = 0; k < 2; ++k) {
+            pool_put(dslot[k]);
+            host_put(hin[k]);
+            host_put(hout[k]);
+            for (int j = 0; j < 3; ++j)
+                if (ev[j][k])
+                    (void)hipEventDestroy(ev[j][k]);
+        }
+        pool_put(ws);
     };
-    for (auto &a : arrays) {
-        const size_t bytes = a.elems / (size_t)sh.lead[a.cls] * (size_t)sh.cnt[a.cls] * a.esize;
-        void *dp = pool_get(dev, bytes);
-        if (!dp) {
+    auto drain = [&]() { /* every stream of this request, the side stream included */
+        hipError_t r = hipSuccess;
+        for (int j = 0; j < 3; ++j) {
+            const hipError_t q = (j == 1) ? sync_request(st[1]) : hipStreamSynchronize(st[j]);
+            if (r == hipSuccess)
+                r = q;
+        }
+        return r;
+    };
+    for (int k = 0; k < nslot; ++k) {
+        dslot[k] = pool_get(dev, slot_bytes);
+        hin[k] = host_get(in_bytes);
+        hout[k] = host_get(out_bytes);
+        for (int j = 0; j < 3; ++j)
+            if (hipEventCreateWithFlags(&ev[j][k], hipEventDisableTiming) != hipSuccess)
+                ev[j][k] = nullptr;
+        if (!dslot[k] || !hin[k] || !hout[k] || !ev[0][k] || !ev[1][k] || !ev[2][k]) {
             cleanup();
-            set_error("device %d: allocation of %zu bytes failed", dev, bytes);
+            set_error("device %d: allocation of the host pipeline's buffers failed (%zu device, %zu + %zu pinned bytes)",
+                      dev, slot_bytes, in_bytes, out_bytes);
             return HHMM_ERR_OUT_OF_MEMORY;
         }
-        owned.push_back(dp);
-        *a.dev_slot = dp;
-        /* inputs always; outputs too when padded steps must round-trip untouched */
-        if (!a.output || ragged) {
-            e = copy_shard(dp, a.host, a, sh, true);
-            if (e != hipSuccess) {
-                cleanup();
-                return hip_fail(e, "hipMemcpy H2D");
-            }
-        }
     }
-    void *dstatus = pool_get(dev, (size_t)P * sizeof(int32_t));
-    if (!dstatus) {
-        cleanup();
-        set_error("device %d: allocation failed (pair_status)", dev);
-        return HHMM_ERR_OUT_OF_MEMORY;
-    }
-    owned.push_back(dstatus);
-    (void)hipMemset(dstatus, 0, (size_t)P * sizeof(int32_t));
-    dres.pair_status = (int32_t *)dstatus;
-
-    const size_t wsb = workspace_bytes(dreq.model, dreq.data.K, dreq.data.L, dreq.data.T_max, dreq.data.T_oos_max, P,
-                                       dreq.outputs, (uint32_t)dreq.flags, dreq.data.n_series, dreq.pairing);
-    void *ws = pool_get(dev, wsb);
+    ws = pool_get(dev, wsb);
     if (!ws) {
         cleanup();
         set_error("device %d: workspace allocation of %zu bytes failed", dev, wsb);
         return HHMM_ERR_OUT_OF_MEMORY;
     }
-    owned.push_back(ws);
 
-    hhmm_status s = launch_all(&dreq, &dres, P, ws, nullptr);
-    if (s != HHMM_OK) {
+    auto bind = [&](const ChunkLayout &L, int k, hhmm_request &cr, hhmm_result &cq) {
+        cr = dreq;
+        cq = dres;
+        cr.data.n_series = L.sh.cnt[SERIES];
+        cr.draws.n_draws = L.sh.cnt[DRAWS];
+        /* the device copies of the request's arrays: describe() recorded where
+         * each pointer lives in dreq / dres; the same field of cr / cq */
+        for (size_t i = 0; i < arrays.size(); ++i) {
+            const char *slot_base = (const char *)arrays[i].dev_slot;
+            void **f = nullptr;
+            if (slot_base >= (const char *)&dreq && slot_base < (const char *)(&dreq + 1))
+                f = (void **)((char *)&cr + (slot_base - (const char *)&dreq));
+            else
+                f = (void **)((char *)&cq + (slot_base - (const char *)&dres));
+            *f = (char *)dslot[k] + L.off[i];
+        }
+        cq.pair_status = (int32_t *)((char *)dslot[k] + L.status_off);
+    };
+    auto gather = [&](const ChunkLayout &L, int k) {
+        for (size_t i = 0; i < arrays.size(); ++i) {
+            const ArrayDesc &a = arrays[i];
+            if (L.off[i] >= L.in_end)
+                continue;
+            const ShardRows r = shard_rows(a.host, a, L.sh);
+            par_copy_rows((char *)hin[k] + L.off[i], r.width, r.base, r.pitch, r.width, r.rows);
+        }
+    };
+    int64_t fails = 0;
+    auto scatter = [&](const ChunkLayout &L, int k) {
+        for (size_t i = 0; i < arrays.size(); ++i) {
+            const ArrayDesc &a = arrays[i];
+            if (!a.output)
+                continue;
+            const ShardRows r = shard_rows(a.host, a, L.sh);
+            par_copy_rows(r.base, r.pitch, (const char *)hout[k] + (L.off[i] - L.out_begin), r.width, r.width,
+                          r.rows);
+        }
+        /* pair_status: [P] in the caller's layout (a PAIRS array of P elements) */
+        const ArrayDesc sa{status, nullptr, (size_t)npairs(req), sizeof(int32_t), true, PAIRS};
+        const ShardRows r = shard_rows(status, sa, L.sh);
+        const char *src = (const char *)hout[k] + (L.status_off - L.out_begin);
+        par_copy_rows(r.base, r.pitch, src, r.width, r.width, r.rows);
+        const int32_t *q = (const int32_t *)src;
+        for (int64_t p = 0; p < L.P; ++p)
+            fails += q[p] != 0;
+    };
+
+    hhmm_status ls = HHMM_OK;
+    const size_t n = chunks.size();
+    for (size_t i = 0; i < n && ls == HHMM_OK; ++i) {
+        const int k = (int)(i % (size_t)nslot);
+        const ChunkLayout &L = lay[i];
+        if (i >= (size_t)nslot && (e = hipEventSynchronize(ev[0][k])) != hipSuccess) /* pinned in-slot free */
+            break;
+        gather(L, k);
+        if (i >= (size_t)nslot && (e = hipStreamWaitEvent(st[0], ev[2][k], 0)) != hipSuccess) /* device slot free */
+            break;
+        if ((e = hipMemcpyAsync(dslot[k], hin[k], L.in_end, hipMemcpyHostToDevice, st[0])) != hipSuccess ||
+            (e = hipEventRecord(ev[0][k], st[0])) != hipSuccess || (e = hipStreamWaitEvent(st[1], ev[0][k], 0)) !=
+                                                                         hipSuccess ||
+            (e = hipMemsetAsync((char *)dslot[k] + L.status_off, 0, (size_t)L.P * sizeof(int32_t), st[1])) !=
+                hipSuccess)
+            break;
+        hhmm_request cr;
+        hhmm_result cq;
+        bind(L, k, cr, cq);
+        ls = launch_all(&cr, &cq, L.P, ws, st[1]);
+        if (ls != HHMM_OK)
+            break;
+        if ((e = hipEventRecord(ev[1][k], st[1])) != hipSuccess || (e = hipStreamWaitEvent(st[2], ev[1][k], 0)) !=
+                                                                        hipSuccess ||
+            (e = hipMemcpyAsync(hout[k], (char *)dslot[k] + L.out_begin, L.total - L.out_begin,
+                                hipMemcpyDeviceToHost, st[2])) != hipSuccess ||
+            (e = hipEventRecord(ev[2][k], st[2])) != hipSuccess)
+            break;
+        if (i >= 1) { /* the previous chunk's outputs, while this one uploads and runs */
+            const int kp = (int)((i - 1) % (size_t)nslot);
+            if ((e = hipEventSynchronize(ev[2][kp])) != hipSuccess)
+                break;
+            scatter(lay[i - 1], kp);
+        }
+    }
+    if (ls != HHMM_OK || e != hipSuccess) {
         /* a failed launch may follow one that is still running: drain this
          * request's streams before its pooled buffers can be handed to another
          * request; a sticky device error from an earlier fault is reported
          * beside the launch error instead of being buried under it */
-        e = sync_request(nullptr);
+        const std::string first = hhmm_last_error();
+        const hipError_t d = drain();
         cleanup();
-        if (e != hipSuccess) {
-            std::string first = hhmm_last_error();
-            set_error("%s; draining the request's streams then failed: %s", first.c_str(), hipGetErrorString(e));
-        }
-        return s;
+        if (ls == HHMM_OK)
+            return hip_fail(e, "host pipeline (copy or kernel execution)");
+        if (d != hipSuccess)
+            set_error("%s; draining the request's streams then failed: %s", first.c_str(), hipGetErrorString(d));
+        return ls;
     }
-    e = sync_request(nullptr);
+    e = drain();
     if (e != hipSuccess) {
         cleanup();
         return hip_fail(e, "kernel execution");
     }
-    for (auto &a : arrays) {
-        if (!a.output)
-            continue;
-        e = copy_shard(*a.dev_slot, a.host, a, sh, false);
-        if (e != hipSuccess) {
-            cleanup();
-            return hip_fail(e, "hipMemcpy D2H");
-        }
-    }
-    /* pair_status: [P] in the caller's layout (a PAIRS array of P elements) */
-    ArrayDesc st{status, nullptr, (size_t)npairs(req), sizeof(int32_t), true, PAIRS};
-    e = copy_shard(dstatus, status, st, sh, false);
+    scatter(lay[n - 1], (int)((n - 1) % (size_t)nslot));
     cleanup();
-    if (e != hipSuccess)
-        return hip_fail(e, "hipMemcpy D2H (status)");
-    const size_t lead = (size_t)sh.lead[PAIRS], cnt = (size_t)sh.cnt[PAIRS], rows = (size_t)npairs(req) / lead;
-    int64_t f = 0;
-    for (size_t r = 0; r < rows; ++r)
-        for (size_t i = 0; i < cnt; ++i)
-            f += status[(size_t)sh.off[PAIRS] + r * lead + i] != 0;
-    *failures = f;
+    *failures = fails;
     return HHMM_OK;
 }
 
@@ -832,6 +1144,7 @@ hhmm_status hhmm_init(int ndev)
 hhmm_status hhmm_shutdown(void)
 {
     pool_release_all();
+    host_release_all();
     return HHMM_OK;
 }
 

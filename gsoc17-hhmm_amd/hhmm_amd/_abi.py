@@ -57,6 +57,11 @@ def flag_scan_chunk_log2(n):
     """T-chunk length 2^n for the parallel scan (HHMM_FLAG_SCAN_CHUNK_LOG2)."""
     return int(n) << 8
 
+
+def flag_host_chunks(n):
+    """hhmm_run's host pipeline in n chunks (HHMM_FLAG_HOST_CHUNKS; 0 = automatic)."""
+    return (int(n) & 0xFF) << 20
+
 OUT = {
     "loglik": 1 << 0,
     "unalpha_tk": 1 << 1,

@@ -237,6 +237,14 @@ typedef struct hhmm_draws {
 /* Forbids the phased sweep where it is the default (the C2 request then runs
  * fb_kernel beside viterbi_kernel on the library's side stream). */
 #define HHMM_FLAG_VFB_OFF (1u << 19)
+/* hhmm_run only (host arrays): the number of chunks its host pipeline splits a
+ * device's share of the request into (0 = automatic: about 512 MB of staged
+ * traffic per chunk, at least 16384 pairs each).  Chunk i+1's upload and
+ * kernels overlap chunk i's download through pinned staging buffers.  The
+ * pipeline chunks only a request that runs no parallel scan over T (it then
+ * pins SCAN_OFF / VIT_SCAN_OFF on the chunks), so the outputs are those of one
+ * device call on the whole request. */
+#define HHMM_FLAG_HOST_CHUNKS(n) ((uint32_t)((n) & 0xff) << 20)
 
 typedef struct hhmm_request {
     uint32_t abi_version;      /* HHMM_ABI_VERSION */
