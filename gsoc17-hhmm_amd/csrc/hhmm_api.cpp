@@ -20,6 +20,7 @@
 #include <thread>
 #include <vector>
 #include <algorithm>
+#include <emmintrin.h>
 
 #include "hhmm_internal.h"
 #include "build_id.h" /* HHMM_SOURCE_HASH (Makefile) */
@@ -301,6 +302,48 @@ struct ArrayDesc {
         }                                                                                           \
     } while (0)
 
+/* 1 when some element v[n + N t] with t < T[n] (T null: every t < Tm) lies
+ * outside [lo, hi].  Time-major, so each thread streams contiguous rows (the
+ * n-major loop that names the first offender in the error message strides by
+ * N and took ~0.2 s at C2-host's 2e8 symbols); threads over time ranges for
+ * large arrays. */
+static bool any_out_of_range(const int32_t *v, int64_t N, int Tm, const int32_t *T, int32_t lo, int32_t hi)
+{
+    const uint32_t span = (uint32_t)(hi - lo);
+    auto rows = [&](int t0, int t1) {
+        bool bad = false;
+        for (int t = t0; t < t1 && !bad; ++t) {
+            const int32_t *r = v + N * (int64_t)t;
+            if (!T) {
+                uint32_t acc = 0;
+                for (int64_t n = 0; n < N; ++n)
+                    acc |= (uint32_t)((uint32_t)(r[n] - lo) > span);
+                bad = acc != 0;
+            } else {
+                for (int64_t n = 0; n < N; ++n)
+                    bad |= (t < T[n]) & ((uint32_t)(r[n] - lo) > span);
+            }
+        }
+        return bad;
+    };
+    const int64_t total = N * (int64_t)Tm;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int nt = total < (int64_t(1) << 22) ? 1 : (int)std::min<int64_t>(std::min(16u, hw), Tm);
+    if (nt <= 1)
+        return rows(0, Tm);
+    std::vector<char> res((size_t)nt, 0);
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt; ++i)
+        th.emplace_back([&, i]() { res[(size_t)i] = rows((int)((int64_t)Tm * i / nt), (int)((int64_t)Tm * (i + 1) / nt)); });
+    res[0] = rows(0, (int)((int64_t)Tm / nt));
+    for (auto &x : th)
+        x.join();
+    for (char c : res)
+        if (c)
+            return true;
+    return false;
+}
+
 /* o == nullptr: the request side only (the segment summary call has no result). */
 static hhmm_status validate_impl(const hhmm_request *r, const hhmm_result *o, bool host)
 {
@@ -391,19 +434,21 @@ static hhmm_status validate_impl(const hhmm_request *r, const hhmm_result *o, bo
             for (int64_t n = 0; n < N; ++n)
                 REQUIRE(d.T[n] >= 1 && d.T[n] <= Tm, "T[%lld] = %d outside 1..T_max=%d", (long long)n, d.T[n], Tm);
         auto len = [&](int64_t n) { return d.T ? d.T[n] : Tm; };
-        if (is_discrete(m))
+        /* the fast time-major scan first; the n-major loops below only run to
+         * name the first offender when it found one */
+        if (is_discrete(m) && any_out_of_range(d.x_int, N, Tm, d.T, 1, d.L))
             for (int64_t n = 0; n < N; ++n)
                 for (int t = 0; t < len(n); ++t) {
                     const int32_t v = d.x_int[n + N * (int64_t)t];
                     REQUIRE(v >= 1 && v <= d.L, "x[%lld, %d] = %d outside 1..L=%d", (long long)n, t + 1, v, d.L);
                 }
-        if (m == HHMM_MODEL_HMM_MULTINOM_SEMISUP)
+        if (m == HHMM_MODEL_HMM_MULTINOM_SEMISUP && any_out_of_range(d.g, N, Tm, d.T, 1, d.G))
             for (int64_t n = 0; n < N; ++n)
                 for (int t = 0; t < len(n); ++t) {
                     const int32_t v = d.g[n + N * (int64_t)t];
                     REQUIRE(v >= 1 && v <= d.G, "g[%lld, %d] = %d outside 1..G=%d", (long long)n, t + 1, v, d.G);
                 }
-        if (m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE)
+        if ((m == HHMM_MODEL_TAYAL || m == HHMM_MODEL_TAYAL_LITE) && any_out_of_range(d.sign, N, Tm, d.T, 1, 2))
             for (int64_t n = 0; n < N; ++n)
                 for (int t = 0; t < len(n); ++t) {
                     const int32_t v = d.sign[n + N * (int64_t)t];
@@ -710,31 +755,74 @@ static hhmm_status get_pipe_streams(int dev, hipStream_t (&st)[3])
     return HHMM_OK;
 }
 
-/* rows x width bytes between pitched buffers, split over host threads when
- * the copy is large (the staging copies run beside the GPU's DMA) */
-static void par_copy_rows(char *dst, size_t dpitch, const char *src, size_t spitch, size_t width, size_t rows)
+/* One row of a staging copy.  Large rows leave the cache alone: the
+ * destination is written with streaming stores (no read-for-ownership of the
+ * caller's lines, which would double the DRAM traffic of the scatter into R's
+ * arrays), 16 bytes at a time once it is 16-byte aligned. */
+static void copy_row(char *dst, const char *src, size_t n)
 {
-    const size_t total = width * rows;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t nt = total < ((size_t)8 << 20) ? 1 : std::min<size_t>(std::min(8u, hw), std::max<size_t>(rows, 1));
-    auto run = [&](size_t r0, size_t r1) {
-        if (dpitch == width && spitch == width) {
-            memcpy(dst + r0 * width, src + r0 * width, (r1 - r0) * width);
-            return;
-        }
-        for (size_t r = r0; r < r1; ++r)
-            memcpy(dst + r * dpitch, src + r * spitch, width);
-    };
-    if (nt <= 1) {
-        run(0, rows);
+    if (n < 4096) {
+        memcpy(dst, src, n);
         return;
     }
-    std::vector<std::thread> th;
-    for (size_t i = 1; i < nt; ++i)
-        th.emplace_back(run, rows * i / nt, rows * (i + 1) / nt);
-    run(0, rows / nt);
-    for (auto &t : th)
-        t.join();
+    const size_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+    memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    const size_t m = n & ~(size_t)63;
+    for (size_t i = 0; i < m; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(src + i));
+        const __m128i b = _mm_loadu_si128((const __m128i *)(src + i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i *)(src + i + 32));
+        const __m128i d = _mm_loadu_si128((const __m128i *)(src + i + 48));
+        _mm_stream_si128((__m128i *)(dst + i), a);
+        _mm_stream_si128((__m128i *)(dst + i + 16), b);
+        _mm_stream_si128((__m128i *)(dst + i + 32), c);
+        _mm_stream_si128((__m128i *)(dst + i + 48), d);
+    }
+    memcpy(dst + m, src + m, n - m);
+}
+
+/* rows x width bytes between pitched buffers, split over host threads when
+ * the copy is large (the staging copies run beside the GPU's DMA; up to 16
+ * threads, the CPU share of one GPU on an 8-GPU node) */
+static void par_copy_rows(char *dst, size_t dpitch, const char *src, size_t spitch, size_t width, size_t rows)
+{
+    if (rows == 0 || width == 0)
+        return;
+    if (dpitch == width && spitch == width) { /* contiguous: one long row, split in pieces */
+        width *= rows;
+        rows = 1;
+        dpitch = spitch = width;
+    }
+    const size_t total = width * rows;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = total < ((size_t)4 << 20) ? 1 : std::min<size_t>(16u, hw);
+    /* work item i: a range of rows, or of bytes of the single row */
+    auto run = [&](size_t i) {
+        if (rows >= nt) {
+            const size_t r0 = rows * i / nt, r1 = rows * (i + 1) / nt;
+            for (size_t r = r0; r < r1; ++r)
+                copy_row(dst + r * dpitch, src + r * spitch, width);
+        } else {
+            for (size_t r = 0; r < rows; ++r) {
+                const size_t b0 = (width * i / nt) & ~(size_t)63, b1 = i + 1 == nt ? width : (width * (i + 1) / nt) & ~(size_t)63;
+                copy_row(dst + r * dpitch + b0, src + r * spitch + b0, b1 - b0);
+            }
+        }
+        _mm_sfence(); /* this thread's streaming stores, before the join */
+    };
+    if (nt <= 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t i = 1; i < nt; ++i)
+            th.emplace_back(run, i);
+        run(0);
+        for (auto &t : th)
+            t.join();
+    }
 }
 
 /* A chunk: its shard, its sub-request, and where each array sits in the slot. */

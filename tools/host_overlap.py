@@ -67,26 +67,42 @@ def direction(r):
 
 def main():
     d, dst = sys.argv[1], sys.argv[2]
-    ker = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows(d, "*kernel_trace.csv")]
+    krows = rows(d, "*kernel_trace.csv")
+    ker = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in krows]
     cp = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), direction(r)) for r in rows(d, "*memory_copy_trace.csv")]
-    big = [c for c in cp if c[1] - c[0] > 100_000]  # copies over 0.1 ms: the pipeline's chunk DMAs
-    h2d = union([[a, b] for a, b, k in big if k == "h2d"])
-    d2h = union([[a, b] for a, b, k in big if k == "d2h"])
-    kk = union([[a, b] for a, b, n in ker if "vfb" in n or "fb_" in n or "viterbi" in n])
-    allu = union(h2d + d2h + kk)
-    out = {
-        "trace_dir": d,
-        "copies_over_0.1ms": len(big),
-        "h2d_busy_ms": length(h2d) / 1e6,
-        "d2h_busy_ms": length(d2h) / 1e6,
-        "kernel_busy_ms": length(kk) / 1e6,
-        "union_busy_ms": length(allu) / 1e6,
-        "serial_sum_ms": (length(h2d) + length(d2h) + length(kk)) / 1e6,
-        "kernel_under_d2h_ms": length(intersect(kk, d2h)) / 1e6,
-        "h2d_under_d2h_ms": length(intersect(h2d, d2h)) / 1e6,
-        "directions_seen": sorted({c[2] for c in cp}),
-    }
-    out["overlap_saved_ms"] = out["serial_sum_ms"] - out["union_busy_ms"]
+    # uploads: SDMA copies from the pinned slots (memory-copy trace); downloads on
+    # this stack: blit kernels (__amd_rocclr_copyBuffer) writing the pinned slots
+    h2d_all = [[a, b] for a, b, k in cp if k == "h2d" and b - a > 100_000]
+    d2h_all = [[a, b] for a, b, n in ker if "copyBuffer" in n and b - a > 100_000]
+    hk = sorted([[a, b] for a, b, n in ker if "hhmm::" in n])
+    # one window per hhmm_run call: hhmm kernels closer than 40 ms
+    wins = []
+    for a, b in hk:
+        if wins and a - wins[-1][1] < 40_000_000:
+            wins[-1][1] = max(wins[-1][1], b)
+            wins[-1][2] += 1
+        else:
+            wins.append([a, b, 1])
+    per = []
+    for a, b, nk in wins:
+        lo, hi = a - 60_000_000, b + 60_000_000  # the call's first upload and last download
+        clip = lambda iv: [[max(x, lo), min(y, hi)] for x, y in iv if y > lo and x < hi]  # noqa: E731
+        h2d, d2h = union(clip(h2d_all)), union(clip(d2h_all))
+        kk = union([[x, y] for x, y in hk if x >= a and y <= b])
+        allu = union(h2d + d2h + kk)
+        per.append({
+            "hhmm_kernels": nk,
+            "span_ms": (allu[-1][1] - allu[0][0]) / 1e6 if allu else 0.0,
+            "h2d_busy_ms": length(h2d) / 1e6, "d2h_busy_ms": length(d2h) / 1e6, "kernel_busy_ms": length(kk) / 1e6,
+            "union_busy_ms": length(allu) / 1e6,
+            "serial_sum_ms": (length(h2d) + length(d2h) + length(kk)) / 1e6,
+            "kernel_under_d2h_ms": length(intersect(kk, d2h)) / 1e6,
+            "h2d_under_d2h_ms": length(intersect(h2d, d2h)) / 1e6,
+        })
+    out = {"trace_dir": d, "calls": per,
+           "note": "one entry per hhmm_run call (hhmm kernels within 40 ms); downloads are blit kernels "
+                   "(__amd_rocclr_copyBuffer) on this stack, uploads SDMA copies; a serial call shows no "
+                   "kernel or upload time under a download"}
     pathlib.Path(dst).write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out, indent=1))
 
