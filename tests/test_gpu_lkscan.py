@@ -1,6 +1,6 @@
 """GPU: the parallel scan over T at large K (hhmm_lkscan.h; SURVEY.md §8 A16
 at 8 < K <= 32, the verdict's N2) against the oracle -- hmm-multinom with few
-pairs and long series: MFMA chunk products (v_mfma_f64_16x16x4_f64), the
+pairs and long series: MFMA chunk products (v_mfma_f64_4x4x4_f64 blocks), the
 scan over chunks, the chunks' forward-backward sweeps.  Posteriors and the
 log-likelihood within tests/tolerances.py (the products reassociate the
 sums); the Viterbi (sequential, beside it) bit-exact."""
@@ -110,6 +110,19 @@ def test_forced_scan_gauss(engine, oracle, K, T, log2):
     in the chunk products, each chunk's sum of the shifts m_t its log scale, the
     summed t = 1 emission (Q2) in phase 2's initial log scale."""
     data, draws = synth.hmm_gauss(N=2, S=3, T=T, K=K)
+    run_gauss(engine, oracle, data, draws, ["loglik", "alpha_tk", "beta_tk", "ungamma_tk", "gamma_tk"],
+              flags=scan_flags(log2))
+
+
+@pytest.mark.parametrize("K", [9, 23])
+@pytest.mark.parametrize("log2", [5, 6])
+def test_forced_scan_gauss_ragged(engine, oracle, K, log2):
+    """ragged series on the Gaussian large-K scan -- partial last
+    chunks, T = 1, lengths that are not multiples of the chunk, and columns past
+    a pair's own chunk count (their log scale sc_bl never accumulates)."""
+    Ts = [1, 700, 33, 64, 65, 451]
+    data, draws = synth.hmm_gauss(N=len(Ts), S=3, T=max(Ts), K=K)
+    data["T"] = np.array(Ts, dtype=np.int32)
     run_gauss(engine, oracle, data, draws, ["loglik", "alpha_tk", "beta_tk", "ungamma_tk", "gamma_tk"],
               flags=scan_flags(log2))
 

@@ -72,9 +72,14 @@ def main():
     ap.add_argument("--T", type=int, default=1000)
     ap.add_argument("--fb", action="store_true")
     ap.add_argument("--names", default="step")
+    ap.add_argument("--libs", default=None,
+                    help="NAME=path,...: library variants, each timed on every set (default: the in-tree build)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    lib = hhmm_amd.load_library()
+    libs = {"tree": hhmm_amd.load_library()}
+    if a.libs:
+        libs = {kv.split("=", 1)[0]: hhmm_amd.load_library(kv.split("=", 1)[1]) for kv in a.libs.split(",")}
+    lib = next(iter(libs.values()))
     x, draws = bench.make_batch(a.pairs, a.T, 9000, dev)
     import ctypes as C
     from hhmm_amd import _abi
@@ -90,23 +95,27 @@ def main():
         ws = C.c_size_t(0)
         assert lib.hhmm_workspace_size(C.byref(q), C.byref(ws)) == 0
         ws_need = max(ws_need, int(ws.value))
-    sets, runs = [], []
+    sets, runs, tags = [], [], []
     for i in range(a.sets):
         sh = Shared(a.pairs, a.T, ws_need, ORDERS[i % len(ORDERS)], PAD_MB[i % len(PAD_MB)], dev)
         sets.append(sh)
-        runs.append(bench.DeviceRun(lib, x, draws, a.pairs, a.T, dev, share=sh))
+        for ln, lb in libs.items():
+            runs.append(bench.DeviceRun(lb, x, draws, a.pairs, a.T, dev, share=sh))
+            tags.append(f"set{i}/{ln}")
         print(json.dumps({"set": i, "order": ORDERS[i % len(ORDERS)], "pad_mb": PAD_MB[i % len(PAD_MB)],
                           "addresses": sh.addresses()}), flush=True)
     torch.cuda.synchronize()
     names = a.names.split(",") + (["fb"] if a.fb else [])
     s0 = torch.cuda.current_stream()
-    for run in runs:  # warm-up + cross-check: every set computes the same outputs
+    g0 = None
+    for i, run in enumerate(runs):  # warm-up + cross-check: every set and library computes the same outputs
         for nm in names:
             run.launch(nm)
-    torch.cuda.synchronize()
-    g0 = runs[0].out["gamma_tk"][:, :8, :4096].cpu()
-    for i, run in enumerate(runs[1:], 1):
-        assert torch.equal(run.out["gamma_tk"][:, :8, :4096].cpu(), g0), f"set {i} differs"
+        torch.cuda.synchronize()
+        g = (run.out["gamma_tk"][:, :8, :4096].cpu(), run.out["zstar_t"][:8].cpu())
+        if g0 is None:
+            g0 = g
+        assert torch.equal(g[0], g0[0]) and torch.equal(g[1], g0[1]), f"{tags[i]} differs"
     times = {(i, nm): [] for i in range(len(runs)) for nm in names}
     for _ in range(a.rounds):
         for i, run in enumerate(runs):
@@ -118,13 +127,14 @@ def main():
                 e1.record(s0)
                 torch.cuda.synchronize()
                 times[(i, nm)].append(e0.elapsed_time(e1) / a.steps)
-    out = {f"set{i}:{nm}": {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
+    out = {f"{tags[i]}:{nm}": {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
            for (i, nm), t in times.items()}
     print(json.dumps({"probe": "placement", "pairs": a.pairs, "T": a.T, "ms": out}), flush=True)
-    for nm in names:
-        med = [float(np.median(times[(i, nm)])) for i in range(len(runs))]
-        print(json.dumps({"name": nm, "spread_pct": 100.0 * (max(med) - min(med)) / min(med), "medians": med}),
-              flush=True)
+    for ln in libs:
+        for nm in names:
+            med = [float(np.median(times[(i, nm)])) for i in range(len(runs)) if tags[i].endswith("/" + ln)]
+            print(json.dumps({"lib": ln, "name": nm, "spread_pct": 100.0 * (max(med) - min(med)) / min(med),
+                              "mean_ms": float(np.mean(med)), "medians": med}), flush=True)
 
 
 if __name__ == "__main__":
