@@ -150,3 +150,24 @@ def test_multinom_schedules_ragged(engine, oracle, outs, flags):
     bad = _corrupt(bad, "x", 41, 100, -3)
     bad = _corrupt(bad, "x", 299, 149, 12)        # the last pair (the final wave's padded lanes)
     _run(engine, oracle, "hmm-multinom", data, bad, draws, outs, [5, 17, 41, 60, 299], pairing="zip", flags=flags)
+
+
+def test_multinom_check_past_grid_y_limit(engine, oracle):
+    """T_max above 65535 strips of 64 steps (4,194,240) -- the check
+    kernel caps grid.y and loops over strips, so the launch still succeeds and a bad
+    symbol past the cap is found (the long series runs the parallel scan over T)."""
+    T = 4_300_000
+    data, draws = synth.hmm_multinom(N=2, S=1, T=64, K=4, L=9)
+    data = dict(data, x=np.random.default_rng(11).integers(1, 10, size=(2, T)).astype(np.int32))
+    bad = _corrupt(data, "x", 1, 4_250_000, 10)   # in the strips past the cap
+    from devrun import DeviceRequest
+    got = DeviceRequest(engine, "hmm-multinom", bad, draws, ["loglik"])
+    got.run()
+    clean = DeviceRequest(engine, "hmm-multinom", data, draws, ["loglik"])
+    clean.run()
+    assert list(got.status.cpu().numpy()) == [0, INVALID_DATA]
+    assert list(clean.status.cpu().numpy()) == [0, 0]
+    # the clean series' pair is computed as usual (the oracle's 77 s at this T is
+    # spared: the same device path on the clean data is the reference here)
+    assert got.host_pairs("loglik", [0])[0] == clean.host_pairs("loglik", [0])[0]
+    assert np.isfinite(clean.host_pairs("loglik", [0, 1])).all()
