@@ -1484,6 +1484,83 @@ hhmm_status hhmm_selftest_shards(const hhmm_request *req, hhmm_result *res, int 
     return HHMM_OK;
 }
 
+hhmm_status hhmm_selftest_pipeline(const hhmm_request *req, hhmm_result *res, int nshards, int nchunks)
+{
+    hhmm_status s = validate(req, res, true);
+    if (s != HHMM_OK)
+        return s;
+    if (nshards < 1 || nchunks < 1) {
+        set_error("nshards and nchunks must be >= 1");
+        return HHMM_ERR_INVALID_ARGUMENT;
+    }
+    hhmm_request dreq = *req;
+    hhmm_result dres = *res;
+    std::vector<ArrayDesc> arrays;
+    describe(req, res, &dreq, &dres, arrays);
+    const bool ragged = req->data.T != nullptr || req->data.T_oos != nullptr;
+    for (const Shard &sh : make_shards(req, nshards)) {
+        for (const Shard &c : split_shard(req, sh, nchunks)) {
+            const ChunkLayout L = chunk_layout(req, arrays, c, ragged);
+            std::vector<char> slot(L.total, 0);
+            /* the gather, as run_on_device stages it, checked byte for byte
+             * against a row-by-row pack of the same slice */
+            for (size_t i = 0; i < arrays.size(); ++i) {
+                const ArrayDesc &a = arrays[i];
+                if (L.off[i] >= L.in_end)
+                    continue;
+                const ShardRows r = shard_rows(a.host, a, L.sh);
+                par_copy_rows(slot.data() + L.off[i], r.width, r.base, r.pitch, r.width, r.rows);
+                std::vector<char> ref(r.rows * r.width);
+                copy_shard_host(ref.data(), a.host, a, L.sh, true);
+                if (memcmp(ref.data(), slot.data() + L.off[i], ref.size()) != 0) {
+                    set_error("pipeline self-test: the staged slice of an input differs");
+                    return HHMM_ERR_INVALID_ARGUMENT;
+                }
+            }
+            /* the "kernel": every output element + 1, every pair status 1 */
+            for (size_t i = 0; i < arrays.size(); ++i) {
+                const ArrayDesc &a = arrays[i];
+                if (!a.output)
+                    continue;
+                const size_t n = shard_bytes(a, L.sh) / a.esize;
+                for (size_t k = 0; k < n; ++k) {
+                    char *e = slot.data() + L.off[i] + k * a.esize;
+                    if (a.esize == sizeof(double)) {
+                        double v;
+                        memcpy(&v, e, 8);
+                        v += 1.0;
+                        memcpy(e, &v, 8);
+                    } else {
+                        int32_t v;
+                        memcpy(&v, e, 4);
+                        v += 1;
+                        memcpy(e, &v, 4);
+                    }
+                }
+            }
+            for (int64_t q = 0; q < L.P; ++q) {
+                const int32_t one = 1;
+                memcpy(slot.data() + L.status_off + (size_t)q * 4, &one, 4);
+            }
+            /* the scatter of the downloaded region, as run_on_device runs it */
+            const char *down = slot.data() + L.out_begin;
+            for (size_t i = 0; i < arrays.size(); ++i) {
+                const ArrayDesc &a = arrays[i];
+                if (!a.output)
+                    continue;
+                const ShardRows r = shard_rows(a.host, a, L.sh);
+                par_copy_rows(r.base, r.pitch, down + (L.off[i] - L.out_begin), r.width, r.width, r.rows);
+            }
+            if (res->pair_status) {
+                const ArrayDesc sa{res->pair_status, nullptr, (size_t)npairs(req), sizeof(int32_t), true, PAIRS};
+                const ShardRows r = shard_rows(res->pair_status, sa, L.sh);
+                par_copy_rows(r.base, r.pitch, down + (L.status_off - L.out_begin), r.width, r.width, r.rows);
+            }
+        }
+    }
+    return HHMM_OK;
+}
+
 hhmm_status hhmm_selftest_cr_log(const double *in, double *out, int64_t n)
 {
     hhmm_status s = check_device();

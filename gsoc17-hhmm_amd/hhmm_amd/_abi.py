@@ -258,4 +258,6 @@ def declare(lib):
     lib.hhmm_selftest_det_exp.restype = C.c_int
     lib.hhmm_selftest_shards.argtypes = [RP, SP, C.c_int]
     lib.hhmm_selftest_shards.restype = C.c_int
+    lib.hhmm_selftest_pipeline.argtypes = [RP, SP, C.c_int, C.c_int]
+    lib.hhmm_selftest_pipeline.restype = C.c_int
     return lib

@@ -386,6 +386,15 @@ hhmm_status hhmm_selftest_det_exp(const double *in, double *out, int64_t n);
  * host ASan / UBSan by tools/sanitize.sh). */
 hhmm_status hhmm_selftest_shards(const hhmm_request *req, hhmm_result *res, int nshards);
 
+/* Host-only self-test of hhmm_run's host pipeline (no GPU used): every
+ * device shard split into `nchunks` chunks exactly as hhmm_run splits it, each
+ * chunk staged through a host "slot" with the pipeline's own layout and
+ * copies (the gather checked byte for byte against a row-by-row pack), every
+ * output element + 1 and every pair status 1 in the slot, then scattered into
+ * the caller's arrays.  Zero-filled outputs end at 1 iff the chunks cover
+ * every element exactly once. */
+hhmm_status hhmm_selftest_pipeline(const hhmm_request *req, hhmm_result *res, int nshards, int nchunks);
+
 #ifdef __cplusplus
 }
 #endif
