@@ -332,10 +332,18 @@ static bool any_out_of_range(const int32_t *v, int64_t N, int Tm, const int32_t 
     if (nt <= 1)
         return rows(0, Tm);
     std::vector<char> res((size_t)nt, 0);
+    auto part = [&](int i) { res[(size_t)i] = rows((int)((int64_t)Tm * i / nt), (int)((int64_t)Tm * (i + 1) / nt)); };
     std::vector<std::thread> th;
-    for (int i = 1; i < nt; ++i)
-        th.emplace_back([&, i]() { res[(size_t)i] = rows((int)((int64_t)Tm * i / nt), (int)((int64_t)Tm * (i + 1) / nt)); });
-    res[0] = rows(0, (int)((int64_t)Tm / nt));
+    std::vector<int> mine{0};
+    for (int i = 1; i < nt; ++i) {
+        try {
+            th.emplace_back(part, i);
+        } catch (...) { /* no exception crosses the C ABI: this thread takes the share */
+            mine.push_back(i);
+        }
+    }
+    for (int i : mine)
+        part(i);
     for (auto &x : th)
         x.join();
     for (char c : res)
@@ -815,14 +823,23 @@ static void par_copy_rows(char *dst, size_t dpitch, const char *src, size_t spit
     };
     if (nt <= 1) {
         run(0);
-    } else {
-        std::vector<std::thread> th;
-        for (size_t i = 1; i < nt; ++i)
-            th.emplace_back(run, i);
-        run(0);
-        for (auto &t : th)
-            t.join();
+        return;
     }
+    /* a thread that cannot be started leaves its share to this one (no
+     * exception crosses the C ABI) */
+    std::vector<std::thread> th;
+    std::vector<size_t> mine{0};
+    for (size_t i = 1; i < nt; ++i) {
+        try {
+            th.emplace_back(run, i);
+        } catch (...) {
+            mine.push_back(i);
+        }
+    }
+    for (size_t i : mine)
+        run(i);
+    for (auto &t : th)
+        t.join();
 }
 
 /* A chunk: its shard, its sub-request, and where each array sits in the slot. */
@@ -1165,11 +1182,18 @@ static hhmm_status run_sharded(const hhmm_request *req, hhmm_result *res)
             msg[i] = hhmm_last_error(); /* thread-local: carried to the caller's thread */
     };
     std::vector<std::thread> th;
-    for (size_t i = 1; i < shards.size(); ++i)
-        th.emplace_back(work, i);
+    std::vector<size_t> mine{0};
+    for (size_t i = 1; i < shards.size(); ++i) {
+        try {
+            th.emplace_back(work, i);
+        } catch (...) { /* no exception crosses the C ABI: this thread runs that shard too */
+            mine.push_back(i);
+        }
+    }
     int cur = 0;
     (void)hipGetDevice(&cur);
-    work(0);
+    for (size_t i : mine)
+        work(i);
     for (auto &t : th)
         t.join();
     (void)hipSetDevice(cur);
