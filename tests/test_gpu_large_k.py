@@ -61,6 +61,49 @@ def test_large_K_invalid_backpointer(engine, oracle):
     run_both(engine, oracle, "hmm-multinom", data, draws)
 
 
+def twin_states(draws, a, b, rel):
+    """States a and b made twins: the same incoming transitions and emissions,
+    so their deltas are equal at every step, and b's outgoing row is a's times
+    (1 + rel): rel = 0 gives exact ties in the max-plus step, a tiny rel
+    candidates an ulp or two apart (lk_viterbi_kernel's fast step marks both,
+    and the block is replayed in the reference's order)."""
+    A = np.array(draws["A_ij"], dtype=np.float64)
+    A[:, :, a] += 4.0  # make the twins likely winners
+    A[:, :, b] = A[:, :, a]
+    A /= A.sum(axis=2, keepdims=True)
+    A[:, b, :] = A[:, a, :] * (1.0 + rel)
+    draws["A_ij"] = A
+    phi = np.array(draws["phi_k"], dtype=np.float64)
+    phi[:, b, :] = phi[:, a, :]
+    draws["phi_k"] = phi
+
+
+@pytest.mark.parametrize("K", [12, 23, 32])
+@pytest.mark.parametrize("rel", [0.0, 2.0 ** -52, -(2.0 ** -50), 2.0 ** -44, 2.0 ** -40])
+def test_large_K_viterbi_ties(engine, oracle, K, rel):
+    """Exact and near ties between two states' candidates: the Viterbi keeps
+    the reference's first-i-on-ties order bit for bit."""
+    data, draws = synth.hmm_multinom(N=3, S=6, T=300, K=K, L=9)
+    twin_states(draws, 2, K - 3, rel)
+    run_both(engine, oracle, "hmm-multinom", data, draws, pars=["zstar_t", "logp_zstar"])
+
+
+def test_large_K_viterbi_ties_gauss(engine, oracle):
+    data, draws = synth.hmm_gauss(N=2, S=5, T=200, K=17)
+    twin_states_g = dict(draws)
+    A = np.array(draws["A_ij"], dtype=np.float64)
+    A[:, :, 4] += 4.0
+    A[:, :, 9] = A[:, :, 4]
+    A /= A.sum(axis=2, keepdims=True)
+    A[:, 9, :] = A[:, 4, :]
+    twin_states_g["A_ij"] = A
+    for k in ("mu_k", "sigma_k"):
+        v = np.array(draws[k], dtype=np.float64)
+        v[:, 9] = v[:, 4]
+        twin_states_g[k] = v
+    run_both(engine, oracle, "hmm", data, twin_states_g, pars=["zstar_t", "logp_zstar"])
+
+
 @pytest.mark.parametrize("K", [12, 23, 32])
 def test_gamma_only_large_K_ragged(engine, oracle, K):
     """The bench's N1 output set (loglik, gamma, zstar, logp_zstar) runs the
@@ -212,7 +255,8 @@ def test_mfma_grid_fb_near_impossible_runs(engine, oracle, tiny):
 
 
 def test_mfma_grid_fb_disjoint_filters(engine, oracle):
-    """The gamma sum below 2^-960: the reference's normalised-vector formula."""
+    """The gamma sum below kGammaDirect = 2^-240 (hhmm_internal.h): the
+    reference's normalised-vector formula."""
     K = 12
     data, draws = synth.hmm_multinom(N=16, S=2, T=600, K=K, L=9)
     A = np.full((2, K, K), 1e-300)
