@@ -549,6 +549,18 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
                 abuf[u] = grp_renorm_at<G>(fwd(w, es[u]), exb, tc + u, ln.dense);
             }
         }
+        /* gamma-only normaliser: sum_j alpha_t(j) beta_t(j) does not depend on t
+         * (alpha_t = e_t .* A' alpha_{t-1} and beta_{t-1} = A (e_t .* beta_t) give
+         * sum_i alpha_{t-1}(i) beta_{t-1}(i) = sum_j alpha_t(j) beta_t(j)), so
+         * between two renormalisations of the recomputed alpha and of beta --
+         * both at steps t with t % kLRenorm == 0, which the walk crosses only
+         * after step t's gamma -- the group sum of one step serves the next
+         * ones: one five-level sum and one reciprocal per kLRenorm steps instead
+         * of per step.  The walk's own rounding moves the sum by a few ulps per
+         * step (non-negative terms), far inside gamma's 1e-9 tolerance.  Dense
+         * waves renormalise every step and sum every step. */
+        double rsg = 0.0;
+        bool direct = false, fresh = true;
 #pragma unroll
         for (int u = kLChunk - 1; u >= 0; --u) {
             const int t = tc + u;
@@ -561,11 +573,16 @@ __global__ void __launch_bounds__(kBlock) lk_fb_kernel(const DevArgs a)
                  * form); the reference's normalised-vector formula where the
                  * product underflows (group-uniform test) */
                 const double ug = av * be;
-                const double sg = grp_sum<G>(ug);
-                if (sg > kGammaDirect) {
-                    /* times the refined reciprocal (fast_rcp: within an ulp; gamma
-                     * is a tolerance output) instead of an IEEE division */
-                    put(a.gamma, t, ug * fast_rcp(sg));
+                if (fresh || ln.dense || (t + 1) % kLRenorm == 0) { /* group-uniform */
+                    const double sg = grp_sum<G>(ug);
+                    direct = sg > kGammaDirect;
+                    /* the refined reciprocal (fast_rcp: within an ulp; gamma is a
+                     * tolerance output) instead of an IEEE division per step */
+                    rsg = direct ? fast_rcp(sg) : 0.0;
+                    fresh = false;
+                }
+                if (direct) {
+                    put(a.gamma, t, ug * rsg);
                 } else {
                     const double sa = grp_sum<G>(av), sb = grp_sum<G>(be);
                     const double un = (av / sa) * (be / sb);
