@@ -28,8 +28,9 @@
  *                        then the approximate scan: the binade k_c expected at
  *                        each chunk's entry
  *   vs_prod<GRID=true>   exact grid products on k_c's grid, tie flags
- *   vs_prod_tie          chunks with a rounding tie: products for even and
- *                        odd entry values (round-half-even depends on parity)
+ *   vs_prod_tie          chunks with a rounding tie (listed by the grid
+ *                        pass): products for even and odd entry values
+ *                        (round-half-even depends on parity), lane per row
  *   vs_scan1 (wave/pair) the exact scan: delta_c (x) M_c where the checks hold
  *                        (entry max in binade k_c, every finite exit
  *                        value inside the binade), else that chunk decoded
@@ -54,14 +55,18 @@
 namespace hhmm {
 
 constexpr int32_t kVsTie = 1 << 30;     /* vs_k: a grid rounding tie inside the chunk */
-/* Discrete models' tie products run inside the grid pass.  Out of line the
- * grid pass drops from 293 VGPRs and 31k instructions to ~125 VGPRs: the first
- * out-of-line version launched the tie kernel over every (pair, chunk, parity)
- * lane and cost more at C5 than the occupancy gained (14.17 against 13.78 ms,
- * profiles/r02zl_ab_c5.log); a list the tie kernel walks (round 3) measured
- * slower too: 15.21 against 13.52 ms inline, interleaved on one box
- * (profiles/r03j_ab_c5.log).  Gaussian models always use the list (a tie shows
- * up during their pass). */
+/* Tie chunks (round 6).  The grid pass lists every chunk holding a rounding
+ * tie (vs_tl) and vs_prod_tie_kernel forms the chunk's two parity products
+ * with one lane per (parity, row): 2K lanes per chunk.  At C5, 75 of 488,500
+ * chunks hold a tie, but while the tie products ran inline (one lane per chunk,
+ * both parities, the whole K x K product) the grid pass needed 293 VGPRs and
+ * 31k instructions and took 4.3 ms; listed, it needs 143 VGPRs and takes
+ * 1.1 ms, and the row-parallel tie kernel 0.6 ms (C5 8.73 -> 7.71 ms,
+ * profiles/r06t_ab_c5_tie_rows.log).  Earlier list versions kept one lane per
+ * chunk-parity and lost (rounds 2-3, round 6: 9.67 against 8.71 ms): that
+ * lane's 512 steps of the whole product were the critical path.  Leaving tie
+ * chunks to the exact scan's step-by-step decode instead costs 4 ms there
+ * (a tie persists over a whole binade, so one pair holds dozens of them). */
 constexpr int32_t kVsNoGrid = -(1 << 20); /* vs_k: no finite magnitude estimate */
 constexpr int32_t kVsSeq = -(1 << 21);    /* vs_k after the exact scan: the chunk was decoded step by step */
 
@@ -174,30 +179,27 @@ __device__ __forceinline__ double vs_add(double o, const VsTerm &t, double &ap)
     return o + t.r;
 }
 
-/* One parity product of a tie chunk (pi = parity of the entry values), into out. */
+/* Row r of one parity product of a tie chunk (pi = parity of the entry
+ * values), into out.  A row of the max-plus product -- the best path sums from
+ * entry state r -- evolves on its own, so a chunk's 2K rows (two parities, K
+ * entry states) run on 2K lanes: the same operations per row as the whole
+ * product, each row's dependent chain a K-th of its length. */
 template <int MODEL, int K>
-__device__ __forceinline__ void vs_tie_product(const DevArgs &a, const VsLane &v, const PairParams<MODEL, K> &pp,
-                                               const double2 *slab, const SeriesPtrs &sp, double iu, double u,
-                                               double pi, double *out)
+__device__ __forceinline__ void vs_tie_row(const DevArgs &a, const VsLane &v, const PairParams<MODEL, K> &pp,
+                                           const double2 *slab, const SeriesPtrs &sp, double iu, double u, double pi,
+                                           int r, double *out)
 {
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
     VsTerm gA[K][K];
-    bool colTie[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        colTie[j] = false;
+    for (int j = 0; j < K; ++j)
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
+        for (int i = 0; i < K; ++i)
             gA[i][j] = vs_term(pp.A[i][j], iu);
-            colTie[j] = colTie[j] || gA[i][j].tie;
-        }
-    }
-    double M[K][K];
+    double M[K];
 #pragma unroll
-    for (int r = 0; r < K; ++r)
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            M[r][j] = (r == j) ? 0.0 : dev_ninf();
+    for (int j = 0; j < K; ++j)
+        M[j] = (r == j) ? 0.0 : dev_ninf();
     vs_steps<MODEL, VAUX>(sp, v.t0, v.t1, [&](int, const Obs &o) {
         double le[K];
         emit_log<MODEL, K>(pp, slab, a.L, o, le);
@@ -210,51 +212,43 @@ __device__ __forceinline__ void vs_tie_product(const DevArgs &a, const VsLane &v
             if constexpr (ModelTraits<MODEL>::kTayal)
                 on[j] = tayal_pred(o.aux, j);
         }
-        double nm[K][K];
+        double nm[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
+            double best = dev_ninf();
 #pragma unroll
-            for (int r = 0; r < K; ++r) {
-                double best = dev_ninf();
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    double cand;
-                    const bool t2 = on[j] && gA[i][j].tie;
-                    if (!gl[j].tie && !t2) { /* no tie in this term: plain grid arithmetic */
-                        cand = M[r][i] + (ModelTraits<MODEL>::kTayal ? (on[j] ? gl[j].r + gA[i][j].r : gl[j].r)
-                                                                     : gA[i][j].r + gl[j].r);
+            for (int i = 0; i < K; ++i) {
+                double cand;
+                const bool t2 = on[j] && gA[i][j].tie;
+                if (!gl[j].tie && !t2) { /* no tie in this term: plain grid arithmetic */
+                    cand = M[i] + (ModelTraits<MODEL>::kTayal ? (on[j] ? gl[j].r + gA[i][j].r : gl[j].r)
+                                                              : gA[i][j].r + gl[j].r);
+                } else {
+                    double ap = vs_parity(M[i] + pi);
+                    if constexpr (ModelTraits<MODEL>::kTayal) {
+                        cand = vs_add(M[i], gl[j], ap);
+                        if (on[j])
+                            cand = vs_add(cand, gA[i][j], ap);
                     } else {
-                        double ap = vs_parity(M[r][i] + pi);
-                        if constexpr (ModelTraits<MODEL>::kTayal) {
-                            cand = vs_add(M[r][i], gl[j], ap);
-                            if (on[j])
-                                cand = vs_add(cand, gA[i][j], ap);
-                        } else {
-                            cand = vs_add(M[r][i], gA[i][j], ap);
-                            cand = vs_add(cand, gl[j], ap);
-                        }
+                        cand = vs_add(M[i], gA[i][j], ap);
+                        cand = vs_add(cand, gl[j], ap);
                     }
-                    best = fmax(best, cand);
                 }
-                nm[r][j] = best;
+                best = fmax(best, cand);
             }
+            nm[j] = best;
         }
 #pragma unroll
-        for (int r = 0; r < K; ++r)
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                M[r][j] = nm[r][j];
+        for (int j = 0; j < K; ++j)
+            M[j] = nm[j];
     });
 #pragma unroll
-    for (int r = 0; r < K; ++r)
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-            out[vs_mat<K>(a, v.p, v.c) + r * K + j] = M[r][j] * u;
+    for (int j = 0; j < K; ++j)
+        out[vs_mat<K>(a, v.p, v.c) + r * K + j] = M[j] * u;
 }
 
-/* The tie chunks' two parity products, one lane per parity, for the chunks
- * the grid pass flagged (kVsTie): Gaussian emissions (a tie shows up during
- * the pass). */
+/* The tie chunks' parity products for the chunks the grid pass listed
+ * (kVsTie), one lane per (chunk, parity, row): 2K lanes per chunk. */
 constexpr int kVsTieBlocks = 512;
 template <int MODEL, int K>
 __global__ void __launch_bounds__(kBlock) vs_prod_tie_kernel(const DevArgs a)
@@ -262,15 +256,18 @@ __global__ void __launch_bounds__(kBlock) vs_prod_tie_kernel(const DevArgs a)
     constexpr bool VAUX = ModelTraits<MODEL>::kTayal;
     constexpr int KP = (K + 1) / 2;
     HIP_DYNAMIC_SHARED(double2, lds)
-    /* work items (listed tie chunk, parity): items [0, n) even entry values,
-     * [n, 2n) odd ones; a grid of kVsTieBlocks workgroups walks them */
+    /* work items (listed tie chunk q, parity, row): item i = 2K q + K parity + row;
+     * a grid of kVsTieBlocks workgroups walks them */
     const int n = __builtin_amdgcn_readfirstlane(a.vs_tl[0]);
+    const int64_t items = 2 * (int64_t)K * n;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < 2 * (int64_t)n; i0 += stride) {
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < items; i0 += stride) {
     const int64_t i = i0 + threadIdx.x;
-    const bool live = i < 2 * (int64_t)n;
-    const int par = live && i >= n;
-    const int64_t g0 = live ? a.vs_tl[1 + (par ? i - n : i)] : 0;
+    const bool live = i < items;
+    const int64_t q = live ? i / (2 * K) : 0;
+    const int rem = (int)(i - q * 2 * K);
+    const int par = rem / K, row = rem % K;
+    const int64_t g0 = live ? a.vs_tl[1 + q] : 0;
     VsLane v;
     v.p = g0 % a.P;
     v.c = (int)(g0 / a.P);
@@ -290,8 +287,8 @@ __global__ void __launch_bounds__(kBlock) vs_prod_tie_kernel(const DevArgs a)
         if constexpr (ModelTraits<MODEL>::kDiscrete)
             fill_table<K, true>(slab, a, v.d);
         const SeriesPtrs sp = series_ptrs<MODEL, VAUX>(a, v.n);
-        vs_tie_product<MODEL, K>(a, v, pp, slab, sp, ldexp(1.0, 52 - kc), ldexp(1.0, kc - 52), (double)par,
-                                 par ? a.vs_m1 : a.vs_m);
+        vs_tie_row<MODEL, K>(a, v, pp, slab, sp, ldexp(1.0, 52 - kc), ldexp(1.0, kc - 52), (double)par, row,
+                             par ? a.vs_m1 : a.vs_m);
     }
     }
 }
@@ -351,11 +348,8 @@ __global__ void __launch_bounds__(kBlock) vs_prod_kernel(const DevArgs a)
                 const double2 e = slab[(l * KP + kp) * 64];
                 any = any || vs_term(e.x, iu).tie || (2 * kp + 1 < K && vs_term(e.y, iu).tie);
             }
-        if (any) {
-            /* the two parity products, inline */
-            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 0.0, a.vs_m);
-            vs_tie_product<MODEL, K>(a, v, pp, slab, sp, iu, u, 1.0, a.vs_m1);
-            a.vs_k[v.p + a.P * (int64_t)v.c] = (kc >= 0) ? (kc | kVsTie) : kVsNoGrid;
+        if (any) { /* listed: vs_prod_tie_kernel forms its parity products */
+            vs_list_tie(a, v, kc);
             return;
         }
     }
@@ -1415,8 +1409,8 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
         else
             hipLaunchKernelGGL((vs_scan0_kernel<MODEL, K, true>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_prod_kernel<MODEL, K, true>), gc, bc, lds_c, st, a);
-        if (ModelTraits<MODEL>::kGauss) /* the listed tie chunks */
-            hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3(kVsTieBlocks), bc, lds_c, st, a);
+        /* the listed tie chunks */
+        hipLaunchKernelGGL((vs_prod_tie_kernel<MODEL, K>), dim3(kVsTieBlocks), bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_scan1_kernel<MODEL, K>), dim3((unsigned)a.P), b64, lds_s, st, a);
         hipLaunchKernelGGL((vs_replay_kernel<MODEL, K>), gc, bc, lds_c, st, a);
         hipLaunchKernelGGL((vs_stitch_kernel<K>), dim3((unsigned)a.P), b64, 0, st, a);
@@ -1473,7 +1467,10 @@ static hhmm_status launch_vscan(const DevArgs &a, hipStream_t st)
         for (int c = 1; c < a.vs_nc; ++c)
             if (k[(size_t)wq + (size_t)a.P * c] == kVsSeq)
                 fprintf(stderr, " %d", c);
-        fprintf(stderr, "\n");
+        int64_t ties = 0;
+        for (int32_t v : k)
+            ties += v >= 0 && (v & kVsTie);
+        fprintf(stderr, "; tie chunks %lld of %lld\n", (long long)ties, (long long)k.size());
     }
     if (e != hipSuccess) {
         set_error("T-parallel Viterbi launch: %s", hipGetErrorString(e));
