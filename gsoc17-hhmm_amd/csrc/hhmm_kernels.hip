@@ -134,19 +134,20 @@ ScanPlan scan_plan(int model, int K, int Tmax, int64_t P, uint32_t outputs, uint
     /* a batch of under 16384 pairs (256 waves: a quarter of the chip's SIMDs)
      * is latency-bound on its T sequential steps already at T of a few hundred:
      * chunks of 4 C steps (C1, 1000 pairs x T = 500: 0.32 -> 0.10 ms), grown
-     * until about 2M (pair, chunk) lanes.  At C5 (250 pairs x T = 10^6, the
-     * V-scan on the high-priority side stream) that is 128-step chunks: with
-     * the lane-parallel boundary scan (round 4) they measured 9.80 ms against
-     * 10.22 for 256 and 11.08 for 64 (profiles/r04l_ab_c5_rn4_chunks.log);
-     * with the serial boundary walk 256 had been best (11.84 against 12.65 for
-     * 512 and 13.69 for 128, profiles/r03u_ab_c5_chunk.log). */
+     * until about 512k (pair, chunk) lanes.  At C5 (250 pairs x T = 10^6, the
+     * V-scan on the high-priority side stream) that is 512-step chunks: once
+     * the V-scan's tie chunks left its grid pass (round 6) the forward-backward
+     * chain was the longer one, and 512 measured 6.85 / 7.50 ms against 7.96 /
+     * 7.94 for 128, 7.19 for 256, 8.18 for 1024 (two boxes,
+     * profiles/r06w_ab_c5_fb_chunks*.log).  Before it, 128 had been best
+     * (9.80 ms against 10.22 for 256, profiles/r04l_ab_c5_rn4_chunks.log). */
     const bool small = P < 16384 && Tmax >= 256;
     int cl;
     if (log2cl > 0) {
         cl = 1 << log2cl;
     } else if (small) {
         cl = 4 * C;
-        while ((int64_t)P * ((Tmax + cl - 1) / cl) > 2097152 && cl < 65536)
+        while ((int64_t)P * ((Tmax + cl - 1) / cl) > 524288 && cl < 65536)
             cl *= 2;
     } else {
         const int64_t want = (int64_t)Tmax * P / 524288;
